@@ -1,0 +1,223 @@
+/*
+ * vpt_gpu.h — C ABI of the MI355X (gfx950) volumetric path-tracing integrator.
+ *
+ * This is the drop-in boundary for the reference's per-tile integration loop
+ *
+ *     void vpt::run(const WorkerParameters&, const Volume&, const Camera&, TileProvider&,
+ *                   Image<float,4>& film, RandomNumberGenerator rng)
+ *         — reference include/vpt/worker.hpp:11, src/worker.cpp:92-208
+ *
+ * The reference has no FFI or plugin registry: `run` is a plain C++ function called by
+ * `num_workers` std::jthreads (src/main.cpp:63-68).  This header exposes the same work as
+ * an opaque-context C API with plain pointers and sizes.  A (tile, wave) job is keyed by
+ * its job id `jid` exactly as TileProvider::next() assigns it (src/tile_provider.cpp:27-31):
+ *     tile = jid % T,  wave = 1 + jid / T,  T = ceil(W/tw) * ceil(H/th)
+ * and its random stream is pcg32_fast seeded with hash(seed, jid) (include/vpt/random.hpp:93-95),
+ * so any partition of the jid space (threads, launches, GPUs) renders the same samples.
+ *
+ * Every function returns VPT_OK (0) or an error code; vpt_last_error() gives the message
+ * (thread-local).  The reference's fatal paths (`vptFATAL` = exit(1), include/vpt/logging.hpp:16)
+ * become error returns here.
+ *
+ * INTEGRATION.md shows the reference-side binding (a `run_gpu` with run()'s signature).
+ */
+#ifndef VPT_GPU_H
+#define VPT_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VPT_ABI_VERSION 1
+
+enum {
+  VPT_OK = 0,
+  VPT_E_INVALID = 1,  /* bad argument / schema violation */
+  VPT_E_HIP = 2,      /* HIP runtime failure or no HIP device */
+  VPT_E_IO = 3,       /* file could not be read */
+  VPT_E_PARSE = 4,    /* JSON syntax error, missing or unknown key */
+  VPT_E_NOMEM = 5,
+  VPT_E_STATE = 6     /* call not valid in the context's current state */
+};
+
+/* ---- scene configuration: include/vpt/configuration.hpp:14-65 ------------------------- */
+
+/* CameraParameters, configuration.hpp:20-27 */
+typedef struct vpt_camera_params {
+  float position[3];
+  float look[3];
+  float up[3];
+  float vfov_deg;
+  float imaging_ratio;
+} vpt_camera_params;
+
+/* WorkerParameters, configuration.hpp:40-50 (image_point_t = Eigen::Index pair) */
+typedef struct vpt_worker_params {
+  int32_t single_pixel_enabled;
+  int32_t use_jitter;
+  int64_t single_pixel_coord[2]; /* (x, y) */
+  float infinite_light_xyz[3];
+  float infinite_light_multiplier;
+  float distant_light_xyz[3];
+  float distant_light_multiplier;
+  float distant_light_inv_direction[3];
+  uint32_t max_depth;
+} vpt_worker_params;
+
+/* VolumeParameters, configuration.hpp:52-59 */
+typedef struct vpt_volume_params {
+  float henyey_greenstein_g;
+  float le_scale;
+  float sigma_a;
+  float sigma_s;
+  float temperature_offset;
+  float temperature_scale;
+} vpt_volume_params;
+
+/* Configuration, configuration.hpp:61-71 */
+typedef struct vpt_configuration {
+  uint32_t seed;
+  uint32_t num_waves;
+  uint32_t num_workers;
+  uint32_t _pad0;
+  int64_t output_size[2]; /* (w, h) */
+  int64_t tile_size[2];   /* (w, h) */
+  vpt_camera_params camera_parameters;
+  vpt_worker_params worker_parameters;
+  vpt_volume_params volume_parameters;
+  char volume_path[4096]; /* as written in the JSON (relative to the config's directory) */
+} vpt_configuration;
+
+/* read_configuration (src/configuration.cpp:8-22): strict JSON reader for exactly this schema;
+ * a missing key (glaze error_on_missing_keys) or an unknown key is VPT_E_PARSE. */
+int vpt_config_read(const char* path, vpt_configuration* out);
+int vpt_config_parse(const char* json_text, size_t len, vpt_configuration* out);
+
+/* ---- grids: include/vpt/volume_grids.hpp:12-14 (nanovdb::NanoGrid<float>) -------------- */
+
+/* A NanoVDB float grid flattened to plain arrays.  Node semantics are NanoVDB's:
+ * leaves 8^3, lower nodes 16^3 leaves (128^3 voxels), upper nodes 32^3 lower nodes
+ * (4096^3 voxels), root tiles keyed by 4096-aligned origin.  Node existence is implied:
+ * a lower node exists if it holds a leaf or a level-1 tile (or is listed in lower_origin),
+ * an upper node exists if it holds a lower node or a level-2 tile (or is listed).
+ * Slots not covered by a child or a listed tile hold (background, inactive). */
+typedef struct vpt_grid_desc {
+  float map_mat[9];      /* nanovdb::Map::mMatF    (index->world, row-major) */
+  float map_inv_mat[9];  /* nanovdb::Map::mInvMatF (world->index, row-major) */
+  float map_vec[3];      /* nanovdb::Map::mVecF    (translation)             */
+  float background;
+  int32_t index_bbox_min[3]; /* Grid::indexBBox(), inclusive (volume.cpp:83) */
+  int32_t index_bbox_max[3];
+  uint64_t leaf_count;
+  const int32_t* leaf_origin;      /* [leaf_count][3], multiples of 8                      */
+  const float* leaf_values;        /* [leaf_count][512], n = (x&7)<<6 | (y&7)<<3 | (z&7)    */
+  const uint64_t* leaf_value_mask; /* [leaf_count][8] active-voxel bits (NanoVDB Mask<3>)  */
+  const float* leaf_max;           /* [leaf_count] LeafNode::getMax() as stored            */
+  uint64_t tile_count;
+  const int32_t* tile_origin; /* [tile_count][3]                                                    */
+  const int32_t* tile_level;  /* 1: lower-node tile (8^3), 2: upper-node tile (128^3), 3: root tile */
+  const float* tile_value;
+  const uint8_t* tile_active;
+  uint64_t lower_count;       /* optional extra internal nodes that hold no leaf (may be 0)  */
+  const int32_t* lower_origin;
+  uint64_t upper_count;
+  const int32_t* upper_origin;
+} vpt_grid_desc;
+
+/* fix_majorants_for_interpolation(grid, order=1) (src/volume.cpp:104-160), host side:
+ * out_leaf_max[i] = max(desc.leaf_max[i], getValue(c) for c in the 26 neighbour leaf boxes
+ * intersected with leaf i's bbox expanded by 1).  Idempotent.  Uses up to num_threads threads. */
+int vpt_fix_majorants(const vpt_grid_desc* grid, float* out_leaf_max, int num_threads);
+
+/* ---- blackbody emission: src/precompute_blackbody.cpp:7-52, src/spectral.cpp:7-20 ------- */
+
+#define VPT_BLACKBODY_ROWS 500
+/* init_blackbody_radiation_xyz(): bb_xyz[i] = spectrum_to_xyz(planck(T = (i-1)*100 K)),
+ * written as [500][3] floats, from the CIE 1931 table shipped with the package. */
+int vpt_blackbody_table(float* out_500x3);
+/* blackbody_radiation_xyz(T) on the host, for tests. */
+int vpt_blackbody_xyz(const float* table_500x3, float temperature_k, float* out_xyz);
+
+/* ---- the integrator ---------------------------------------------------------------------- */
+
+typedef struct vpt_gpu_ctx vpt_gpu_ctx;
+
+/* Event counters accumulated by every launch (for algorithmic bytes). */
+typedef struct vpt_counters {
+  uint64_t samples;        /* film samples written (pixels traced)                     */
+  uint64_t dda_steps;      /* HDDA steps taken (volume.cpp:56)                          */
+  uint64_t segments;       /* majorant segments returned by RayMajorantIterator::next   */
+  uint64_t draws;          /* exponential free-flight draws (sampler.cpp:44)            */
+  uint64_t stencils;       /* density trilinear stencil refreshes (cell changes)        */
+  uint64_t density_evals;  /* density trilinear evaluations                             */
+  uint64_t temp_stencils;  /* temperature trilinear stencil refreshes                   */
+  uint64_t scatters;       /* scatter events                                            */
+  uint64_t shadow_rays;    /* sample_Ld calls that traced a ray                         */
+  uint64_t rng_draws;      /* uniform<float>() calls                                    */
+} vpt_counters;
+
+/* Create a context on HIP device `device`.  Copies everything it needs (the grids are
+ * flattened into an HBM brick pool + leaf-slot/majorant tables; the caller's arrays may be
+ * freed afterwards).  `density` is required (volume_grids.cpp:58-60); `temperature` may be
+ * NULL (volume_grids.cpp:61-66).  `blackbody_500x3` may be NULL: the table is then computed
+ * with vpt_blackbody_table().  The density grid's leaf maxima are fixed for interpolation
+ * here (Volume::Volume, volume.cpp:162-170) — passing already-fixed maxima is harmless. */
+int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density,
+                   const vpt_grid_desc* temperature, const float* blackbody_500x3, int device,
+                   vpt_gpu_ctx** out);
+int vpt_gpu_destroy(vpt_gpu_ctx* ctx);
+
+/* Jobs per wave T and total jobs num_waves*T of the context's configuration. */
+int vpt_gpu_job_space(const vpt_gpu_ctx* ctx, uint64_t* jobs_per_wave, uint64_t* total_jobs);
+
+/* Render jobs [jid_begin, jid_begin + jid_count) asynchronously on `hip_stream`
+ * (a hipStream_t; NULL = the context's own stream), accumulating into `film_device`:
+ * a device float[H][W][4] (X, Y, Z, sample count; image.hpp:40-60) — NULL = the context's own
+ * film.  Film adds are fp32 atomics, so the per-pixel sum order may differ from the
+ * reference's wave order (≈1e-7 relative). */
+int vpt_gpu_render_jobs(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count,
+                        float* film_device, void* hip_stream);
+
+/* Like vpt_gpu_render_jobs but also writes every sample's radiance L (before the
+ * imaging_ratio scale) to records_device[(jid - jid_begin) * tile_w*tile_h + y_local*rect_w + x_local][3]
+ * — a debug path for bit-exact per-sample parity. */
+int vpt_gpu_render_jobs_records(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count,
+                                float* film_device, float* records_device, void* hip_stream);
+
+int vpt_gpu_sync(vpt_gpu_ctx* ctx);
+/* Zero the context's own film. */
+int vpt_gpu_film_clear(vpt_gpu_ctx* ctx);
+/* Device pointer of the context's own film (for an RCCL reduce), and its element count H*W*4. */
+int vpt_gpu_film_device_ptr(vpt_gpu_ctx* ctx, float** film_device, uint64_t* count);
+/* film_host[i] += own film[i] (synchronous), the caller-owned reference-layout film. */
+int vpt_gpu_film_add_to_host(vpt_gpu_ctx* ctx, float* film_host_hxwx4);
+/* Counters summed over every launch since creation (or the last reset). */
+int vpt_gpu_counters(vpt_gpu_ctx* ctx, vpt_counters* out, int reset);
+/* Launch geometry used by the integrator kernel (for reports). */
+int vpt_gpu_launch_info(const vpt_gpu_ctx* ctx, int* grid_blocks, int* block_threads);
+
+/* ---- synthetic stand-in volumes (the reference's .nvdb files are not available) ---------- */
+
+/* kind 0: constant density 1.0 over index [0,n)^3 (n = 128)
+ * kind 1: procedural cloud density over [0,n)^3 (C3, n = 512):
+ *         p = (ijk + 0.5)/(n/2) - 1, base = clamp((0.85 - |p|)/0.35, 0, 1),
+ *         density = base * (0.5 + 0.5 sin(11px+2) sin(13py+1) sin(17pz+3))  (double, then float)
+ * kind 2: temperature 40*base on the same lattice (C4)
+ * world = index - n/2; leaves with no non-zero voxel are omitted; non-zero voxels are active;
+ * indexBBox = bbox of active voxels; leaf_max = max over active voxels.  NULL on bad arguments.
+ * The returned desc owns its arrays: release it with vpt_synth_free. */
+vpt_grid_desc* vpt_synth_grid(int kind, int n);
+void vpt_synth_free(vpt_grid_desc* desc);
+
+/* Thread-local message for the last non-OK return. */
+const char* vpt_last_error(void);
+int vpt_abi_version(void);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* VPT_GPU_H */

@@ -1,0 +1,146 @@
+// hostsim.cpp — TEST HARNESS: runs the device integrator state machine (vpt_integrator.h)
+// serially on the CPU so that its control flow and float semantics can be checked bit-for-bit
+// against the oracle without a GPU.  Not part of the product library; the product path is the
+// HIP kernel in volume_path_tracer_amd/csrc/vpt_gpu.hip.
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../volume_path_tracer_amd/csrc/vpt_internal.h"
+
+namespace vpt {
+static thread_local std::string g_err;
+int set_error(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+}  // namespace vpt
+
+namespace {
+struct HostEnv {
+  uint64_t jid_begin, jid_count, next = 0;
+  float* film;
+  float* records;
+  int32_t tile_area;
+  bool fetch_job(uint64_t& j) {
+    if (next >= jid_count) return false;
+    j = next++;
+    return true;
+  }
+  void film_add(const vpt::DevScene& S, const vpt::Lane& ln) {
+    float* f = film + ((int64_t)ln.py * S.W + ln.px) * 4;
+    f[3] += 1.0f;
+    f[0] += S.imaging_ratio * ln.L[0];
+    f[1] += S.imaging_ratio * ln.L[1];
+    f[2] += S.imaging_ratio * ln.L[2];
+    if (records) {
+      int32_t xl = ln.px - ln.x0, yl = ln.py - ln.y0;
+      float* r = records + (ln.jid_local * (uint64_t)tile_area + (uint64_t)(yl * ln.rw + xl)) * 3;
+      r[0] = ln.L[0];
+      r[1] = ln.L[1];
+      r[2] = ln.L[2];
+    }
+  }
+};
+}  // namespace
+
+extern "C" int vpths_render_jobs(const vpt_configuration* cfg, const vpt_grid_desc* density,
+                                 const vpt_grid_desc* temperature, const float* bb500, uint64_t jid_begin,
+                                 uint64_t jid_count, float* film, float* records, vpt_counters* counters) {
+  vpt::DevScene S;
+  int rc = vpt::build_scene(*cfg, S);
+  if (rc) return rc;
+  vpt::HostGrid hd, ht;
+  if ((rc = vpt::build_host_grid(*density, true, 0, hd))) return rc;
+  S.density = hd.dev;
+  if (temperature) {
+    if ((rc = vpt::build_host_grid(*temperature, false, 0, ht))) return rc;
+    S.temperature = ht.dev;
+    S.has_temperature = 1;
+  }
+  std::vector<float> bb(501 * 3, 0.0f);
+  if (bb500)
+    std::memcpy(bb.data(), bb500, 500 * 3 * sizeof(float));
+  else
+    vpt::blackbody_table(bb.data());
+  S.bb = bb.data();
+  S.cie = vpt::cie_table();
+  HostEnv env{jid_begin, jid_count, 0, film, records, S.tw * S.th};
+  vpt::Lane ln;
+  std::memset(&ln, 0, sizeof ln);
+  ln.state = vpt::ST_FETCH;
+  while (ln.state != vpt::ST_DONE) vpt::lane_iteration(S, ln, env);
+  if (counters) {
+    counters->samples += ln.cnt.samples;
+    counters->dda_steps += ln.cnt.dda_steps;
+    counters->segments += ln.cnt.segments;
+    counters->draws += ln.cnt.draws;
+    counters->stencils += ln.cnt.stencils;
+    counters->density_evals += ln.cnt.density_evals;
+    counters->temp_stencils += ln.cnt.temp_stencils;
+    counters->scatters += ln.cnt.scatters;
+    counters->shadow_rays += ln.cnt.shadow_rays;
+    counters->rng_draws += ln.cnt.rng_draws;
+  }
+  return 0;
+}
+
+// Leaf majorants after fix_majorants (product builder), for comparison with the oracle.
+extern "C" int vpths_fixed_leaf_max(const vpt_grid_desc* d, float* out) {
+  vpt::HostGrid h;
+  int rc = vpt::build_host_grid(*d, true, 0, h);
+  if (rc) return rc;
+  std::memcpy(out, h.leaf_max.data(), h.leaf_max.size() * sizeof(float));
+  return 0;
+}
+
+// getValue / max(8,getDim) / majorant through the product's flattened tables.
+extern "C" int vpths_probe(const vpt_grid_desc* d, const int32_t* ijk, int n, float* value, int32_t* dim, float* maj) {
+  vpt::HostGrid h;
+  int rc = vpt::build_host_grid(*d, true, 0, h);
+  if (rc) return rc;
+  for (int q = 0; q < n; ++q) {
+    vpt::Cell c = vpt::cell_at(h.dev, ijk[3 * q], ijk[3 * q + 1], ijk[3 * q + 2]);
+    value[q] = vpt::value_at(h.dev, ijk[3 * q], ijk[3 * q + 1], ijk[3 * q + 2]);
+    dim[q] = vpt::hdda_dim_of(c);
+    maj[q] = vpt::majorant_of(c);
+  }
+  return 0;
+}
+
+// The math clones vs glibc, over every input the integrator can produce.
+#include <cmath>
+extern "C" int64_t vpths_math_mismatches(int which) {
+  int64_t bad = 0;
+  for (uint32_t b = 0;; ++b) {
+    float fr;
+    std::memcpy(&fr, &b, 4);
+    if (fr > 4294967296.0f) break;
+    if (fr != std::floor(fr)) continue;
+    float u = fr * 0x1p-32f;
+    if (!(u < 0x1.fffffep-1f)) u = 0x1.fffffep-1f;
+    if (which == 0) {
+      float x = 1.0f - u;
+      if (vpt::math::as_u32(vpt::math::logf_glibc(x)) != vpt::math::as_u32(std::log(x))) ++bad;
+    } else {
+      float phi = 2.0f * 3.14159274f * u;
+      if (which == 1 && vpt::math::as_u32(vpt::math::sinf_glibc(phi)) != vpt::math::as_u32(std::sin(phi))) ++bad;
+      if (which == 2 && vpt::math::as_u32(vpt::math::cosf_glibc(phi)) != vpt::math::as_u32(std::cos(phi))) ++bad;
+    }
+  }
+  return bad;
+}
+
+// powf(x, 2.0f) == x * x for every finite float (the device squares instead of calling pow).
+extern "C" int64_t vpths_pow2_mismatches(void) {
+  int64_t bad = 0;
+  for (uint64_t b = 0; b < (1ULL << 32); b += 1) {
+    uint32_t u = (uint32_t)b;
+    float x;
+    std::memcpy(&x, &u, 4);
+    if (!std::isfinite(x)) continue;
+    float p = std::pow(x, 2.0f), q = x * x;
+    if (vpt::math::as_u32(p) != vpt::math::as_u32(q)) ++bad;
+  }
+  return bad;
+}

@@ -1,0 +1,14 @@
+"""volume_path_tracer_amd — MI355X (gfx950) drop-in for the volume_path_tracer per-tile integrator.
+
+Layers:
+  include/vpt_gpu.h        C ABI (the drop-in boundary for vpt::run, src/worker.cpp:92-208)
+  csrc/vpt_integrator.h    the device state machine (delta tracking, HDDA, NEE, blackbody)
+  csrc/vpt_gpu.hip         persistent HIP kernel + context
+  csrc/vpt_grid_build.cpp  NanoVDB-style grid -> HBM leaf-slot tables + 9^3 apron brick pool
+  csrc/vpt_config.cpp      strict scene-JSON reader (read_configuration)
+  capi.py / scenes.py      ctypes mirror of the ABI, scene presets
+  render.py                host driver: TileProvider-compatible job enumeration, multi-GPU sharding
+"""
+from . import capi  # noqa: F401
+
+__all__ = ["capi"]

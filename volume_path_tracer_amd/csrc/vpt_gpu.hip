@@ -1,0 +1,331 @@
+// vpt_gpu.hip — the MI355X (gfx950) integrator kernel and the C ABI around it.
+//
+// Kernel shape: a persistent grid sized to the device's resident capacity.  Every lane runs the
+// state machine of vpt_integrator.h; when its (tile, wave) job ends it takes the next job id from
+// a device counter (one returning atomic per job; the compiler merges a wavefront's simultaneous
+// fetches into one atomic), so lanes are refilled until the job range is drained and every wave
+// reaches ST_DONE.  Film accumulation uses no-return fp32 atomics into the [H][W][4] XYZW film.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "vpt_internal.h"
+
+namespace vpt {
+
+static thread_local std::string g_last_error;
+
+int set_error(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define VPT_HIP(call)                                                                                 \
+  do {                                                                                                \
+    hipError_t e_ = (call);                                                                           \
+    if (e_ != hipSuccess)                                                                             \
+      return ::vpt::set_error(VPT_E_HIP, std::string(#call " failed: ") + hipGetErrorString(e_));            \
+  } while (0)
+
+constexpr int kCounterCount = 10;
+constexpr int kBlockThreads = 256;
+
+struct KernelEnv {
+  uint64_t jid_begin;
+  uint64_t jid_count;
+  unsigned long long* job_counter;
+  float* film;
+  float* records;
+  int32_t tile_area;
+
+  __device__ __forceinline__ bool fetch_job(uint64_t& j) {
+    unsigned long long v = atomicAdd(job_counter, 1ULL);
+    if (v >= jid_count) return false;
+    j = v;
+    return true;
+  }
+  __device__ __forceinline__ void film_add(const DevScene& S, const Lane& ln) {
+    float* f = film + ((int64_t)ln.py * S.W + ln.px) * 4;
+    const float r = S.imaging_ratio;
+    atomicAdd(f + 3, 1.0f);
+    atomicAdd(f + 0, r * ln.L[0]);
+    atomicAdd(f + 1, r * ln.L[1]);
+    atomicAdd(f + 2, r * ln.L[2]);
+    if (records) {
+      const int32_t xl = ln.px - ln.x0, yl = ln.py - ln.y0;
+      float* rec = records + (ln.jid_local * (uint64_t)tile_area + (uint64_t)(yl * ln.rw + xl)) * 3;
+      rec[0] = ln.L[0];
+      rec[1] = ln.L[1];
+      rec[2] = ln.L[2];
+    }
+  }
+};
+
+__global__ __launch_bounds__(kBlockThreads) void vpt_integrate_kernel(DevScene S, KernelEnv env,
+                                                                       unsigned long long* counters) {
+  Lane ln;
+  ln.state = ST_FETCH;
+  ln.sm = SM_NEED_SEG;
+  ln.dens.valid = 0;
+  ln.temp.valid = 0;
+  ln.cnt = LaneCounters{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  while (ln.state != ST_DONE) lane_iteration(S, ln, env);
+  const uint32_t c[kCounterCount] = {ln.cnt.samples, ln.cnt.dda_steps, ln.cnt.segments, ln.cnt.draws,
+                                     ln.cnt.stencils, ln.cnt.density_evals, ln.cnt.temp_stencils,
+                                     ln.cnt.scatters, ln.cnt.shadow_rays, ln.cnt.rng_draws};
+  for (int i = 0; i < kCounterCount; ++i)
+    if (c[i]) atomicAdd(counters + i, (unsigned long long)c[i]);
+}
+
+// ------------------------------------------------------------------------------------------------
+struct DeviceGrid {
+  void* cells8 = nullptr;
+  void* cells128 = nullptr;
+  void* root = nullptr;
+  void* bricks = nullptr;
+  DevGrid dev{};
+  size_t bytes = 0;
+};
+
+static int upload(const void* src, size_t n, void** dst, size_t& bytes) {
+  *dst = nullptr;
+  if (n == 0) return VPT_OK;
+  VPT_HIP(hipMalloc(dst, n));
+  VPT_HIP(hipMemcpy(*dst, src, n, hipMemcpyHostToDevice));
+  bytes += n;
+  return VPT_OK;
+}
+
+static int upload_grid(const HostGrid& h, DeviceGrid& d) {
+  d.dev = h.dev;
+  int rc;
+  if ((rc = upload(h.cells8.data(), h.cells8.size() * sizeof(int2), &d.cells8, d.bytes))) return rc;
+  if ((rc = upload(h.cells128.data(), h.cells128.size() * sizeof(int2), &d.cells128, d.bytes))) return rc;
+  if ((rc = upload(h.root.data(), h.root.size() * sizeof(RootTileDev), &d.root, d.bytes))) return rc;
+  if ((rc = upload(h.bricks.data(), h.bricks.size() * sizeof(float), &d.bricks, d.bytes))) return rc;
+  d.dev.cells8 = (const int2*)d.cells8;
+  d.dev.cells128 = (const int2*)d.cells128;
+  d.dev.root = (const RootTileDev*)d.root;
+  d.dev.bricks = (const float*)d.bricks;
+  return VPT_OK;
+}
+
+static void free_grid(DeviceGrid& d) {
+  (void)hipFree(d.cells8);
+  (void)hipFree(d.cells128);
+  (void)hipFree(d.root);
+  (void)hipFree(d.bricks);
+  d = DeviceGrid{};
+}
+
+}  // namespace vpt
+
+struct vpt_gpu_ctx {
+  int device = 0;
+  vpt_configuration cfg{};
+  vpt::DevScene scene{};
+  vpt::DeviceGrid density, temperature;
+  float* bb = nullptr;
+  float* cie = nullptr;
+  float* film = nullptr;
+  uint64_t film_count = 0;
+  unsigned long long* job_counter = nullptr;
+  unsigned long long* counters = nullptr;
+  hipStream_t stream = nullptr;
+  int grid_blocks = 0;
+};
+
+namespace {
+
+int ctx_device(vpt_gpu_ctx* ctx) {
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return vpt::set_error(VPT_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  return VPT_OK;
+}
+
+void destroy(vpt_gpu_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  vpt::free_grid(ctx->density);
+  vpt::free_grid(ctx->temperature);
+  (void)hipFree(ctx->bb);
+  (void)hipFree(ctx->cie);
+  (void)hipFree(ctx->film);
+  (void)hipFree(ctx->job_counter);
+  (void)hipFree(ctx->counters);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film, float* records, void* stream_ptr) {
+  if (!ctx) return vpt::set_error(VPT_E_INVALID, "render: null context");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  if (jid_count == 0) return VPT_OK;
+  const uint64_t total = ctx->scene.T * (uint64_t)ctx->cfg.num_waves;
+  (void)total;  // jids beyond num_waves are valid jobs too (TileProvider only stops at requested_waves)
+  hipStream_t s = stream_ptr ? (hipStream_t)stream_ptr : ctx->stream;
+  vpt::KernelEnv env;
+  env.jid_begin = jid_begin;
+  env.jid_count = jid_count;
+  env.job_counter = ctx->job_counter;
+  env.film = film ? film : ctx->film;
+  env.records = records;
+  env.tile_area = ctx->scene.tw * ctx->scene.th;
+  VPT_HIP(hipMemsetAsync(ctx->job_counter, 0, sizeof(unsigned long long), s));
+  hipLaunchKernelGGL(vpt::vpt_integrate_kernel, dim3(ctx->grid_blocks), dim3(vpt::kBlockThreads), 0, s, ctx->scene,
+                     env, ctx->counters);
+  VPT_HIP(hipGetLastError());
+  return VPT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* vpt_last_error(void) { return vpt::g_last_error.c_str(); }
+int vpt_abi_version(void) { return VPT_ABI_VERSION; }
+
+int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, const vpt_grid_desc* temperature,
+                   const float* blackbody_500x3, int device, vpt_gpu_ctx** out) {
+  if (!cfg || !density || !out) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_create: null argument");
+  *out = nullptr;
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev <= 0)
+    return vpt::set_error(VPT_E_HIP, "vpt_gpu_create: no HIP device (the integrator has no CPU fallback)");
+  if (device < 0 || device >= ndev) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_create: bad device index");
+  std::unique_ptr<vpt_gpu_ctx, void (*)(vpt_gpu_ctx*)> ctx(new vpt_gpu_ctx(), destroy);
+  ctx->device = device;
+  ctx->cfg = *cfg;
+  int rc = ctx_device(ctx.get());
+  if (rc) return rc;
+  if ((rc = vpt::build_scene(*cfg, ctx->scene))) return rc;
+
+  // Volume::Volume: fix the density majorants (volume.cpp:162-170); temperature is only sampled.
+  {
+    vpt::HostGrid h;
+    if ((rc = vpt::build_host_grid(*density, true, 0, h))) return rc;
+    if ((rc = vpt::upload_grid(h, ctx->density))) return rc;
+  }
+  if (temperature) {
+    vpt::HostGrid h;
+    if ((rc = vpt::build_host_grid(*temperature, false, 0, h))) return rc;
+    if ((rc = vpt::upload_grid(h, ctx->temperature))) return rc;
+  }
+  ctx->scene.density = ctx->density.dev;
+  ctx->scene.temperature = ctx->temperature.dev;
+  ctx->scene.has_temperature = temperature ? 1 : 0;
+
+  std::vector<float> bb(501 * 3, 0.0f);  // row 500 = 0 (reference reads past its table)
+  if (blackbody_500x3)
+    std::memcpy(bb.data(), blackbody_500x3, 500 * 3 * sizeof(float));
+  else
+    vpt::blackbody_table(bb.data());
+  size_t scratch = 0;
+  if ((rc = vpt::upload(bb.data(), bb.size() * sizeof(float), (void**)&ctx->bb, scratch))) return rc;
+  if ((rc = vpt::upload(vpt::cie_table(), 471 * 3 * sizeof(float), (void**)&ctx->cie, scratch))) return rc;
+  ctx->scene.bb = ctx->bb;
+  ctx->scene.cie = ctx->cie;
+
+  ctx->film_count = (uint64_t)cfg->output_size[0] * (uint64_t)cfg->output_size[1] * 4;
+  VPT_HIP(hipMalloc((void**)&ctx->film, ctx->film_count * sizeof(float)));
+  VPT_HIP(hipMemset(ctx->film, 0, ctx->film_count * sizeof(float)));
+  VPT_HIP(hipMalloc((void**)&ctx->job_counter, sizeof(unsigned long long)));
+  VPT_HIP(hipMalloc((void**)&ctx->counters, vpt::kCounterCount * sizeof(unsigned long long)));
+  VPT_HIP(hipMemset(ctx->counters, 0, vpt::kCounterCount * sizeof(unsigned long long)));
+  VPT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+
+  // Persistent grid: as many blocks as are resident at once.
+  int per_cu = 0, cus = 0;
+  VPT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, vpt::vpt_integrate_kernel, vpt::kBlockThreads, 0));
+  VPT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+  if (per_cu < 1) per_cu = 1;
+  ctx->grid_blocks = per_cu * cus;
+  *out = ctx.release();
+  return VPT_OK;
+}
+
+int vpt_gpu_destroy(vpt_gpu_ctx* ctx) {
+  destroy(ctx);
+  return VPT_OK;
+}
+
+int vpt_gpu_job_space(const vpt_gpu_ctx* ctx, uint64_t* jobs_per_wave, uint64_t* total_jobs) {
+  if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
+  if (jobs_per_wave) *jobs_per_wave = ctx->scene.T;
+  if (total_jobs) *total_jobs = ctx->scene.T * (uint64_t)ctx->cfg.num_waves;
+  return VPT_OK;
+}
+
+int vpt_gpu_render_jobs(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film_device,
+                        void* hip_stream) {
+  return render(ctx, jid_begin, jid_count, film_device, nullptr, hip_stream);
+}
+
+int vpt_gpu_render_jobs_records(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film_device,
+                                float* records_device, void* hip_stream) {
+  return render(ctx, jid_begin, jid_count, film_device, records_device, hip_stream);
+}
+
+int vpt_gpu_sync(vpt_gpu_ctx* ctx) {
+  if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  VPT_HIP(hipDeviceSynchronize());
+  return VPT_OK;
+}
+
+int vpt_gpu_film_clear(vpt_gpu_ctx* ctx) {
+  if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  VPT_HIP(hipMemsetAsync(ctx->film, 0, ctx->film_count * sizeof(float), ctx->stream));
+  VPT_HIP(hipStreamSynchronize(ctx->stream));
+  return VPT_OK;
+}
+
+int vpt_gpu_film_device_ptr(vpt_gpu_ctx* ctx, float** film_device, uint64_t* count) {
+  if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
+  if (film_device) *film_device = ctx->film;
+  if (count) *count = ctx->film_count;
+  return VPT_OK;
+}
+
+int vpt_gpu_film_add_to_host(vpt_gpu_ctx* ctx, float* film_host) {
+  if (!ctx || !film_host) return vpt::set_error(VPT_E_INVALID, "null argument");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  VPT_HIP(hipDeviceSynchronize());
+  std::vector<float> tmp(ctx->film_count);
+  VPT_HIP(hipMemcpy(tmp.data(), ctx->film, ctx->film_count * sizeof(float), hipMemcpyDeviceToHost));
+  for (uint64_t i = 0; i < ctx->film_count; ++i) film_host[i] += tmp[i];
+  return VPT_OK;
+}
+
+int vpt_gpu_counters(vpt_gpu_ctx* ctx, vpt_counters* out, int reset) {
+  if (!ctx || !out) return vpt::set_error(VPT_E_INVALID, "null argument");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  VPT_HIP(hipDeviceSynchronize());
+  unsigned long long c[vpt::kCounterCount];
+  VPT_HIP(hipMemcpy(c, ctx->counters, sizeof c, hipMemcpyDeviceToHost));
+  uint64_t* o = reinterpret_cast<uint64_t*>(out);
+  for (int i = 0; i < vpt::kCounterCount; ++i) o[i] = c[i];
+  if (reset) VPT_HIP(hipMemset(ctx->counters, 0, sizeof c));
+  return VPT_OK;
+}
+
+int vpt_gpu_launch_info(const vpt_gpu_ctx* ctx, int* grid_blocks, int* block_threads) {
+  if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
+  if (grid_blocks) *grid_blocks = ctx->grid_blocks;
+  if (block_threads) *block_threads = vpt::kBlockThreads;
+  return VPT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,397 @@
+// vpt_grid_build.cpp — flattens a NanoVDB-style float grid into the GPU layout.
+//
+// HBM layout (per grid):
+//   cells8   int2[r8_n.x][r8_n.y][r8_n.z]  one entry per 8^3 voxel cell over every lower node
+//            (x = leaf index or -(2*dim+active), y = leaf majorant or tile value bits)
+//   cells128 int2[...]                     one entry per 128^3 cell over every upper node
+//   root     RootTileDev[]                 value tiles at the root (outside every upper node)
+//   bricks   float[leaf][9][9][9]          each leaf's 8^3 voxels plus a +1 apron, so that a
+//                                          trilinear stencil whose corner cell is in the leaf
+//                                          reads one brick (NanoVDB SampleFromVoxels semantics)
+// One 8-byte cells8 load answers getDim, probeLeaf, probeValue and the majorant of
+// RayMajorantIterator::update_current_majorant (volume.cpp:18-36) for any voxel of the cell.
+//
+// fix_majorants_for_interpolation (volume.cpp:104-160) is applied to the leaf maxima here.
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "vpt_internal.h"
+
+namespace vpt {
+namespace {
+
+inline uint64_t pack(int32_t i, int32_t j, int32_t k) {
+  return ((uint64_t)(uint32_t)i * 0x9E3779B97F4A7C15ULL) ^ ((uint64_t)(uint32_t)j << 21) ^ ((uint64_t)(uint32_t)k << 42) ^
+         ((uint64_t)(uint32_t)k >> 22);
+}
+struct Key3 {
+  int32_t i, j, k;
+  bool operator==(const Key3& o) const { return i == o.i && j == o.j && k == o.k; }
+};
+struct Key3Hash {
+  size_t operator()(const Key3& a) const { return (size_t)pack(a.i, a.j, a.k); }
+};
+struct TileVal {
+  float value;
+  int32_t active;
+};
+
+template <class F>
+void parallel_for(int64_t n, int threads, F f) {
+  if (threads <= 1 || n < 1024) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::thread> ts;
+  int64_t chunk = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; ++t) {
+    int64_t b = t * chunk, e = std::min<int64_t>(n, b + chunk);
+    if (b >= e) break;
+    ts.emplace_back([=]() { f(b, e); });
+  }
+  for (auto& t : ts) t.join();
+}
+
+inline int2 enc(int32_t code, float v) {
+  int32_t bits;
+  std::memcpy(&bits, &v, 4);
+  return int2{code, bits};
+}
+
+}  // namespace
+
+float host_value_at(const HostGrid& g, int32_t i, int32_t j, int32_t k) { return value_at(g.dev, i, j, k); }
+
+int build_host_grid(const vpt_grid_desc& d, bool fix, int threads, HostGrid& out) {
+  if (d.leaf_count && (!d.leaf_origin || !d.leaf_values || !d.leaf_max))
+    return set_error(VPT_E_INVALID, "grid: leaf arrays missing");
+  if (d.tile_count && (!d.tile_origin || !d.tile_level || !d.tile_value || !d.tile_active))
+    return set_error(VPT_E_INVALID, "grid: tile arrays missing");
+  if (d.leaf_count > (uint64_t)std::numeric_limits<int32_t>::max())
+    return set_error(VPT_E_INVALID, "grid: too many leaves");
+  if (threads <= 0) threads = default_threads();
+  const uint64_t nleaf = d.leaf_count;
+
+  DevGrid& G = out.dev;
+  std::memset(&G, 0, sizeof G);
+  std::memcpy(G.mat, d.map_mat, sizeof G.mat);
+  std::memcpy(G.inv_mat, d.map_inv_mat, sizeof G.inv_mat);
+  std::memcpy(G.vec, d.map_vec, sizeof G.vec);
+  G.background = d.background;
+  std::memcpy(G.bbox_min, d.index_bbox_min, sizeof G.bbox_min);
+  std::memcpy(G.bbox_max, d.index_bbox_max, sizeof G.bbox_max);
+
+  // --- node sets ------------------------------------------------------------------------------
+  std::unordered_set<Key3, Key3Hash> lowers, uppers;
+  std::unordered_map<Key3, TileVal, Key3Hash> t1, t2, t3;  // tiles by level, keyed by tile origin
+  for (uint64_t n = 0; n < nleaf; ++n) {
+    const int32_t* o = d.leaf_origin + 3 * n;
+    if ((o[0] & 7) || (o[1] & 7) || (o[2] & 7)) return set_error(VPT_E_INVALID, "grid: leaf origin not 8-aligned");
+    lowers.insert(Key3{o[0] & ~127, o[1] & ~127, o[2] & ~127});
+  }
+  for (uint64_t n = 0; n < d.lower_count; ++n) {
+    const int32_t* o = d.lower_origin + 3 * n;
+    lowers.insert(Key3{o[0] & ~127, o[1] & ~127, o[2] & ~127});
+  }
+  for (uint64_t n = 0; n < d.tile_count; ++n) {
+    const int32_t* o = d.tile_origin + 3 * n;
+    int lvl = d.tile_level[n];
+    TileVal tv{d.tile_value[n], d.tile_active[n] ? 1 : 0};
+    if (lvl == 1) {
+      t1[Key3{o[0] & ~7, o[1] & ~7, o[2] & ~7}] = tv;
+      lowers.insert(Key3{o[0] & ~127, o[1] & ~127, o[2] & ~127});
+    } else if (lvl == 2) {
+      t2[Key3{o[0] & ~127, o[1] & ~127, o[2] & ~127}] = tv;
+      uppers.insert(Key3{o[0] & ~4095, o[1] & ~4095, o[2] & ~4095});
+    } else if (lvl == 3) {
+      t3[Key3{o[0] & ~4095, o[1] & ~4095, o[2] & ~4095}] = tv;
+    } else {
+      return set_error(VPT_E_INVALID, "grid: tile_level must be 1, 2 or 3");
+    }
+  }
+  for (const Key3& l : lowers) uppers.insert(Key3{l.i & ~4095, l.j & ~4095, l.k & ~4095});
+  for (uint64_t n = 0; n < d.upper_count; ++n) {
+    const int32_t* o = d.upper_origin + 3 * n;
+    uppers.insert(Key3{o[0] & ~4095, o[1] & ~4095, o[2] & ~4095});
+  }
+  for (const Key3& u : uppers) t3.erase(u);  // a root slot holds a child or a value, not both
+
+  // Info for a voxel that is in no lower node: upper-node tile (dim 128) or root (dim 4096).
+  auto upper_level = [&](int32_t i, int32_t j, int32_t k) -> int2 {
+    Key3 uk{i & ~4095, j & ~4095, k & ~4095};
+    if (uppers.count(uk)) {
+      auto it = t2.find(Key3{i & ~127, j & ~127, k & ~127});
+      if (it != t2.end()) return enc(-(2 * 128 + it->second.active), it->second.value);
+      return enc(-(2 * 128), d.background);
+    }
+    auto it = t3.find(uk);
+    if (it != t3.end()) return enc(-(2 * 4096 + it->second.active), it->second.value);
+    return enc(-(2 * 4096), d.background);
+  };
+
+  // --- cells128 over all upper nodes -----------------------------------------------------------
+  if (!uppers.empty()) {
+    int32_t lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+    for (const Key3& u : uppers) {
+      const int32_t c[3] = {u.i, u.j, u.k};
+      for (int a = 0; a < 3; ++a) {
+        lo[a] = std::min(lo[a], c[a]);
+        hi[a] = std::max(hi[a], c[a]);
+      }
+    }
+    int64_t cnt = 1;
+    for (int a = 0; a < 3; ++a) {
+      G.r128_org[a] = lo[a];
+      G.r128_n[a] = (int32_t)(((int64_t)hi[a] - lo[a]) / 128 + 32);
+      cnt *= G.r128_n[a];
+    }
+    if (cnt > (int64_t)1 << 31) return set_error(VPT_E_NOMEM, "grid: upper-node table too large");
+    out.cells128.resize((size_t)cnt);
+    const int32_t ny = G.r128_n[1], nz = G.r128_n[2];
+    parallel_for(G.r128_n[0], threads, [&](int64_t b, int64_t e) {
+      for (int64_t a = b; a < e; ++a)
+        for (int32_t bb = 0; bb < ny; ++bb)
+          for (int32_t c = 0; c < nz; ++c)
+            out.cells128[((size_t)a * ny + bb) * nz + c] =
+                upper_level(G.r128_org[0] + (int32_t)a * 128, G.r128_org[1] + bb * 128, G.r128_org[2] + c * 128);
+    });
+  }
+
+  // --- cells8 over all lower nodes -------------------------------------------------------------
+  if (!lowers.empty()) {
+    int32_t lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+    for (const Key3& l : lowers) {
+      const int32_t c[3] = {l.i, l.j, l.k};
+      for (int a = 0; a < 3; ++a) {
+        lo[a] = std::min(lo[a], c[a]);
+        hi[a] = std::max(hi[a], c[a]);
+      }
+    }
+    int64_t cnt = 1;
+    int32_t nl[3];
+    for (int a = 0; a < 3; ++a) {
+      G.r8_org[a] = lo[a];
+      nl[a] = (int32_t)(((int64_t)hi[a] - lo[a]) / 128 + 1);
+      G.r8_n[a] = nl[a] * 16;
+      cnt *= G.r8_n[a];
+    }
+    if (cnt > (int64_t)1 << 32) return set_error(VPT_E_NOMEM, "grid: leaf-slot table too large");
+    out.cells8.resize((size_t)cnt);
+    std::vector<uint8_t> lower_present((size_t)nl[0] * nl[1] * nl[2], 0);
+    for (const Key3& l : lowers)
+      lower_present[((size_t)((l.i - lo[0]) / 128) * nl[1] + (l.j - lo[1]) / 128) * nl[2] + (l.k - lo[2]) / 128] = 1;
+    const int32_t ny = G.r8_n[1], nz = G.r8_n[2];
+    parallel_for(G.r8_n[0], threads, [&](int64_t b, int64_t e) {
+      for (int64_t a = b; a < e; ++a)
+        for (int32_t bb = 0; bb < ny; ++bb)
+          for (int32_t c = 0; c < nz; ++c) {
+            int32_t i = G.r8_org[0] + (int32_t)a * 8, j = G.r8_org[1] + bb * 8, k = G.r8_org[2] + c * 8;
+            int2 v;
+            if (lower_present[((size_t)(a >> 4) * nl[1] + (bb >> 4)) * nl[2] + (c >> 4)]) {
+              auto it = t1.find(Key3{i, j, k});
+              v = (it != t1.end()) ? enc(-(2 * 8 + it->second.active), it->second.value) : enc(-(2 * 8), d.background);
+            } else {
+              v = upper_level(i, j, k);
+            }
+            out.cells8[((size_t)a * ny + bb) * nz + c] = v;
+          }
+    });
+    for (uint64_t n = 0; n < nleaf; ++n) {
+      const int32_t* o = d.leaf_origin + 3 * n;
+      size_t idx = ((size_t)((o[0] - lo[0]) >> 3) * ny + ((o[1] - lo[1]) >> 3)) * nz + ((o[2] - lo[2]) >> 3);
+      out.cells8[idx] = enc((int32_t)n, d.leaf_max[n]);
+    }
+  }
+
+  for (const auto& kv : t3) {
+    RootTileDev r{};
+    r.origin[0] = kv.first.i;
+    r.origin[1] = kv.first.j;
+    r.origin[2] = kv.first.k;
+    r.value = kv.second.value;
+    r.active = kv.second.active;
+    out.root.push_back(r);
+  }
+  G.root_count = (int32_t)out.root.size();
+  G.cells8 = out.cells8.data();
+  G.cells128 = out.cells128.data();
+  G.root = out.root.data();
+
+  // --- bricks: 8^3 leaf voxels + the +1 apron ------------------------------------------------
+  out.bricks.assign((size_t)nleaf * kBrickVox, 0.0f);
+  G.bricks = out.bricks.data();
+  // interior first (the apron reads neighbours' interiors through value_at)
+  parallel_for((int64_t)nleaf, threads, [&](int64_t b, int64_t e) {
+    for (int64_t n = b; n < e; ++n) {
+      const float* src = d.leaf_values + (size_t)n * 512;
+      float* dst = out.bricks.data() + (size_t)n * kBrickVox;
+      for (int x = 0; x < 8; ++x)
+        for (int y = 0; y < 8; ++y)
+          for (int z = 0; z < 8; ++z) dst[x * 81 + y * 9 + z] = src[(x << 6) | (y << 3) | z];
+    }
+  });
+  parallel_for((int64_t)nleaf, threads, [&](int64_t b, int64_t e) {
+    for (int64_t n = b; n < e; ++n) {
+      const int32_t* o = d.leaf_origin + 3 * n;
+      float* dst = out.bricks.data() + (size_t)n * kBrickVox;
+      for (int x = 0; x < 9; ++x)
+        for (int y = 0; y < 9; ++y)
+          for (int z = 0; z < 9; ++z)
+            if (x == 8 || y == 8 || z == 8) dst[x * 81 + y * 9 + z] = value_at(G, o[0] + x, o[1] + y, o[2] + z);
+    }
+  });
+
+  // --- majorants -------------------------------------------------------------------------------
+  out.leaf_max.assign(d.leaf_max, d.leaf_max + nleaf);
+  if (fix) {
+    parallel_for((int64_t)nleaf, threads, [&](int64_t b, int64_t e) {
+      for (int64_t n = b; n < e; ++n) {
+        const int32_t* o = d.leaf_origin + 3 * n;
+        float m = d.leaf_max[n];
+        // The 26 neighbour leaf boxes intersected with the leaf bbox expanded by 1 = the one-voxel
+        // shell around the leaf; std::max keeps the first argument on ties/NaN like the reference.
+        for (int32_t x = o[0] - 1; x <= o[0] + 8; ++x)
+          for (int32_t y = o[1] - 1; y <= o[1] + 8; ++y)
+            for (int32_t z = o[2] - 1; z <= o[2] + 8; ++z) {
+              bool inside = x >= o[0] && x <= o[0] + 7 && y >= o[1] && y <= o[1] + 7 && z >= o[2] && z <= o[2] + 7;
+              if (inside) continue;
+              float v = value_at(G, x, y, z);
+              m = std::max(m, v);
+            }
+        out.leaf_max[n] = m;
+      }
+    });
+    for (uint64_t n = 0; n < nleaf; ++n) {
+      const int32_t* o = d.leaf_origin + 3 * n;
+      size_t idx = ((size_t)((o[0] - G.r8_org[0]) >> 3) * G.r8_n[1] + ((o[1] - G.r8_org[1]) >> 3)) * G.r8_n[2] +
+                   ((o[2] - G.r8_org[2]) >> 3);
+      out.cells8[idx] = enc((int32_t)n, out.leaf_max[n]);
+    }
+  }
+  return VPT_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Synthetic stand-in volumes: the real wdas_cloud.nvdb / fire.nvdb are not available.
+// ------------------------------------------------------------------------------------------------
+namespace {
+struct SynthDesc {
+  vpt_grid_desc d;  // must stay first
+  std::vector<int32_t> origin;
+  std::vector<float> values, maxv;
+  std::vector<uint64_t> mask;
+};
+
+double synth_voxel(int kind, int n, int i, int j, int k) {
+  if (kind == 0) return 1.0;
+  const double half = n / 2.0;
+  const double px = (i + 0.5) / half - 1.0, py = (j + 0.5) / half - 1.0, pz = (k + 0.5) / half - 1.0;
+  const double r = std::sqrt(px * px + py * py + pz * pz);
+  const double base = std::min(1.0, std::max(0.0, (0.85 - r) / 0.35));
+  if (kind == 2) return 40.0 * base;
+  return base * (0.5 + 0.5 * std::sin(11.0 * px + 2.0) * std::sin(13.0 * py + 1.0) * std::sin(17.0 * pz + 3.0));
+}
+}  // namespace
+
+}  // namespace vpt
+
+extern "C" int vpt_fix_majorants(const vpt_grid_desc* grid, float* out_leaf_max, int num_threads) {
+  if (!grid || !out_leaf_max) return vpt::set_error(VPT_E_INVALID, "vpt_fix_majorants: null argument");
+  vpt::HostGrid hg;
+  int rc = vpt::build_host_grid(*grid, true, num_threads, hg);
+  if (rc) return rc;
+  std::copy(hg.leaf_max.begin(), hg.leaf_max.end(), out_leaf_max);
+  return VPT_OK;
+}
+
+// kind 0: constant 1.0 over [0,n)^3 (C2); kind 1: procedural cloud density (C3);
+// kind 2: temperature 40*base on the same lattice (C4).  world = index - n/2, voxel size 1.
+// Leaves with no non-zero voxel are omitted; non-zero voxels are active; indexBBox = active bbox;
+// leaf max = max over active voxels (NanoVDB's stored statistic).
+extern "C" vpt_grid_desc* vpt_synth_grid(int kind, int n) {
+  if (n <= 0 || (n % 8) != 0 || kind < 0 || kind > 2) {
+    vpt::set_error(VPT_E_INVALID, "vpt_synth_grid: kind in {0,1,2}, n a positive multiple of 8");
+    return nullptr;
+  }
+  auto* s = new vpt::SynthDesc();
+  const int nl = n / 8;
+  const int T = vpt::default_threads();
+  struct Part {
+    std::vector<int32_t> origin;
+    std::vector<float> values, maxv;
+    std::vector<uint64_t> mask;
+    int32_t lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+  };
+  std::vector<Part> parts(nl);
+  vpt::parallel_for(nl, T, [&](int64_t b, int64_t e) {
+    std::vector<float> buf(512);
+    for (int64_t li = b; li < e; ++li) {
+      Part& P = parts[li];
+      for (int lj = 0; lj < nl; ++lj)
+        for (int lk = 0; lk < nl; ++lk) {
+          bool any = false;
+          float mx = -std::numeric_limits<float>::infinity();
+          uint64_t mask[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+          for (int a = 0; a < 8; ++a)
+            for (int bb = 0; bb < 8; ++bb)
+              for (int c = 0; c < 8; ++c) {
+                const int i = (int)li * 8 + a, j = lj * 8 + bb, k = lk * 8 + c;
+                float v = (float)vpt::synth_voxel(kind, n, i, j, k);
+                int off = (a << 6) | (bb << 3) | c;
+                buf[off] = v;
+                if (v != 0.0f) {
+                  any = true;
+                  mask[off >> 6] |= 1ULL << (off & 63);
+                  mx = std::max(mx, v);
+                  const int32_t cc[3] = {i, j, k};
+                  for (int q = 0; q < 3; ++q) {
+                    P.lo[q] = std::min(P.lo[q], cc[q]);
+                    P.hi[q] = std::max(P.hi[q], cc[q]);
+                  }
+                }
+              }
+          if (!any) continue;
+          P.origin.insert(P.origin.end(), {(int32_t)li * 8, lj * 8, lk * 8});
+          P.values.insert(P.values.end(), buf.begin(), buf.end());
+          P.mask.insert(P.mask.end(), mask, mask + 8);
+          P.maxv.push_back(mx);
+        }
+    }
+  });
+  int32_t lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+  for (auto& P : parts) {
+    s->origin.insert(s->origin.end(), P.origin.begin(), P.origin.end());
+    s->values.insert(s->values.end(), P.values.begin(), P.values.end());
+    s->mask.insert(s->mask.end(), P.mask.begin(), P.mask.end());
+    s->maxv.insert(s->maxv.end(), P.maxv.begin(), P.maxv.end());
+    for (int q = 0; q < 3; ++q) {
+      lo[q] = std::min(lo[q], P.lo[q]);
+      hi[q] = std::max(hi[q], P.hi[q]);
+    }
+  }
+  vpt_grid_desc& d = s->d;
+  std::memset(&d, 0, sizeof d);
+  const float half = (float)(n / 2);
+  for (int a = 0; a < 9; ++a) d.map_mat[a] = d.map_inv_mat[a] = (a % 4 == 0) ? 1.0f : 0.0f;
+  for (int q = 0; q < 3; ++q) {
+    d.map_vec[q] = -half;
+    d.index_bbox_min[q] = lo[q];
+    d.index_bbox_max[q] = hi[q];
+  }
+  d.background = 0.0f;
+  d.leaf_count = s->maxv.size();
+  d.leaf_origin = s->origin.data();
+  d.leaf_values = s->values.data();
+  d.leaf_value_mask = s->mask.data();
+  d.leaf_max = s->maxv.data();
+  return &s->d;
+}
+
+extern "C" void vpt_synth_free(vpt_grid_desc* d) { delete reinterpret_cast<vpt::SynthDesc*>(d); }

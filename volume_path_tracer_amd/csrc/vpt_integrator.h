@@ -1,0 +1,717 @@
+// vpt_integrator.h — the per-lane volumetric path-tracing state machine (device code).
+//
+// One lane owns one (tile, wave) job at a time and traces the tile's pixels serially in the job's
+// pcg32_fast stream, exactly as vpt::run does on one CPU thread (src/worker.cpp:104-207): the RNG
+// stream order forbids tracing a tile's pixels concurrently.  The nested loops of the reference
+//   run -> per pixel -> per bounce -> MajorantTransmittanceSampler::next -> RayMajorantIterator::next
+// (worker.cpp:130-195, majorant_transmittance_sampler.cpp:21-81, volume.cpp:38-76)
+// are flattened into one state machine whose unit of work is ONE HDDA step or ONE free-flight draw,
+// so the 64 lanes of a wavefront advance together no matter how different their paths are, and a
+// lane whose job ends picks the next job (persistent kernel, lane refill).
+//
+// Every floating-point operation is the reference's, in the reference's order (built with
+// -ffp-contract=off): Eigen 3-vector reductions as x0 + (x1 + x2), NanoVDB Map products with fmaf,
+// NanoVDB Vec3::length as (x*x + y*y) + z*z, glibc logf/sinf/cosf via vpt_math.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "vpt_math.h"
+
+namespace vpt {
+
+// ------------------------------------------------------------------------------------------------
+// HBM layout of one grid (built by vpt_grid_build.cpp)
+// ------------------------------------------------------------------------------------------------
+// Cell code: >= 0 -> leaf index (value = leaf majorant after fix_majorants_for_interpolation);
+//            <  0 -> no leaf: -(2*dim + active), dim = ReadAccessor::getDim (8 lower tile,
+//                    128 upper tile, 4096 root tile / background), value = tile value.
+struct RootTileDev {
+  int32_t origin[3];
+  float value;
+  int32_t active;
+  int32_t pad[3];
+};
+
+struct DevGrid {
+  float mat[9], inv_mat[9], vec[3];  // nanovdb::Map float members
+  float background;
+  int32_t bbox_min[3], bbox_max[3];  // indexBBox (inclusive)
+  int32_t r8_org[3], r8_n[3];        // dense 8^3-cell table over all lower nodes
+  int32_t r128_org[3], r128_n[3];    // dense 128^3-cell table over all upper nodes
+  int32_t root_count, pad0;
+  const int2* cells8;
+  const int2* cells128;
+  const RootTileDev* root;
+  const float* bricks;  // [leaf][9][9][9]: voxel (origin + (x,y,z)) for x,y,z in 0..8 (apron +1)
+};
+
+constexpr int kBrick = 9;
+constexpr int kBrickVox = kBrick * kBrick * kBrick;  // 729
+
+struct Cell {
+  int32_t code;
+  float value;
+};
+
+__host__ __device__ __forceinline__ Cell cell_at(const DevGrid& g, int32_t i, int32_t j, int32_t k) {
+  int32_t a = (i - g.r8_org[0]) >> 3, b = (j - g.r8_org[1]) >> 3, c = (k - g.r8_org[2]) >> 3;
+  if ((uint32_t)a < (uint32_t)g.r8_n[0] && (uint32_t)b < (uint32_t)g.r8_n[1] && (uint32_t)c < (uint32_t)g.r8_n[2]) {
+    int2 e = g.cells8[((int64_t)a * g.r8_n[1] + b) * g.r8_n[2] + c];
+    return Cell{e.x, math::as_f32((uint32_t)e.y)};
+  }
+  a = (i - g.r128_org[0]) >> 7;
+  b = (j - g.r128_org[1]) >> 7;
+  c = (k - g.r128_org[2]) >> 7;
+  if ((uint32_t)a < (uint32_t)g.r128_n[0] && (uint32_t)b < (uint32_t)g.r128_n[1] && (uint32_t)c < (uint32_t)g.r128_n[2]) {
+    int2 e = g.cells128[((int64_t)a * g.r128_n[1] + b) * g.r128_n[2] + c];
+    return Cell{e.x, math::as_f32((uint32_t)e.y)};
+  }
+  for (int32_t r = 0; r < g.root_count; ++r) {
+    const RootTileDev& t = g.root[r];
+    if ((i & ~4095) == t.origin[0] && (j & ~4095) == t.origin[1] && (k & ~4095) == t.origin[2])
+      return Cell{-(2 * 4096 + t.active), t.value};
+  }
+  return Cell{-(2 * 4096), g.background};
+}
+
+// max(8, ReadAccessor::getDim(ijk)) (volume.cpp:11-14): a leaf's getDim is 1.
+__host__ __device__ __forceinline__ int32_t hdda_dim_of(Cell c) { return c.code >= 0 ? 8 : ((-c.code) >> 1); }
+// update_current_majorant (volume.cpp:18-36): leaf max, else active tile value, else 0.
+__host__ __device__ __forceinline__ float majorant_of(Cell c) {
+  if (c.code >= 0) return c.value;
+  return ((-c.code) & 1) ? c.value : 0.0f;
+}
+// ReadAccessor::getValue(ijk)
+__host__ __device__ __forceinline__ float value_at(const DevGrid& g, int32_t i, int32_t j, int32_t k) {
+  Cell c = cell_at(g, i, j, k);
+  if (c.code < 0) return c.value;
+  return g.bricks[(int64_t)c.code * kBrickVox + (i & 7) * 81 + (j & 7) * 9 + (k & 7)];
+}
+
+// nanovdb::math::SampleFromVoxels<Acc,1,true> stencil cache (values identical with or without it).
+struct Stencil {
+  int32_t i, j, k;
+  int32_t valid;
+  float v[8];  // v[a*4 + b*2 + c] = value(i+a, j+b, k+c)
+};
+
+__host__ __device__ __forceinline__ void fetch_stencil(const DevGrid& g, Stencil& s, int32_t i, int32_t j, int32_t k) {
+  s.i = i;
+  s.j = j;
+  s.k = k;
+  s.valid = 1;
+  Cell c = cell_at(g, i, j, k);
+  if (c.code >= 0) {
+    // Corner cell inside a leaf: the 9^3 apron brick holds the whole 2^3 stencil.
+    const float* b = g.bricks + (int64_t)c.code * kBrickVox + (i & 7) * 81 + (j & 7) * 9 + (k & 7);
+    s.v[0] = b[0];
+    s.v[1] = b[1];
+    s.v[2] = b[9];
+    s.v[3] = b[10];
+    s.v[4] = b[81];
+    s.v[5] = b[82];
+    s.v[6] = b[90];
+    s.v[7] = b[91];
+  } else {
+    for (int a = 0; a < 2; ++a)
+      for (int b = 0; b < 2; ++b)
+        for (int cc = 0; cc < 2; ++cc) s.v[a * 4 + b * 2 + cc] = value_at(g, i + a, j + b, k + cc);
+  }
+}
+
+// TrilinearSampler::sample: lerp(a, b, w) = a + w * (b - a), z then y then x.
+__host__ __device__ __forceinline__ float lerpf(float a, float b, float w) { return a + w * (b - a); }
+// Returns true when the stencil had to be (re)fetched.
+__host__ __device__ __forceinline__ bool trilinear(const DevGrid& g, Stencil& s, float x, float y, float z, float& out) {
+  float fi = floorf(x), fj = floorf(y), fk = floorf(z);
+  float u = x - fi, v = y - fj, w = z - fk;
+  int32_t i = (int32_t)fi, j = (int32_t)fj, k = (int32_t)fk;
+  bool refresh = !s.valid || i != s.i || j != s.j || k != s.k;
+  if (refresh) fetch_stencil(g, s, i, j, k);
+  out = lerpf(lerpf(lerpf(s.v[0], s.v[1], w), lerpf(s.v[2], s.v[3], w), v),
+              lerpf(lerpf(s.v[4], s.v[5], w), lerpf(s.v[6], s.v[7], w), v), u);
+  return refresh;
+}
+
+// nanovdb Map: matMult with fmaf.
+__host__ __device__ __forceinline__ void map_inv(const DevGrid& g, float x, float y, float z, float& ox, float& oy, float& oz) {
+  const float* m = g.inv_mat;
+  float a = x - g.vec[0], b = y - g.vec[1], c = z - g.vec[2];
+  ox = __builtin_fmaf(a, m[0], __builtin_fmaf(b, m[1], c * m[2]));
+  oy = __builtin_fmaf(a, m[3], __builtin_fmaf(b, m[4], c * m[5]));
+  oz = __builtin_fmaf(a, m[6], __builtin_fmaf(b, m[7], c * m[8]));
+}
+__host__ __device__ __forceinline__ void jac_inv(const DevGrid& g, float x, float y, float z, float& ox, float& oy, float& oz) {
+  const float* m = g.inv_mat;
+  ox = __builtin_fmaf(x, m[0], __builtin_fmaf(y, m[1], z * m[2]));
+  oy = __builtin_fmaf(x, m[3], __builtin_fmaf(y, m[4], z * m[5]));
+  oz = __builtin_fmaf(x, m[6], __builtin_fmaf(y, m[7], z * m[8]));
+}
+__host__ __device__ __forceinline__ void map_fwd(const DevGrid& g, float x, float y, float z, float& ox, float& oy, float& oz) {
+  const float* m = g.mat;
+  ox = __builtin_fmaf(x, m[0], __builtin_fmaf(y, m[1], __builtin_fmaf(z, m[2], g.vec[0])));
+  oy = __builtin_fmaf(x, m[3], __builtin_fmaf(y, m[4], __builtin_fmaf(z, m[5], g.vec[1])));
+  oz = __builtin_fmaf(x, m[6], __builtin_fmaf(y, m[7], __builtin_fmaf(z, m[8], g.vec[2])));
+}
+
+// ------------------------------------------------------------------------------------------------
+// Scene constants (host-computed once with the reference's formulas)
+// ------------------------------------------------------------------------------------------------
+struct DevScene {
+  DevGrid density;
+  DevGrid temperature;
+  int32_t has_temperature;
+  uint32_t seed;
+  int32_t W, H, tw, th;
+  uint32_t ntx;
+  uint32_t max_depth;
+  uint64_t T;  // jobs per wave
+  int32_t single_pixel_enabled;
+  int32_t sp_x, sp_y;
+  float jitter_scale;   // use_jitter ? 0.5 : 0.0 (worker.cpp:122)
+  float cam_L[9];       // Camera::raster_to_world_dir linear (row-major)
+  float cam_t[3];       // and translation
+  float cam_pos[3];
+  float imaging_ratio;
+  float le_inf[3];      // infinite_light.xyz * multiplier (worker.cpp:199)
+  float Li[3];          // distant_light.xyz * multiplier (worker.cpp:55)
+  int32_t li_zero;      // Li == 0 -> sample_Ld returns before any draw (worker.cpp:57-58)
+  float wi[3];          // distant_light.inv_direction.normalized() (worker.cpp:54)
+  float sigma_a, sigma_s, sigma_t, g_hg, le_scale, temp_scale, temp_offset;
+  const float* bb;      // blackbody table [501][3] (row 500 = 0)
+  const float* cie;     // [471][3] for T >= 49900 K
+  float y_integral;
+};
+
+// ------------------------------------------------------------------------------------------------
+// RNG: hash(seed, jid) + pcg32_fast + uniform<float> (hash.hpp:20-67, random.hpp:86-115)
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t job_seed(uint64_t seed, uint64_t k) {
+  const uint64_t m = 0xc6a4a7935bd1e995ULL;
+  uint64_t h = seed ^ (8ULL * m);
+  k *= m;
+  k ^= k >> 47;
+  k *= m;
+  h ^= k;
+  h *= m;
+  h ^= h >> 47;
+  h *= m;
+  h ^= h >> 47;
+  return h | 3ULL;  // pcg32_fast::seed: state = s | 3
+}
+__host__ __device__ __forceinline__ float rng_uniform(uint64_t& state) {
+  uint64_t old = state;
+  state = state * 6364136223846793005ULL;
+  uint32_t rshift = (uint32_t)(old >> 61);
+  old ^= old >> 22;
+  uint32_t r = (uint32_t)(old >> (22 + rshift));
+  float v = (float)r * 0x1p-32f;
+  const float one_minus_eps = 0x1.fffffep-1f;
+  return (v < one_minus_eps) ? v : one_minus_eps;  // std::min<float>(1-eps, v)
+}
+
+// ------------------------------------------------------------------------------------------------
+// Blackbody lookup (precompute_blackbody.cpp:25-52)
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ float bb_idx_to_temp(int idx) { return (idx - 1) * 100.0f; }
+__host__ __device__ inline float planck_dev(float lambda_m, float t) {
+  if (t <= 0.0f) return 0.0f;
+  const float c = 299792458.f, h = 6.62606957e-34f, kb = 1.3806488e-23f;
+  const float num = 2 * h * c * c;
+  float l2 = lambda_m * lambda_m;
+  float lambda5 = (float)((double)l2 * (double)l2 * (double)lambda_m);  // pow(double(l),5) (not bit-exact)
+  float e = expf((h * c) / (lambda_m * kb * t));
+  return num / (lambda5 * (e - 1));
+}
+__host__ __device__ inline void blackbody_xyz(const DevScene& S, float t, float& X, float& Y, float& Z) {
+  if (!(t - t == 0.0f)) {  // !isfinite
+    X = Y = Z = __builtin_nanf("");
+    return;
+  }
+  if (t <= 0.0f) {
+    X = Y = Z = 0.0f;
+    return;
+  }
+  if (t >= 49900.0f) {
+    // Direct spectral integration (spectral.hpp:62-75).  Rare path: std::pow/std::exp are glibc's
+    // on the host, so this branch is not bit-exact (documented in DESIGN.md).
+    float acc[3] = {0.0f, 0.0f, 0.0f};
+    for (int c = 0; c < 3; ++c) {
+      float integ = 0.0f;
+      for (int i = 0; i < 471; ++i) integ += S.cie[i * 3 + c] * planck_dev((float)(360 + i) * 1e-9f, t);
+      acc[c] = integ;
+    }
+    X = acc[0] / S.y_integral;
+    Y = acc[1] / S.y_integral;
+    Z = acc[2] / S.y_integral;
+    return;
+  }
+  int dn = (int)(t / 100.0f);
+  while (t <= bb_idx_to_temp(dn - 1)) --dn;
+  while (t >= bb_idx_to_temp(dn + 1)) ++dn;
+  const float* a = S.bb + dn * 3;
+  if (t == bb_idx_to_temp(dn)) {
+    X = a[0];
+    Y = a[1];
+    Z = a[2];
+    return;
+  }
+  float w = (t - bb_idx_to_temp(dn)) / 100.0f;
+  const float* b = a + 3;
+  X = a[0] + (b[0] - a[0]) * w;  // vpt::lerp: a + (b - a) * t (utils.hpp:26-29)
+  Y = a[1] + (b[1] - a[1]) * w;
+  Z = a[2] + (b[2] - a[2]) * w;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Lane state
+// ------------------------------------------------------------------------------------------------
+enum : int32_t {
+  ST_FETCH = 0,   // take the next job
+  ST_PIXEL = 1,   // start the next pixel of the tile
+  ST_BOUNCE = 2,  // top of the depth loop: intersect the current primary ray
+  ST_SAMPLE = 3,  // inside MajorantTransmittanceSampler::next (primary or shadow ray)
+  ST_NEE_DONE = 4,
+  ST_FINISH = 5,  // pixel done: environment light, film
+  ST_DONE = 6
+};
+enum : int32_t { SM_NEED_SEG = 0, SM_STEP = 1, SM_DRAW = 2 };
+
+struct LaneCounters {
+  uint32_t samples, dda_steps, segments, draws, stencils, density_evals, temp_stencils, scatters, shadow_rays,
+      rng_draws;
+};
+
+struct Lane {
+  int32_t state, sm;
+  uint64_t jid_local;  // job index relative to jid_begin
+  uint64_t rng;
+  int32_t x0, y0, rw, rh, pix, px, py;
+  uint32_t depth;
+  int32_t terminated, shadow;
+  float L[3];
+  float ro[3], rd[3];  // current primary world ray
+  float sp[3];         // scatter point (world) while the shadow ray runs
+  float Tr;            // shadow-ray transmittance
+  // RayMajorantIterator: index-space ray, scale, majorant, HDDA
+  float e[3], d[3], inv[3];
+  float scale, maj;
+  int32_t dim;
+  float T0, T1;
+  float nxt[3], dlt[3];
+  int32_t vox[3], stp[3];
+  // current majorant segment
+  float s_t0, s_t1, s_dmaj;
+  // collision record (MediumProperties)
+  float cp[3], c_sigma_maj, c_density;
+  Stencil dens;
+  Stencil temp;
+  LaneCounters cnt;
+};
+
+// Volume::intersect (volume.cpp:78-88) + RayMajorantIterator ctor (volume.cpp:90-98).
+__host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, const float o[3], const float dir[3]) {
+  // nanovdb::math::Ray<float>(eye, dir) with t0 = 1e-5 (Delta<float>), t1 = FLT_MAX; worldToIndexF.
+  float ex, ey, ez, dx, dy, dz;
+  map_inv(g, o[0], o[1], o[2], ex, ey, ez);
+  jac_inv(g, dir[0], dir[1], dir[2], dx, dy, dz);
+  float len = sqrtf(dx * dx + dy * dy + dz * dz);
+  float inv_len = 1.0f / len;
+  dx = dx * inv_len;
+  dy = dy * inv_len;
+  dz = dz * inv_len;
+  float t0 = len * 1e-5f;
+  float t1 = 3.40282347e+38f;
+  float ix = 1 / dx, iy = 1 / dy, iz = 1 / dz;
+  // Ray::clip(indexBBox): slab test against [min, max + 1].
+  const float E[3] = {ex, ey, ez}, I[3] = {ix, iy, iz};
+  for (int a = 0; a < 3; ++a) {
+    float lo = (float)g.bbox_min[a], hi = (float)(g.bbox_max[a] + 1);
+    lo = (lo - E[a]) * I[a];
+    hi = (hi - E[a]) * I[a];
+    if (lo > hi) {
+      float tmp = lo;
+      lo = hi;
+      hi = tmp;
+    }
+    if (lo > t0) t0 = lo;
+    if (hi < t1) t1 = hi;
+    if (t0 > t1) return false;
+  }
+  ln.e[0] = ex;
+  ln.e[1] = ey;
+  ln.e[2] = ez;
+  ln.d[0] = dx;
+  ln.d[1] = dy;
+  ln.d[2] = dz;
+  ln.inv[0] = ix;
+  ln.inv[1] = iy;
+  ln.inv[2] = iz;
+  // m_scale = 1 / |worldToIndexDirF(index dir)|
+  float jx, jy, jz;
+  jac_inv(g, dx, dy, dz, jx, jy, jz);
+  ln.scale = 1 / sqrtf(jx * jx + jy * jy + jz * jz);
+  ln.maj = __builtin_nanf("");
+  // HDDA(ray, max(8, getDim(floor(ray.start())))) -> init(ray, t0, t1, dim)
+  float px = ex + dx * t0, py = ey + dy * t0, pz = ez + dz * t0;
+  int32_t dim = hdda_dim_of(cell_at(g, (int32_t)floorf(px), (int32_t)floorf(py), (int32_t)floorf(pz)));
+  ln.dim = dim;
+  ln.T0 = t0;
+  ln.T1 = t1;
+  const float P[3] = {px, py, pz}, D[3] = {dx, dy, dz};
+  for (int a = 0; a < 3; ++a) {
+    int32_t v = ((int32_t)floorf(P[a])) & (~(dim - 1));
+    ln.vox[a] = v;
+    if (D[a] == 0.0f) {
+      ln.nxt[a] = 3.40282347e+38f;
+      ln.stp[a] = 0;
+      ln.dlt[a] = 0.0f;
+    } else if (I[a] > 0) {
+      ln.stp[a] = 1;
+      ln.nxt[a] = t0 + ((float)(v + dim) - P[a]) * I[a];
+      ln.dlt[a] = I[a];
+    } else {
+      ln.stp[a] = -1;
+      ln.nxt[a] = t0 + ((float)v - P[a]) * I[a];
+      ln.dlt[a] = -I[a];
+    }
+  }
+  ln.sm = SM_NEED_SEG;
+  ln.dens.valid = 0;
+  return true;
+}
+
+// One iteration of the do-while in RayMajorantIterator::next (volume.cpp:53-71).
+// Returns true when the segment [s_t0, s_t1) with majorant s_dmaj is complete.
+__host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
+  ln.s_dmaj = ln.maj;
+  ++ln.cnt.dda_steps;
+  // HDDA::step(): axis = MinIndex(next); written with static indices so the lane state stays in VGPRs.
+  const float n0 = ln.nxt[0], n1 = ln.nxt[1], n2 = ln.nxt[2];
+  const float fdim = (float)ln.dim;
+  float tn;
+  if (n0 < n1 && n0 < n2) {
+    tn = n0;
+    ln.nxt[0] = tn + fdim * ln.dlt[0];
+    ln.vox[0] += ln.dim * ln.stp[0];
+  } else if (n1 < n2) {
+    tn = n1;
+    ln.nxt[1] = tn + fdim * ln.dlt[1];
+    ln.vox[1] += ln.dim * ln.stp[1];
+  } else {
+    tn = n2;
+    ln.nxt[2] = tn + fdim * ln.dlt[2];
+    ln.vox[2] += ln.dim * ln.stp[2];
+  }
+  ln.T0 = tn;
+  if (!(tn <= ln.T1)) {
+    ln.s_t1 = ln.T1;
+    return true;
+  }
+  // new_dim = max(8, getDim(floor(ray(time + 1.0001f))))
+  float tl = ln.T0 + 1.0001f;
+  Cell la = cell_at(g, (int32_t)floorf(ln.e[0] + ln.d[0] * tl), (int32_t)floorf(ln.e[1] + ln.d[1] * tl),
+                    (int32_t)floorf(ln.e[2] + ln.d[2] * tl));
+  int32_t nd = hdda_dim_of(la);
+  // HDDA::update(ray, dim)
+  if (nd != ln.dim) {
+    ln.dim = nd;
+    float P[3] = {ln.e[0] + ln.d[0] * ln.T0, ln.e[1] + ln.d[1] * ln.T0, ln.e[2] + ln.d[2] * ln.T0};
+    for (int b = 0; b < 3; ++b) ln.vox[b] = ((int32_t)floorf(P[b])) & (~(nd - 1));
+    for (int b = 0; b < 3; ++b) {
+      if (ln.stp[b] == 0) continue;
+      float n = ln.T0 + ((float)ln.vox[b] - P[b]) * ln.inv[b];
+      if (ln.stp[b] > 0) n += (float)nd * ln.inv[b];
+      ln.nxt[b] = n;
+    }
+  }
+  ln.maj = majorant_of(cell_at(g, ln.vox[0], ln.vox[1], ln.vox[2]));
+  if (ln.maj == ln.s_dmaj) return false;
+  ln.s_t1 = ln.T0;
+  return true;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Phase function helpers (random.hpp:56-84, utils.hpp:39-66)
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ void sample_hg(const float w[3], float u0, float u1, float g, float out[3]) {
+  float g2 = g * g;  // std::pow(g, 2.0f): correctly rounded square
+  float cos_theta;
+  if (fabsf(g) < 1e-3f) {
+    cos_theta = 1 - 2 * u0;
+  } else {
+    float q = (1.0f - g2) / (1.0f + g - 2.0f * g * u0);
+    cos_theta = 1.0f / (2.0f * g) * (1.0f + g2 - q * q);
+  }
+  float sin_theta = sqrtf(fmaxf(0.0f, 1.0f - cos_theta * cos_theta));
+  float phi = 2.0f * 3.14159274f * u1;
+  float sc = sin_theta < -1.0f ? -1.0f : (sin_theta > 1.0f ? 1.0f : sin_theta);
+  float cc = cos_theta < -1.0f ? -1.0f : (cos_theta > 1.0f ? 1.0f : cos_theta);
+  float lx = sc * math::cosf_glibc(phi), ly = sc * math::sinf_glibc(phi), lz = cc;
+  float n2 = lx * lx + (ly * ly + lz * lz);  // local.normalize()
+  if (n2 > 0.0f) {
+    float s = sqrtf(n2);
+    lx = lx / s;
+    ly = ly / s;
+    lz = lz / s;
+  }
+  // coordinate_system(w, x, y)
+  float sign = copysignf(1.0f, w[2]);
+  float a = -1.0f / (sign + w[2]);
+  float b = w[0] * w[1] * a;
+  float X0 = 1.0f + sign * a * (w[0] * w[0]), X1 = sign * b, X2 = -sign * w[0];
+  float Y0 = b, Y1 = sign + a * (w[1] * w[1]), Y2 = -w[1];
+  out[0] = (lx * X0 + ly * Y0) + lz * w[0];
+  out[1] = (lx * X1 + ly * Y1) + lz * w[1];
+  out[2] = (lx * X2 + ly * Y2) + lz * w[2];
+}
+
+__host__ __device__ __forceinline__ float hg_eval(float cos_theta, float g) {
+  float den = 1.0f + g * g + 2.0f * g * cos_theta;
+  const float inv_4_pi = (float)(0.318309886183790671537767526745028724 / 4.0);  // float(inv_pi / 4.0)
+  return inv_4_pi * (1.0f - g * g) / (den * sqrtf(fmaxf(0.0f, den)));
+}
+
+// ------------------------------------------------------------------------------------------------
+// One iteration of the lane loop.  Env supplies: fetch_job(uint64_t& jid_local) -> bool,
+// jid_begin, film_add(px, py, ratio*L), record(...).
+// ------------------------------------------------------------------------------------------------
+template <class Env>
+__host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane& ln, Env& env) {
+  const DevGrid& G = S.density;
+
+  if (ln.state == ST_FETCH) {
+    uint64_t j;
+    if (!env.fetch_job(j)) {
+      ln.state = ST_DONE;
+      return;
+    }
+    ln.jid_local = j;
+    uint64_t jid = env.jid_begin + j;
+    ln.rng = job_seed(S.seed, jid);
+    uint64_t tile = jid % S.T;
+    ln.x0 = (int32_t)(tile % S.ntx) * S.tw;  // TileProvider::compute_tile_rect
+    ln.y0 = (int32_t)(tile / S.ntx) * S.th;
+    ln.rw = min(S.W - ln.x0, S.tw);
+    ln.rh = min(S.H - ln.y0, S.th);
+    ln.pix = 0;
+    ln.temp.valid = 0;
+    ln.state = ST_PIXEL;
+  }
+
+  if (ln.state == ST_PIXEL) {
+    // Skip pixels filtered by single_pixel mode without any draw (worker.cpp:113-116).
+    while (true) {
+      if (ln.pix >= ln.rw * ln.rh) {
+        ln.state = ST_FETCH;
+        return;
+      }
+      int32_t y = ln.pix / ln.rw, x = ln.pix - y * ln.rw;
+      ln.px = ln.x0 + x;
+      ln.py = ln.y0 + y;
+      ++ln.pix;
+      if (!S.single_pixel_enabled || (ln.px == S.sp_x && ln.py == S.sp_y)) break;
+    }
+    float jx = rng_uniform(ln.rng);
+    float jy = rng_uniform(ln.rng);
+    ln.cnt.rng_draws += 2;
+    jx *= S.jitter_scale;
+    jy *= S.jitter_scale;
+    // Camera::generate_ray (camera.hpp:14-23)
+    float rx = ((float)ln.px + 0.5f) + jx, ry = ((float)ln.py + 0.5f) + jy;
+    float dv[3];
+    for (int i = 0; i < 3; ++i) dv[i] = S.cam_t[i] + (S.cam_L[i * 3] * rx + (S.cam_L[i * 3 + 1] * ry + S.cam_L[i * 3 + 2] * 0.0f));
+    float n2 = dv[0] * dv[0] + (dv[1] * dv[1] + dv[2] * dv[2]);
+    if (n2 > 0.0f) {
+      float s = sqrtf(n2);
+      dv[0] = dv[0] / s;
+      dv[1] = dv[1] / s;
+      dv[2] = dv[2] / s;
+    }
+    for (int i = 0; i < 3; ++i) {
+      ln.ro[i] = S.cam_pos[i];
+      ln.rd[i] = dv[i];
+      ln.L[i] = 0.0f;
+    }
+    ln.terminated = 0;
+    ln.depth = 0;
+    ln.state = ST_BOUNCE;
+  }
+
+  if (ln.state == ST_BOUNCE) {
+    // for (depth < max_depth) { intersection = vol.intersect(r); if (!intersection) break; ... }
+    if (ln.depth < S.max_depth && begin_ray(G, ln, ln.ro, ln.rd)) {
+      ln.shadow = 0;
+      ln.state = ST_SAMPLE;
+    } else {
+      ln.state = ST_FINISH;
+    }
+  }
+
+  if (ln.state == ST_SAMPLE) {
+    bool none = false, hit = false;
+    if (ln.sm == SM_NEED_SEG) {
+      // RayMajorantIterator::next prologue (volume.cpp:40-51)
+      if (ln.T0 >= ln.T1) {
+        none = true;
+      } else {
+        ln.s_t0 = ln.T0;
+        if (ln.maj != ln.maj) ln.maj = majorant_of(cell_at(G, ln.vox[0], ln.vox[1], ln.vox[2]));
+        ln.sm = SM_STEP;
+      }
+    }
+    if (ln.sm == SM_STEP && !none) {
+      if (hdda_step(G, ln)) {
+        ++ln.cnt.segments;
+        ln.sm = (ln.s_dmaj <= 0.0f) ? SM_NEED_SEG : SM_DRAW;  // empty segment: no draw (:32-35)
+      }
+    }
+    if (ln.sm == SM_DRAW && !none) {
+      // MajorantTransmittanceSampler::next body (majorant_transmittance_sampler.cpp:39-79)
+      float sigma_maj = ln.s_dmaj * S.sigma_t;
+      float u = rng_uniform(ln.rng);
+      ++ln.cnt.draws;
+      ++ln.cnt.rng_draws;
+      float dt_m = -math::logf_glibc(1 - u) / sigma_maj;
+      float t = ln.s_t0 + dt_m / ln.scale;
+      if (t < ln.s_t1) {
+        ln.s_t0 = t;
+        float pi_x = ln.e[0] + ln.d[0] * t, pi_y = ln.e[1] + ln.d[1] * t, pi_z = ln.e[2] + ln.d[2] * t;
+        float dens;
+        ++ln.cnt.density_evals;
+        if (trilinear(G, ln.dens, pi_x, pi_y, pi_z, dens)) ++ln.cnt.stencils;
+        if (dens > 0.0f) {
+          map_fwd(G, pi_x, pi_y, pi_z, ln.cp[0], ln.cp[1], ln.cp[2]);
+          ln.c_sigma_maj = sigma_maj;
+          ln.c_density = dens;
+          hit = true;
+        }
+      } else {
+        ln.sm = SM_NEED_SEG;
+      }
+    }
+
+    if (hit && !ln.shadow) {
+      // worker.cpp:148-188
+      float p_a = (S.sigma_a * ln.c_density) / ln.c_sigma_maj;
+      float p_s = (S.sigma_s * ln.c_density) / ln.c_sigma_maj;
+      float p_n = fmaxf(1.0f - p_a - p_s, 0.0f);
+      if (S.has_temperature) {
+        float tx, ty, tz, tadim, X, Y, Z;
+        map_inv(S.temperature, ln.cp[0], ln.cp[1], ln.cp[2], tx, ty, tz);
+        if (trilinear(S.temperature, ln.temp, tx, ty, tz, tadim)) ++ln.cnt.temp_stencils;
+        float tK = tadim * S.temp_scale + S.temp_offset;
+        blackbody_xyz(S, tK, X, Y, Z);
+        float sc = p_a * S.le_scale;
+        ln.L[0] = ln.L[0] + sc * X;
+        ln.L[1] = ln.L[1] + sc * Y;
+        ln.L[2] = ln.L[2] + sc * Z;
+      }
+      float ue = rng_uniform(ln.rng);
+      ++ln.cnt.rng_draws;
+      // sample_discrete({Null p_n, Absorption p_a, Scatter p_s}, u) (random.hpp:30-47)
+      float total = ((0.0f + p_n) + p_a) + p_s;
+      float uu = ue * total;
+      int ev;
+      uu -= p_n;
+      if (uu <= 0) {
+        ev = 0;
+      } else {
+        uu -= p_a;
+        ev = (uu <= 0) ? 1 : 2;
+      }
+      if (ev == 1) {
+        ln.terminated = 1;
+        ln.state = ST_FINISH;
+      } else if (ev == 2) {
+        if (ln.depth++ >= S.max_depth) {
+          ln.terminated = 1;
+          ln.state = ST_FINISH;
+        } else {
+          ++ln.cnt.scatters;
+          for (int i = 0; i < 3; ++i) ln.sp[i] = ln.cp[i];
+          // sample_Ld (worker.cpp:52-90)
+          if (S.li_zero) {
+            ln.Tr = -1.0f;  // returns Li == 0 without draws
+            ln.state = ST_NEE_DONE;
+          } else {
+            ln.Tr = 1.0f;
+            if (begin_ray(G, ln, ln.sp, S.wi)) {
+              ++ln.cnt.shadow_rays;
+              ln.shadow = 1;
+            } else {
+              ln.state = ST_NEE_DONE;
+            }
+          }
+        }
+      }
+      // ev == 0 (Null): keep drawing in the same segment.
+    } else if (hit) {
+      // Ratio tracking with Russian roulette (worker.cpp:68-85)
+      float sigma_n = fmaxf(0.0f, ln.c_sigma_maj - S.sigma_t * ln.c_density);
+      ln.Tr *= sigma_n / ln.c_sigma_maj;
+      if (ln.Tr <= 0.05f) {
+        float q = 0.75f;
+        ++ln.cnt.rng_draws;
+        if (rng_uniform(ln.rng) < q)
+          ln.Tr = 0.0f;
+        else
+          ln.Tr /= 1 - q;
+      }
+      if (ln.Tr <= 0.0f) {
+        ln.Tr = -1.0f;  // returns Zero()
+        ln.state = ST_NEE_DONE;
+      }
+    }
+
+    if (none) {
+      if (ln.shadow)
+        ln.state = ST_NEE_DONE;
+      else
+        ln.state = ST_FINISH;  // the sampler ran dry without scattering: break
+    }
+  }
+
+  if (ln.state == ST_NEE_DONE) {
+    if (ln.Tr >= 0.0f) {
+      // p * T_ray * Li with p = HG(w . wi)
+      float c = ln.rd[0] * S.wi[0] + (ln.rd[1] * S.wi[1] + ln.rd[2] * S.wi[2]);
+      float p = hg_eval(c, S.g_hg);
+      float pt = p * ln.Tr;
+      ln.L[0] = ln.L[0] + pt * S.Li[0];
+      ln.L[1] = ln.L[1] + pt * S.Li[1];
+      ln.L[2] = ln.L[2] + pt * S.Li[2];
+    } else {
+      ln.L[0] = ln.L[0] + 0.0f;
+      ln.L[1] = ln.L[1] + 0.0f;
+      ln.L[2] = ln.L[2] + 0.0f;
+    }
+    float u0 = rng_uniform(ln.rng);
+    float u1 = rng_uniform(ln.rng);
+    ln.cnt.rng_draws += 2;
+    float nd[3];
+    sample_hg(ln.rd, u0, u1, S.g_hg, nd);
+    for (int i = 0; i < 3; ++i) {
+      ln.ro[i] = ln.sp[i];
+      ln.rd[i] = nd[i];
+    }
+    ++ln.depth;  // the for-loop increment (worker.cpp:130)
+    ln.shadow = 0;
+    ln.state = ST_BOUNCE;
+  }
+
+  if (ln.state == ST_FINISH) {
+    if (!ln.terminated) {
+      ln.L[0] = ln.L[0] + S.le_inf[0];
+      ln.L[1] = ln.L[1] + S.le_inf[1];
+      ln.L[2] = ln.L[2] + S.le_inf[2];
+    }
+    env.film_add(S, ln);
+    ++ln.cnt.samples;
+    ln.state = ST_PIXEL;
+  }
+}
+
+}  // namespace vpt

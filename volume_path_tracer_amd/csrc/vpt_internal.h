@@ -1,0 +1,42 @@
+// vpt_internal.h — host-side internals shared by the C-ABI translation units.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/vpt_gpu.h"
+#include "vpt_integrator.h"
+
+namespace vpt {
+
+// Thread-local error message behind vpt_last_error().
+int set_error(int code, const std::string& msg);
+
+// A grid flattened for the GPU (host copies; vpt_gpu.hip uploads them).
+struct HostGrid {
+  DevGrid dev{};  // pointers are filled in after upload
+  std::vector<int2> cells8, cells128;
+  std::vector<RootTileDev> root;
+  std::vector<float> bricks;     // [leaf][729]
+  std::vector<float> leaf_max;   // fixed majorants
+};
+
+// Builds the leaf-slot tables and the 9^3 apron brick pool; fixes the majorants
+// (fix_majorants_for_interpolation, volume.cpp:104-160) when fix == true.
+int build_host_grid(const vpt_grid_desc& d, bool fix, int threads, HostGrid& out);
+
+// Host getValue on a built grid (same tables the device reads).
+float host_value_at(const HostGrid& g, int32_t i, int32_t j, int32_t k);
+
+// Fills the scene constants (camera matrix, light terms, ...) for a configuration.
+int build_scene(const vpt_configuration& cfg, DevScene& S);
+
+// Blackbody table from the embedded CIE 1931 data (init_blackbody_radiation_xyz).
+void blackbody_table(float* out_500x3);
+const float* cie_table();  // [471][3]
+float cie_y_integral();
+
+int default_threads();
+
+}  // namespace vpt

@@ -1,0 +1,163 @@
+// vpt_math.h — float transcendentals that reproduce glibc bit for bit on the integrator's inputs.
+//
+// The reference calls std::log / std::sin / std::cos on floats (random.hpp:21, :71-72), i.e.
+// glibc logf/sinf/cosf (glibc >= 2.28: the ARM optimized-routines algorithms; x86-64 selects the
+// -mfma build of the same C source at run time).  On the GPU, ocml's versions differ from glibc in
+// 1-4% of the integrator's inputs, and one flipped bit in a free-flight distance decorrelates
+// the whole path.  These are the same algorithms (same tables, same double-precision operation
+// sequence with fused multiply-adds), so the GPU's IEEE double arithmetic gives glibc's results.
+// tests/test_math_clone.py checks them against the host's glibc over EVERY input the integrator
+// can produce (1 - u and 2*pi*u for all 2^24+ values of uniform<float>()).
+//
+// Used by device code (the integrator kernel) and, through the same header, by a host test.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vpt {
+namespace math {
+
+__host__ __device__ __forceinline__ uint32_t as_u32(float f) {
+  uint32_t u;
+  __builtin_memcpy(&u, &f, 4);
+  return u;
+}
+__host__ __device__ __forceinline__ float as_f32(uint32_t u) {
+  float f;
+  __builtin_memcpy(&f, &u, 4);
+  return f;
+}
+
+// logf: LOGF_TABLE_BITS = 4, polynomial order 4 (glibc sysdeps/ieee754/flt-32/e_logf.c).
+struct LogfTab {
+  double invc, logc;
+};
+__host__ __device__ __forceinline__ LogfTab logf_tab(int i) {
+  // Table entries: 1/c and log(c) for the 16 sub-intervals of [0x3f330000, 2*0x3f330000).
+  switch (i) {
+    case 0: return {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2};
+    case 1: return {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2};
+    case 2: return {0x1.49539f0f010b0p+0, -0x1.01eae7f513a67p-2};
+    case 3: return {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3};
+    case 4: return {0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3};
+    case 5: return {0x1.25e227b0b8ea0p+0, -0x1.1aa2bc79c8100p-3};
+    case 6: return {0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4};
+    case 7: return {0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4};
+    case 8: return {0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5};
+    case 9: return {0x1.0000000000000p+0, 0x0.0p+0};
+    case 10: return {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5};
+    case 11: return {0x1.ca4b31f026aa0p-1, 0x1.c5e53aa362eb4p-4};
+    case 12: return {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3};
+    case 13: return {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d224770p-3};
+    case 14: return {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2};
+    default: return {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2};
+  }
+}
+
+// glibc logf for x > 0 finite (the integrator only takes log(1 - u), u in [0, 1 - 2^-24]).
+__host__ __device__ __forceinline__ float logf_glibc(float x) {
+  const double Ln2 = 0x1.62e42fefa39efp-1;
+  const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2, A2 = -0x1.ffffef20a4123p-2;
+  uint32_t ix = as_u32(x);
+  if (ix == 0x3f800000u) return 0.0f;
+  if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
+    // zero / subnormal / inf / nan / negative
+    if (ix * 2 == 0) return -__builtin_inff();
+    if (ix == 0x7f800000u) return x;
+    if ((ix & 0x80000000u) || ix * 2 >= 0xff000000u) return __builtin_nanf("");
+    ix = as_u32(x * 0x1p23f);
+    ix -= 23u << 23;
+  }
+  uint32_t tmp = ix - 0x3f330000u;
+  int i = (int)((tmp >> (23 - 4)) % 16u);
+  int k = (int32_t)tmp >> 23;
+  uint32_t iz = ix - (tmp & (0x1ffu << 23));
+  LogfTab t = logf_tab(i);
+  double z = (double)as_f32(iz);
+  double r = __builtin_fma(z, t.invc, -1.0);
+  double y0 = __builtin_fma((double)k, Ln2, t.logc);
+  double r2 = r * r;
+  double y = __builtin_fma(A1, r, A2);
+  y = __builtin_fma(A0, r2, y);
+  y = __builtin_fma(y, r2, y0 + r);
+  return (float)y;
+}
+
+// sinf / cosf (glibc sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c, sincosf.h), for |x| < 120.
+struct SinCosTab {
+  double sign0, sign1, sign2, sign3, hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4;
+};
+__host__ __device__ __forceinline__ SinCosTab sincos_tab(int which) {
+  if (which == 0)
+    return {1.0, -1.0, -1.0, 1.0, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, 0x1p0, -0x1.ffffffd0c621cp-2,
+            -0x1.555545995a603p-3, 0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10,
+            -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16};
+  return {1.0, -1.0, -1.0, 1.0, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, -0x1p0, 0x1.ffffffd0c621cp-2,
+          -0x1.555545995a603p-3, -0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10,
+          -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16};
+}
+__host__ __device__ __forceinline__ uint32_t abstop12(float x) { return (as_u32(x) >> 20) & 0x7ff; }
+__host__ __device__ __forceinline__ float sinf_poly(double x, double x2, const SinCosTab& p, int n) {
+  if ((n & 1) == 0) {
+    double x3 = x * x2;
+    double s1 = __builtin_fma(x2, p.s3, p.s2);
+    double x7 = x3 * x2;
+    double s = __builtin_fma(x3, p.s1, x);
+    return (float)__builtin_fma(x7, s1, s);
+  }
+  double x4 = x2 * x2;
+  double c2 = __builtin_fma(x2, p.c4, p.c3);
+  double c1 = __builtin_fma(x2, p.c1, p.c0);
+  double x6 = x4 * x2;
+  double c = __builtin_fma(x4, p.c2, c1);
+  return (float)__builtin_fma(x6, c2, c);
+}
+__host__ __device__ __forceinline__ double reduce_fast(double x, const SinCosTab& p, int* np) {
+  double r = x * p.hpi_inv;
+  int n = ((int32_t)r + 0x800000) >> 24;
+  *np = n;
+  return __builtin_fma(-(double)n, p.hpi, x);
+}
+__host__ __device__ __forceinline__ double quadrant_sign(const SinCosTab& p, int n) {
+  switch (n & 3) {
+    case 0: return p.sign0;
+    case 1: return p.sign1;
+    case 2: return p.sign2;
+    default: return p.sign3;
+  }
+}
+// Valid for finite |y| < 120 (the integrator calls it with phi = 2*pi*u in [0, 2*pi)).
+__host__ __device__ __forceinline__ float sinf_glibc(float y) {
+  const uint32_t pio4_top = 0x3f4u;  // abstop12(0x1.921fb6p-1f)
+  double x = y;
+  if (abstop12(y) < pio4_top) {
+    double s = x * x;
+    if (abstop12(y) < 0x398u) return y;  // abstop12(0x1p-12f)
+    return sinf_poly(x, s, sincos_tab(0), 0);
+  }
+  int n;
+  SinCosTab p0 = sincos_tab(0);
+  x = reduce_fast(x, p0, &n);
+  double s = quadrant_sign(p0, n);
+  SinCosTab p = (n & 2) ? sincos_tab(1) : p0;
+  return sinf_poly(x * s, x * x, p, n);
+}
+__host__ __device__ __forceinline__ float cosf_glibc(float y) {
+  const uint32_t pio4_top = 0x3f4u;
+  double x = y;
+  if (abstop12(y) < pio4_top) {
+    double x2 = x * x;
+    if (abstop12(y) < 0x398u) return 1.0f;
+    return sinf_poly(x, x2, sincos_tab(0), 1);
+  }
+  int n;
+  SinCosTab p0 = sincos_tab(0);
+  x = reduce_fast(x, p0, &n);
+  double s = quadrant_sign(p0, n);
+  SinCosTab p = (n & 2) ? sincos_tab(1) : p0;
+  return sinf_poly(x * s, x * x, p, n ^ 1);
+}
+
+}  // namespace math
+}  // namespace vpt
