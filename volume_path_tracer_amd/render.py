@@ -1,0 +1,186 @@
+"""Host driver: the reference's work-distribution API over the HIP integrator.
+
+``TileProvider`` restates include/vpt/tile_provider.hpp / src/tile_provider.cpp (job id -> (tile,
+wave), wave bookkeeping, stop_at_next_wave, progress/ETA).  ``run`` is the drop-in for
+``vpt::run`` (src/worker.cpp:92-208): instead of tracing one token at a time on a CPU thread, it
+drains the provider in contiguous job-id batches and launches each batch on the GPU.  Job ids key
+the RNG streams (hash(seed, jid)), so the batching does not change any sample.
+
+Device memory (film, per-sample records) is plain torch CUDA tensors — torch is plumbing here; the
+integrator itself is the HIP kernel in libvpt_amd.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import threading
+import time
+from typing import Optional
+
+import numpy as np
+
+from . import capi
+
+
+def ceildiv(a: int, b: int) -> int:
+    return a // b + (a % b != 0)
+
+
+class TileProvider:
+    """tile_provider.cpp:14-111 — job index -> (tile, wave); waves start when first touched."""
+
+    def __init__(self, img_size, waves: int, tile_size):
+        self.img_w, self.img_h = int(img_size[0]), int(img_size[1])
+        self.tile_w, self.tile_h = int(tile_size[0]), int(tile_size[1])
+        self.ntx, self.nty = ceildiv(self.img_w, self.tile_w), ceildiv(self.img_h, self.tile_h)
+        self.num_tiles = self.ntx * self.nty
+        self.requested_waves = int(waves)
+        self.max_wave_idx = 0
+        self._job_idx = 0
+        self._force_stop = False
+        self._lock = threading.Lock()
+        self._start = time.monotonic()
+
+    # token next() without per-tile wave gating: on the GPU the film adds are atomics, so two
+    # waves of a tile may be in flight together (the reference serialises them, tile_provider.cpp:40-60).
+    def next_batch(self, max_jobs: int):
+        """Reserve up to max_jobs consecutive job ids: (jid_begin, count), count 0 when done."""
+        with self._lock:
+            if self._force_stop:
+                return self._job_idx, 0
+            end = self.requested_waves * self.num_tiles
+            begin = self._job_idx
+            count = max(0, min(max_jobs, end - begin))
+            self._job_idx += count
+            if count:
+                self.max_wave_idx = max(self.max_wave_idx, 1 + (begin + count - 1) // self.num_tiles)
+            return begin, count
+
+    def job(self, jid: int):
+        """(tile, wave) of a job id (tile_provider.cpp:30-31)."""
+        return jid % self.num_tiles, 1 + jid // self.num_tiles
+
+    def compute_tile_rect(self, tile: int):
+        """tile_provider.cpp:95-105 -> (x0, y0, w, h)."""
+        x0 = (tile % self.ntx) * self.tile_w
+        y0 = (tile // self.ntx) * self.tile_h
+        return x0, y0, min(self.img_w - x0, self.tile_w), min(self.img_h - y0, self.tile_h)
+
+    def stop_at_next_wave(self):
+        """tile_provider.cpp:107-110: requested_waves = the highest wave already started."""
+        with self._lock:
+            self.requested_waves = self.max_wave_idx
+
+    def stop_now(self):
+        self._force_stop = True
+
+    def reset_eta(self):
+        self._start = time.monotonic()
+
+    def progress_ratio(self) -> float:
+        total = self.requested_waves * self.num_tiles
+        return self._job_idx / total if total else 1.0
+
+    def progress(self) -> int:
+        return int(self.progress_ratio() * 100.0)
+
+    def eta(self) -> float:
+        p = self.progress_ratio()
+        el = time.monotonic() - self._start
+        return (1 - p) / (p / el) if p > 0 and el > 0 else float("inf")
+
+
+class Integrator:
+    """One HIP context on one device: the flattened grids, scene constants and a film."""
+
+    def __init__(self, cfg: capi.Configuration, density, temperature=None, device: int = 0, blackbody=None):
+        import torch
+
+        self.torch = torch
+        self.cfg = cfg.copy()
+        self.device = int(device)
+        self.dev = torch.device("cuda", self.device)
+        L = capi.lib()
+        h = C.c_void_p()
+        dens_desc = density.desc if hasattr(density, "desc") else density
+        temp_desc = None if temperature is None else (temperature.desc if hasattr(temperature, "desc") else temperature)
+        bb = None
+        if blackbody is not None:
+            bb = np.ascontiguousarray(blackbody, np.float32)
+        capi.check(L.vpt_gpu_create(C.byref(self.cfg), C.byref(dens_desc),
+                                    C.byref(temp_desc) if temp_desc is not None else None,
+                                    bb.ctypes.data_as(C.POINTER(C.c_float)) if bb is not None else None,
+                                    self.device, C.byref(h)), "vpt_gpu_create")
+        self.h = h
+        jpw, tot = C.c_uint64(), C.c_uint64()
+        capi.check(L.vpt_gpu_job_space(h, C.byref(jpw), C.byref(tot)), "vpt_gpu_job_space")
+        self.jobs_per_wave, self.total_jobs = int(jpw.value), int(tot.value)
+        self.film = torch.zeros((self.cfg.height, self.cfg.width, 4), dtype=torch.float32, device=self.dev)
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                capi.lib().vpt_gpu_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def stream_handle(self, stream=None) -> int:
+        s = stream if stream is not None else self.torch.cuda.current_stream(self.dev)
+        return int(s.cuda_stream)
+
+    def render_jobs(self, jid_begin: int, jid_count: int, film=None, records=None, stream=None):
+        """Asynchronously render jobs [jid_begin, jid_begin + jid_count) into `film` (default: own)."""
+        film = self.film if film is None else film
+        assert film.is_cuda and film.dtype == self.torch.float32 and film.is_contiguous()
+        assert film.numel() == self.cfg.height * self.cfg.width * 4
+        L = capi.lib()
+        s = C.c_void_p(self.stream_handle(stream))
+        if records is None:
+            capi.check(L.vpt_gpu_render_jobs(self.h, jid_begin, jid_count, C.c_void_p(film.data_ptr()), s),
+                       "vpt_gpu_render_jobs")
+        else:
+            area = int(self.cfg.tile_size[0] * self.cfg.tile_size[1])
+            assert records.numel() >= jid_count * area * 3 and records.dtype == self.torch.float32
+            capi.check(L.vpt_gpu_render_jobs_records(self.h, jid_begin, jid_count, C.c_void_p(film.data_ptr()),
+                                                     C.c_void_p(records.data_ptr()), s),
+                       "vpt_gpu_render_jobs_records")
+
+    def render_waves(self, first_wave: int, num_waves: int, film=None, stream=None):
+        """Waves are 1-based (tile_provider.cpp:30): wave w covers jids [(w-1)*T, w*T)."""
+        self.render_jobs((first_wave - 1) * self.jobs_per_wave, num_waves * self.jobs_per_wave, film, None, stream)
+
+    def counters(self, reset: bool = False) -> dict:
+        c = capi.Counters()
+        capi.check(capi.lib().vpt_gpu_counters(self.h, C.byref(c), 1 if reset else 0), "vpt_gpu_counters")
+        return c.as_dict()
+
+    def launch_info(self):
+        g, b = C.c_int(), C.c_int()
+        capi.check(capi.lib().vpt_gpu_launch_info(self.h, C.byref(g), C.byref(b)), "vpt_gpu_launch_info")
+        return int(g.value), int(b.value)
+
+    def film_host(self) -> np.ndarray:
+        self.torch.cuda.synchronize(self.dev)
+        return self.film.cpu().numpy()
+
+
+def run(cfg: capi.Configuration, integrator: Integrator, tp: TileProvider, film: Optional[np.ndarray] = None,
+        batch_waves: int = 8) -> np.ndarray:
+    """Drop-in for vpt::run (worker.cpp:92-208): drain `tp` on the GPU and add into `film`
+    (host float32 [H][W][4], the reference's Image<float,4> layout)."""
+    batch = max(1, batch_waves) * tp.num_tiles
+    while True:
+        begin, count = tp.next_batch(batch)
+        if count == 0:
+            break
+        integrator.render_jobs(begin, count)
+    out = integrator.film_host()
+    if film is not None:
+        film += out
+        return film
+    return out
+
+
+def film_to_xyz(film: np.ndarray) -> np.ndarray:
+    """XYZ / W per pixel (main.cpp:15)."""
+    return film[..., :3] / film[..., 3:4]
