@@ -174,7 +174,7 @@ int vpt_gpu_destroy(vpt_gpu_ctx* ctx);
 int vpt_gpu_job_space(const vpt_gpu_ctx* ctx, uint64_t* jobs_per_wave, uint64_t* total_jobs);
 
 /* Render jobs [jid_begin, jid_begin + jid_count) asynchronously on `hip_stream`
- * (a hipStream_t; NULL = the context's own stream), accumulating into `film_device`:
+ * (a hipStream_t; NULL = the null stream, as everywhere in HIP), accumulating into `film_device`:
  * a device float[H][W][4] (X, Y, Z, sample count; image.hpp:40-60) — NULL = the context's own
  * film.  Film adds are fp32 atomics, so the per-pixel sum order may differ from the
  * reference's wave order (≈1e-7 relative). */
@@ -196,6 +196,11 @@ int vpt_gpu_film_device_ptr(vpt_gpu_ctx* ctx, float** film_device, uint64_t* cou
 int vpt_gpu_film_add_to_host(vpt_gpu_ctx* ctx, float* film_host_hxwx4);
 /* Counters summed over every launch since creation (or the last reset). */
 int vpt_gpu_counters(vpt_gpu_ctx* ctx, vpt_counters* out, int reset);
+/* Scheduling knobs (results never depend on them): a rare lane state (new job, new pixel, ray
+ * setup, NEE completion, film write) runs when >= gate_min lanes of a wavefront wait for it or
+ * fewer than gate_idle lanes are sampling; grid_blocks overrides the persistent grid size.
+ * Pass <= 0 (gate_idle < 0) to keep a value. */
+int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_blocks);
 /* Launch geometry used by the integrator kernel (for reports). */
 int vpt_gpu_launch_info(const vpt_gpu_ctx* ctx, int* grid_blocks, int* block_threads);
 

@@ -22,20 +22,21 @@ struct HostEnv {
   float* film;
   float* records;
   int32_t tile_area;
+  int32_t count(bool pred) { return pred ? 1 : 0; }  // one lane
   bool fetch_job(uint64_t& j) {
     if (next >= jid_count) return false;
     j = next++;
     return true;
   }
-  void film_add(const vpt::DevScene& S, const vpt::Lane& ln) {
-    float* f = film + ((int64_t)ln.py * S.W + ln.px) * 4;
+  void film_add(const vpt::DevScene& S, const vpt::Lane& ln, int32_t px, int32_t py, int32_t rw) {
+    float* f = film + ((int64_t)py * S.W + px) * 4;
     f[3] += 1.0f;
     f[0] += S.imaging_ratio * ln.L[0];
     f[1] += S.imaging_ratio * ln.L[1];
     f[2] += S.imaging_ratio * ln.L[2];
     if (records) {
-      int32_t xl = ln.px - ln.x0, yl = ln.py - ln.y0;
-      float* r = records + (ln.jid_local * (uint64_t)tile_area + (uint64_t)(yl * ln.rw + xl)) * 3;
+      int32_t xl = px - ln.x0, yl = py - ln.y0;
+      float* r = records + (ln.jid_local * (uint64_t)tile_area + (uint64_t)(yl * rw + xl)) * 3;
       r[0] = ln.L[0];
       r[1] = ln.L[1];
       r[2] = ln.L[2];
@@ -65,11 +66,16 @@ extern "C" int vpths_render_jobs(const vpt_configuration* cfg, const vpt_grid_de
     vpt::blackbody_table(bb.data());
   S.bb = bb.data();
   S.cie = vpt::cie_table();
+  S.gate_min = 1;
+  S.gate_idle = 1;
   HostEnv env{jid_begin, jid_count, 0, film, records, S.tw * S.th};
   vpt::Lane ln;
   std::memset(&ln, 0, sizeof ln);
-  ln.state = vpt::ST_FETCH;
-  while (ln.state != vpt::ST_DONE) vpt::lane_iteration(S, ln, env);
+  vpt::lane_init(ln);
+  if (temperature)
+    while (ln.state != vpt::ST_DONE) vpt::lane_iteration<true, true>(S, ln, env);
+  else
+    while (ln.state != vpt::ST_DONE) vpt::lane_iteration<false, true>(S, ln, env);
   if (counters) {
     counters->samples += ln.cnt.samples;
     counters->dda_steps += ln.cnt.dda_steps;

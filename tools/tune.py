@@ -1,0 +1,32 @@
+"""GPU tuning sweep (timing only): C3 frames at reduced spp under scheduling knobs / library builds.
+    python tools/tune.py --spp 8 --gates 1:1,16:16 [--lib path]"""
+import argparse, json, os, sys, time
+from pathlib import Path
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+ap = argparse.ArgumentParser()
+ap.add_argument("--spp", type=int, default=8)
+ap.add_argument("--config", default="c3")
+ap.add_argument("--gates", default="16:16")
+ap.add_argument("--blocks", default="0")
+ap.add_argument("--reps", type=int, default=2)
+a = ap.parse_args()
+import torch
+from volume_path_tracer_amd.render import Integrator
+from volume_path_tracer_amd.scenes import SynthGrid, workload
+wl = workload(a.config, spp=a.spp)
+dg = SynthGrid(wl.density_kind, wl.grid_n); tg = SynthGrid(2, wl.grid_n) if wl.temperature else None
+it = Integrator(wl.cfg, dg.grid(copy=False), tg.grid(copy=False) if tg else None)
+base_blocks = it.launch_info()[0]
+it.render_waves(1, 1); torch.cuda.synchronize()
+for g in a.gates.split(","):
+    gm, gi = map(int, g.split(":"))
+    for b in map(int, a.blocks.split(",")):
+        it.set_tuning(gm, gi, b if b > 0 else base_blocks)
+        best = 1e9
+        for _ in range(a.reps):
+            it.film.zero_(); torch.cuda.synchronize(); t = time.perf_counter()
+            it.render_waves(1, a.spp); torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t)
+        ms = best * 1e3
+        print(json.dumps({"lib": os.environ.get("VPT_LIB", "default"), "gate": g, "blocks": b or base_blocks,
+                          "spp": a.spp, "ms": round(ms, 2), "Msps": round(wl.cfg.width * wl.cfg.height * a.spp / best / 1e6, 2)}), flush=True)

@@ -14,7 +14,7 @@ import numpy as np
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_DIR = PKG_DIR / "lib"
-LIB_PATH = LIB_DIR / "libvpt_amd.so"
+LIB_PATH = Path(os.environ["VPT_LIB"]) if os.environ.get("VPT_LIB") else LIB_DIR / "libvpt_amd.so"
 
 VPT_OK = 0
 VPT_BLACKBODY_ROWS = 500
@@ -209,6 +209,7 @@ def lib() -> C.CDLL:
     L.vpt_gpu_film_device_ptr.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_uint64)]
     L.vpt_gpu_film_add_to_host.argtypes = [vp, fp]
     L.vpt_gpu_counters.argtypes = [vp, C.POINTER(Counters), C.c_int]
+    L.vpt_gpu_set_tuning.argtypes = [vp, C.c_int, C.c_int, C.c_int]
     L.vpt_gpu_launch_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.vpt_last_error.restype = C.c_char_p
     L.vpt_synth_grid.argtypes = [C.c_int, C.c_int]

@@ -34,6 +34,11 @@ int set_error(int code, const std::string& msg) {
 
 constexpr int kCounterCount = 10;
 constexpr int kBlockThreads = 256;
+#ifdef VPT_LB
+#define VPT_LB_ARG , VPT_LB
+#else
+#define VPT_LB_ARG
+#endif
 
 struct KernelEnv {
   uint64_t jid_begin;
@@ -43,22 +48,24 @@ struct KernelEnv {
   float* records;
   int32_t tile_area;
 
+  // lanes of this wavefront for which pred holds
+  __device__ __forceinline__ int32_t count(bool pred) { return (int32_t)__popcll(__ballot(pred)); }
   __device__ __forceinline__ bool fetch_job(uint64_t& j) {
     unsigned long long v = atomicAdd(job_counter, 1ULL);
     if (v >= jid_count) return false;
     j = v;
     return true;
   }
-  __device__ __forceinline__ void film_add(const DevScene& S, const Lane& ln) {
-    float* f = film + ((int64_t)ln.py * S.W + ln.px) * 4;
+  __device__ __forceinline__ void film_add(const DevScene& S, const Lane& ln, int32_t px, int32_t py, int32_t rw) {
+    float* f = film + ((int64_t)py * S.W + px) * 4;
     const float r = S.imaging_ratio;
     atomicAdd(f + 3, 1.0f);
     atomicAdd(f + 0, r * ln.L[0]);
     atomicAdd(f + 1, r * ln.L[1]);
     atomicAdd(f + 2, r * ln.L[2]);
     if (records) {
-      const int32_t xl = ln.px - ln.x0, yl = ln.py - ln.y0;
-      float* rec = records + (ln.jid_local * (uint64_t)tile_area + (uint64_t)(yl * ln.rw + xl)) * 3;
+      const int32_t xl = px - ln.x0, yl = py - ln.y0;
+      float* rec = records + (ln.jid_local * (uint64_t)tile_area + (uint64_t)(yl * rw + xl)) * 3;
       rec[0] = ln.L[0];
       rec[1] = ln.L[1];
       rec[2] = ln.L[2];
@@ -66,20 +73,18 @@ struct KernelEnv {
   }
 };
 
-__global__ __launch_bounds__(kBlockThreads) void vpt_integrate_kernel(DevScene S, KernelEnv env,
+// counters[] order = vpt_counters field order
+template <bool HasTemp, bool Debug>
+__global__ __launch_bounds__(kBlockThreads VPT_LB_ARG) void vpt_integrate_kernel(DevScene S, KernelEnv env,
                                                                        unsigned long long* counters) {
   Lane ln;
-  ln.state = ST_FETCH;
-  ln.sm = SM_NEED_SEG;
-  ln.dens.valid = 0;
-  ln.temp.valid = 0;
-  ln.cnt = LaneCounters{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  while (ln.state != ST_DONE) lane_iteration(S, ln, env);
-  const uint32_t c[kCounterCount] = {ln.cnt.samples, ln.cnt.dda_steps, ln.cnt.segments, ln.cnt.draws,
-                                     ln.cnt.stencils, ln.cnt.density_evals, ln.cnt.temp_stencils,
-                                     ln.cnt.scatters, ln.cnt.shadow_rays, ln.cnt.rng_draws};
+  lane_init(ln);
+  while (ln.state != ST_DONE) lane_iteration<HasTemp, Debug>(S, ln, env);
+  const LaneCounters& c = ln.cnt;
+  const uint32_t v[kCounterCount] = {c.samples, c.dda_steps, c.segments, c.draws, c.stencils,
+                                     c.density_evals, c.temp_stencils, c.scatters, c.shadow_rays, c.rng_draws};
   for (int i = 0; i < kCounterCount; ++i)
-    if (c[i]) atomicAdd(counters + i, (unsigned long long)c[i]);
+    if (v[i]) atomicAdd(counters + i, (unsigned long long)v[i]);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -169,7 +174,7 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   if (jid_count == 0) return VPT_OK;
   const uint64_t total = ctx->scene.T * (uint64_t)ctx->cfg.num_waves;
   (void)total;  // jids beyond num_waves are valid jobs too (TileProvider only stops at requested_waves)
-  hipStream_t s = stream_ptr ? (hipStream_t)stream_ptr : ctx->stream;
+  hipStream_t s = (hipStream_t)stream_ptr;  // NULL = the null stream (HIP convention)
   vpt::KernelEnv env;
   env.jid_begin = jid_begin;
   env.jid_count = jid_count;
@@ -178,8 +183,10 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.records = records;
   env.tile_area = ctx->scene.tw * ctx->scene.th;
   VPT_HIP(hipMemsetAsync(ctx->job_counter, 0, sizeof(unsigned long long), s));
-  hipLaunchKernelGGL(vpt::vpt_integrate_kernel, dim3(ctx->grid_blocks), dim3(vpt::kBlockThreads), 0, s, ctx->scene,
-                     env, ctx->counters);
+  const bool temp = ctx->scene.has_temperature != 0, dbg = records != nullptr;
+  auto kernel = temp ? (dbg ? vpt::vpt_integrate_kernel<true, true> : vpt::vpt_integrate_kernel<true, false>)
+                     : (dbg ? vpt::vpt_integrate_kernel<false, true> : vpt::vpt_integrate_kernel<false, false>);
+  hipLaunchKernelGGL(kernel, dim3(ctx->grid_blocks), dim3(vpt::kBlockThreads), 0, s, ctx->scene, env, ctx->counters);
   VPT_HIP(hipGetLastError());
   return VPT_OK;
 }
@@ -243,10 +250,15 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
 
   // Persistent grid: as many blocks as are resident at once.
   int per_cu = 0, cus = 0;
-  VPT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, vpt::vpt_integrate_kernel, vpt::kBlockThreads, 0));
+  // sized for the production kernel of this scene; the debug variant is launched with the same grid
+  VPT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &per_cu, temperature ? vpt::vpt_integrate_kernel<true, false> : vpt::vpt_integrate_kernel<false, false>,
+      vpt::kBlockThreads, 0));
   VPT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
   if (per_cu < 1) per_cu = 1;
   ctx->grid_blocks = per_cu * cus;
+  ctx->scene.gate_min = 16;  // rare states run when a quarter of the wavefront waits for them
+  ctx->scene.gate_idle = 16;
   *out = ctx.release();
   return VPT_OK;
 }
@@ -318,6 +330,14 @@ int vpt_gpu_counters(vpt_gpu_ctx* ctx, vpt_counters* out, int reset) {
   uint64_t* o = reinterpret_cast<uint64_t*>(out);
   for (int i = 0; i < vpt::kCounterCount; ++i) o[i] = c[i];
   if (reset) VPT_HIP(hipMemset(ctx->counters, 0, sizeof c));
+  return VPT_OK;
+}
+
+int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_blocks) {
+  if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
+  if (gate_min > 0) ctx->scene.gate_min = gate_min;
+  if (gate_idle >= 0) ctx->scene.gate_idle = gate_idle;
+  if (grid_blocks > 0) ctx->grid_blocks = grid_blocks;
   return VPT_OK;
 }
 

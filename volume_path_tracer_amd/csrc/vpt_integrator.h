@@ -90,50 +90,51 @@ __host__ __device__ __forceinline__ float value_at(const DevGrid& g, int32_t i, 
   return g.bricks[(int64_t)c.code * kBrickVox + (i & 7) * 81 + (j & 7) * 9 + (k & 7)];
 }
 
-// nanovdb::math::SampleFromVoxels<Acc,1,true> stencil cache (values identical with or without it).
-struct Stencil {
+// nanovdb::math::SampleFromVoxels<Acc,1,true> caches the 2x2x2 stencil of the last cell; the cache
+// never changes a value, and on the cloud it hits < 2% of evaluations, so the device re-reads the
+// stencil every time and only remembers the last cell to count refreshes (algorithmic bytes).
+struct StencilCell {
   int32_t i, j, k;
-  int32_t valid;
-  float v[8];  // v[a*4 + b*2 + c] = value(i+a, j+b, k+c)
 };
 
-__host__ __device__ __forceinline__ void fetch_stencil(const DevGrid& g, Stencil& s, int32_t i, int32_t j, int32_t k) {
-  s.i = i;
-  s.j = j;
-  s.k = k;
-  s.valid = 1;
+__host__ __device__ __forceinline__ void fetch_stencil(const DevGrid& g, int32_t i, int32_t j, int32_t k, float v[8]) {
   Cell c = cell_at(g, i, j, k);
   if (c.code >= 0) {
     // Corner cell inside a leaf: the 9^3 apron brick holds the whole 2^3 stencil.
     const float* b = g.bricks + (int64_t)c.code * kBrickVox + (i & 7) * 81 + (j & 7) * 9 + (k & 7);
-    s.v[0] = b[0];
-    s.v[1] = b[1];
-    s.v[2] = b[9];
-    s.v[3] = b[10];
-    s.v[4] = b[81];
-    s.v[5] = b[82];
-    s.v[6] = b[90];
-    s.v[7] = b[91];
+    v[0] = b[0];
+    v[1] = b[1];
+    v[2] = b[9];
+    v[3] = b[10];
+    v[4] = b[81];
+    v[5] = b[82];
+    v[6] = b[90];
+    v[7] = b[91];
   } else {
     for (int a = 0; a < 2; ++a)
       for (int b = 0; b < 2; ++b)
-        for (int cc = 0; cc < 2; ++cc) s.v[a * 4 + b * 2 + cc] = value_at(g, i + a, j + b, k + cc);
+        for (int cc = 0; cc < 2; ++cc) v[a * 4 + b * 2 + cc] = value_at(g, i + a, j + b, k + cc);
   }
 }
 
 // TrilinearSampler::sample: lerp(a, b, w) = a + w * (b - a), z then y then x.
 __host__ __device__ __forceinline__ float lerpf(float a, float b, float w) { return a + w * (b - a); }
-// Returns true when the stencil had to be (re)fetched.
-__host__ __device__ __forceinline__ bool trilinear(const DevGrid& g, Stencil& s, float x, float y, float z, float& out) {
+// Returns true when the cell differs from the previous evaluation (a NanoVDB stencil refresh).
+__host__ __device__ __forceinline__ bool trilinear(const DevGrid& g, StencilCell& last, float x, float y, float z,
+                                                   float& out) {
   float fi = floorf(x), fj = floorf(y), fk = floorf(z);
   float u = x - fi, v = y - fj, w = z - fk;
   int32_t i = (int32_t)fi, j = (int32_t)fj, k = (int32_t)fk;
-  bool refresh = !s.valid || i != s.i || j != s.j || k != s.k;
-  if (refresh) fetch_stencil(g, s, i, j, k);
-  out = lerpf(lerpf(lerpf(s.v[0], s.v[1], w), lerpf(s.v[2], s.v[3], w), v),
-              lerpf(lerpf(s.v[4], s.v[5], w), lerpf(s.v[6], s.v[7], w), v), u);
+  bool refresh = i != last.i || j != last.j || k != last.k;
+  last.i = i;
+  last.j = j;
+  last.k = k;
+  float s[8];
+  fetch_stencil(g, i, j, k, s);
+  out = lerpf(lerpf(lerpf(s[0], s[1], w), lerpf(s[2], s[3], w), v), lerpf(lerpf(s[4], s[5], w), lerpf(s[6], s[7], w), v), u);
   return refresh;
 }
+constexpr int32_t kNoCell = (int32_t)0x80000000;  // "no previous cell" (reset per sampler instance)
 
 // nanovdb Map: matMult with fmaf.
 __host__ __device__ __forceinline__ void map_inv(const DevGrid& g, float x, float y, float z, float& ox, float& oy, float& oz) {
@@ -180,6 +181,9 @@ struct DevScene {
   int32_t li_zero;      // Li == 0 -> sample_Ld returns before any draw (worker.cpp:57-58)
   float wi[3];          // distant_light.inv_direction.normalized() (worker.cpp:54)
   float sigma_a, sigma_s, sigma_t, g_hg, le_scale, temp_scale, temp_offset;
+  // Wave gating of the rare states: a rare block runs when at least gate_min lanes of the wavefront
+  // wait for it, or when fewer than gate_idle lanes are sampling (1/64 = always run).
+  int32_t gate_min, gate_idle;
   const float* bb;      // blackbody table [501][3] (row 500 = 0)
   const float* cie;     // [471][3] for T >= 49900 K
   float y_integral;
@@ -271,7 +275,7 @@ __host__ __device__ inline void blackbody_xyz(const DevScene& S, float t, float&
 enum : int32_t {
   ST_FETCH = 0,   // take the next job
   ST_PIXEL = 1,   // start the next pixel of the tile
-  ST_BOUNCE = 2,  // top of the depth loop: intersect the current primary ray
+  ST_RAY = 2,     // Volume::intersect + iterator setup: primary ray (top of the depth loop) or shadow ray
   ST_SAMPLE = 3,  // inside MajorantTransmittanceSampler::next (primary or shadow ray)
   ST_NEE_DONE = 4,
   ST_FINISH = 5,  // pixel done: environment light, film
@@ -279,37 +283,38 @@ enum : int32_t {
 };
 enum : int32_t { SM_NEED_SEG = 0, SM_STEP = 1, SM_DRAW = 2 };
 
+// Event counters.  The production kernel keeps the four that price algorithmic bytes
+// (SURVEY §8d); the debug kernel (per-sample records) keeps all of them for parity checks.
 struct LaneCounters {
-  uint32_t samples, dda_steps, segments, draws, stencils, density_evals, temp_stencils, scatters, shadow_rays,
-      rng_draws;
+  uint32_t samples, dda_steps, stencils, temp_stencils;
+  uint32_t segments, draws, density_evals, scatters, shadow_rays, rng_draws;
 };
 
 struct Lane {
-  int32_t state, sm;
-  uint64_t jid_local;  // job index relative to jid_begin
+  int32_t state, sm, shadow, terminated;
   uint64_t rng;
-  int32_t x0, y0, rw, rh, pix, px, py;
+  uint64_t jid_local;  // job index relative to jid_begin (records only)
+  int32_t x0, y0, pix;
   uint32_t depth;
-  int32_t terminated, shadow;
   float L[3];
-  float ro[3], rd[3];  // current primary world ray
-  float sp[3];         // scatter point (world) while the shadow ray runs
-  float Tr;            // shadow-ray transmittance
-  // RayMajorantIterator: index-space ray, scale, majorant, HDDA
+  float ro[3], rd[3];  // current primary world ray; ro is also the scatter point during NEE
+  float Tr;            // shadow-ray transmittance (< 0: sample_Ld returns zero)
+  // RayMajorantIterator: index-space ray, scale, majorant, HDDA (NanoVDB math::HDDA state)
   float e[3], d[3], inv[3];
   float scale, maj;
   int32_t dim;
   float T0, T1;
-  float nxt[3], dlt[3];
-  int32_t vox[3], stp[3];
+  float nxt[3];
+  int32_t vox[3];
   // current majorant segment
   float s_t0, s_t1, s_dmaj;
-  // collision record (MediumProperties)
-  float cp[3], c_sigma_maj, c_density;
-  Stencil dens;
-  Stencil temp;
+  StencilCell dens_cell, temp_cell;
   LaneCounters cnt;
 };
+
+// HDDA step direction and per-cell increment from the (normalised, index-space) direction:
+// step = 0 if dir == 0, +1 if invDir > 0, else -1; delta = |invDir| (NanoVDB HDDA::init).
+__host__ __device__ __forceinline__ int32_t hdda_stp(float d, float inv) { return d == 0.0f ? 0 : (inv > 0 ? 1 : -1); }
 
 // Volume::intersect (volume.cpp:78-88) + RayMajorantIterator ctor (volume.cpp:90-98).
 __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, const float o[3], const float dir[3]) {
@@ -364,22 +369,15 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
   for (int a = 0; a < 3; ++a) {
     int32_t v = ((int32_t)floorf(P[a])) & (~(dim - 1));
     ln.vox[a] = v;
-    if (D[a] == 0.0f) {
+    if (D[a] == 0.0f)
       ln.nxt[a] = 3.40282347e+38f;
-      ln.stp[a] = 0;
-      ln.dlt[a] = 0.0f;
-    } else if (I[a] > 0) {
-      ln.stp[a] = 1;
+    else if (I[a] > 0)
       ln.nxt[a] = t0 + ((float)(v + dim) - P[a]) * I[a];
-      ln.dlt[a] = I[a];
-    } else {
-      ln.stp[a] = -1;
+    else
       ln.nxt[a] = t0 + ((float)v - P[a]) * I[a];
-      ln.dlt[a] = -I[a];
-    }
   }
   ln.sm = SM_NEED_SEG;
-  ln.dens.valid = 0;
+  ln.dens_cell.i = kNoCell;
   return true;
 }
 
@@ -388,22 +386,22 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
 __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
   ln.s_dmaj = ln.maj;
   ++ln.cnt.dda_steps;
-  // HDDA::step(): axis = MinIndex(next); written with static indices so the lane state stays in VGPRs.
+  // HDDA::step(): axis = MinIndex(next); static indices keep the lane state in VGPRs.
   const float n0 = ln.nxt[0], n1 = ln.nxt[1], n2 = ln.nxt[2];
   const float fdim = (float)ln.dim;
   float tn;
   if (n0 < n1 && n0 < n2) {
     tn = n0;
-    ln.nxt[0] = tn + fdim * ln.dlt[0];
-    ln.vox[0] += ln.dim * ln.stp[0];
+    ln.nxt[0] = tn + fdim * fabsf(ln.inv[0]);
+    ln.vox[0] += ln.dim * hdda_stp(ln.d[0], ln.inv[0]);
   } else if (n1 < n2) {
     tn = n1;
-    ln.nxt[1] = tn + fdim * ln.dlt[1];
-    ln.vox[1] += ln.dim * ln.stp[1];
+    ln.nxt[1] = tn + fdim * fabsf(ln.inv[1]);
+    ln.vox[1] += ln.dim * hdda_stp(ln.d[1], ln.inv[1]);
   } else {
     tn = n2;
-    ln.nxt[2] = tn + fdim * ln.dlt[2];
-    ln.vox[2] += ln.dim * ln.stp[2];
+    ln.nxt[2] = tn + fdim * fabsf(ln.inv[2]);
+    ln.vox[2] += ln.dim * hdda_stp(ln.d[2], ln.inv[2]);
   }
   ln.T0 = tn;
   if (!(tn <= ln.T1)) {
@@ -418,12 +416,13 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
   // HDDA::update(ray, dim)
   if (nd != ln.dim) {
     ln.dim = nd;
-    float P[3] = {ln.e[0] + ln.d[0] * ln.T0, ln.e[1] + ln.d[1] * ln.T0, ln.e[2] + ln.d[2] * ln.T0};
+    const float P[3] = {ln.e[0] + ln.d[0] * ln.T0, ln.e[1] + ln.d[1] * ln.T0, ln.e[2] + ln.d[2] * ln.T0};
     for (int b = 0; b < 3; ++b) ln.vox[b] = ((int32_t)floorf(P[b])) & (~(nd - 1));
     for (int b = 0; b < 3; ++b) {
-      if (ln.stp[b] == 0) continue;
+      const int32_t st = hdda_stp(ln.d[b], ln.inv[b]);
+      if (st == 0) continue;
       float n = ln.T0 + ((float)ln.vox[b] - P[b]) * ln.inv[b];
-      if (ln.stp[b] > 0) n += (float)nd * ln.inv[b];
+      if (st > 0) n += (float)nd * ln.inv[b];
       ln.nxt[b] = n;
     }
   }
@@ -437,7 +436,7 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
 // Phase function helpers (random.hpp:56-84, utils.hpp:39-66)
 // ------------------------------------------------------------------------------------------------
 __host__ __device__ __forceinline__ void sample_hg(const float w[3], float u0, float u1, float g, float out[3]) {
-  float g2 = g * g;  // std::pow(g, 2.0f): correctly rounded square
+  float g2 = g * g;  // std::pow(g, 2.0f): the correctly rounded square (tests/test_math_clone.py)
   float cos_theta;
   if (fabsf(g) < 1e-3f) {
     cos_theta = 1 - 2 * u0;
@@ -475,52 +474,64 @@ __host__ __device__ __forceinline__ float hg_eval(float cos_theta, float g) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// One iteration of the lane loop.  Env supplies: fetch_job(uint64_t& jid_local) -> bool,
-// jid_begin, film_add(px, py, ratio*L), record(...).
+// One iteration of the lane loop.  Env supplies fetch_job(uint64_t& jid_local) -> bool, jid_begin,
+// film_add(S, lane, px, py, rw).  HasTemp: the scene has a temperature grid (fire).
+// Debug: keep every counter and the job index (per-sample records).
 // ------------------------------------------------------------------------------------------------
-template <class Env>
+template <bool HasTemp, bool Debug, class Env>
 __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane& ln, Env& env) {
   const DevGrid& G = S.density;
+  // Lanes of the wavefront sampling right now; rare states run when enough lanes wait for them
+  // or the wavefront is short of sampling work (never changes a lane's own operation order).
+  const int32_t n_sampling = env.count(ln.state == ST_SAMPLE);
+  const bool starving = n_sampling < S.gate_idle;
+  auto go = [&](int32_t st) -> bool {
+    const int32_t n = env.count(ln.state == st);
+    return n > 0 && (starving || n >= S.gate_min) && ln.state == st;
+  };
 
-  if (ln.state == ST_FETCH) {
+  if (go(ST_FETCH)) {
     uint64_t j;
     if (!env.fetch_job(j)) {
       ln.state = ST_DONE;
       return;
     }
-    ln.jid_local = j;
+    if (Debug) ln.jid_local = j;
     uint64_t jid = env.jid_begin + j;
     ln.rng = job_seed(S.seed, jid);
     uint64_t tile = jid % S.T;
     ln.x0 = (int32_t)(tile % S.ntx) * S.tw;  // TileProvider::compute_tile_rect
     ln.y0 = (int32_t)(tile / S.ntx) * S.th;
-    ln.rw = min(S.W - ln.x0, S.tw);
-    ln.rh = min(S.H - ln.y0, S.th);
     ln.pix = 0;
-    ln.temp.valid = 0;
+    if (HasTemp) ln.temp_cell.i = kNoCell;
     ln.state = ST_PIXEL;
   }
 
-  if (ln.state == ST_PIXEL) {
+  // Clipped tile extent (tile_provider.cpp:102): recomputed, not stored.
+  const int32_t rw = min(S.W - ln.x0, S.tw);
+  const int32_t rh = min(S.H - ln.y0, S.th);
+
+  if (go(ST_PIXEL)) {
     // Skip pixels filtered by single_pixel mode without any draw (worker.cpp:113-116).
+    int32_t px, py;
     while (true) {
-      if (ln.pix >= ln.rw * ln.rh) {
+      if (ln.pix >= rw * rh) {
         ln.state = ST_FETCH;
         return;
       }
-      int32_t y = ln.pix / ln.rw, x = ln.pix - y * ln.rw;
-      ln.px = ln.x0 + x;
-      ln.py = ln.y0 + y;
+      int32_t y = ln.pix / rw;
+      px = ln.x0 + (ln.pix - y * rw);
+      py = ln.y0 + y;
       ++ln.pix;
-      if (!S.single_pixel_enabled || (ln.px == S.sp_x && ln.py == S.sp_y)) break;
+      if (!S.single_pixel_enabled || (px == S.sp_x && py == S.sp_y)) break;
     }
     float jx = rng_uniform(ln.rng);
     float jy = rng_uniform(ln.rng);
-    ln.cnt.rng_draws += 2;
+    if (Debug) ln.cnt.rng_draws += 2;
     jx *= S.jitter_scale;
     jy *= S.jitter_scale;
     // Camera::generate_ray (camera.hpp:14-23)
-    float rx = ((float)ln.px + 0.5f) + jx, ry = ((float)ln.py + 0.5f) + jy;
+    float rx = ((float)px + 0.5f) + jx, ry = ((float)py + 0.5f) + jy;
     float dv[3];
     for (int i = 0; i < 3; ++i) dv[i] = S.cam_t[i] + (S.cam_L[i * 3] * rx + (S.cam_L[i * 3 + 1] * ry + S.cam_L[i * 3 + 2] * 0.0f));
     float n2 = dv[0] * dv[0] + (dv[1] * dv[1] + dv[2] * dv[2]);
@@ -537,21 +548,31 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     }
     ln.terminated = 0;
     ln.depth = 0;
-    ln.state = ST_BOUNCE;
+    ln.shadow = 0;
+    ln.state = ST_RAY;
   }
 
-  if (ln.state == ST_BOUNCE) {
-    // for (depth < max_depth) { intersection = vol.intersect(r); if (!intersection) break; ... }
-    if (ln.depth < S.max_depth && begin_ray(G, ln, ln.ro, ln.rd)) {
-      ln.shadow = 0;
-      ln.state = ST_SAMPLE;
-    } else {
+  if (go(ST_RAY)) {
+    // Primary: for (depth < max_depth) { intersection = vol.intersect(r); if (!intersection) break; }
+    // Shadow: sample_Ld's vol.intersect(Ray(pos, wi)) (worker.cpp:64-65).
+    const bool shadow = ln.shadow != 0;
+    if (!shadow && !(ln.depth < S.max_depth)) {
       ln.state = ST_FINISH;
+    } else {
+      float dir[3];
+      for (int i = 0; i < 3; ++i) dir[i] = shadow ? S.wi[i] : ln.rd[i];
+      if (begin_ray(G, ln, ln.ro, dir)) {
+        if (Debug && shadow) ++ln.cnt.shadow_rays;
+        ln.state = ST_SAMPLE;
+      } else {
+        ln.state = shadow ? ST_NEE_DONE : ST_FINISH;  // shadow miss: T_ray stays 1
+      }
     }
   }
 
   if (ln.state == ST_SAMPLE) {
     bool none = false, hit = false;
+    float cp[3], c_sigma_maj = 0.0f, c_density = 0.0f;
     if (ln.sm == SM_NEED_SEG) {
       // RayMajorantIterator::next prologue (volume.cpp:40-51)
       if (ln.T0 >= ln.T1) {
@@ -564,7 +585,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     }
     if (ln.sm == SM_STEP && !none) {
       if (hdda_step(G, ln)) {
-        ++ln.cnt.segments;
+        if (Debug) ++ln.cnt.segments;
         ln.sm = (ln.s_dmaj <= 0.0f) ? SM_NEED_SEG : SM_DRAW;  // empty segment: no draw (:32-35)
       }
     }
@@ -572,20 +593,22 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
       // MajorantTransmittanceSampler::next body (majorant_transmittance_sampler.cpp:39-79)
       float sigma_maj = ln.s_dmaj * S.sigma_t;
       float u = rng_uniform(ln.rng);
-      ++ln.cnt.draws;
-      ++ln.cnt.rng_draws;
+      if (Debug) {
+        ++ln.cnt.draws;
+        ++ln.cnt.rng_draws;
+      }
       float dt_m = -math::logf_glibc(1 - u) / sigma_maj;
       float t = ln.s_t0 + dt_m / ln.scale;
       if (t < ln.s_t1) {
         ln.s_t0 = t;
         float pi_x = ln.e[0] + ln.d[0] * t, pi_y = ln.e[1] + ln.d[1] * t, pi_z = ln.e[2] + ln.d[2] * t;
         float dens;
-        ++ln.cnt.density_evals;
-        if (trilinear(G, ln.dens, pi_x, pi_y, pi_z, dens)) ++ln.cnt.stencils;
+        if (Debug) ++ln.cnt.density_evals;
+        if (trilinear(G, ln.dens_cell, pi_x, pi_y, pi_z, dens)) ++ln.cnt.stencils;
         if (dens > 0.0f) {
-          map_fwd(G, pi_x, pi_y, pi_z, ln.cp[0], ln.cp[1], ln.cp[2]);
-          ln.c_sigma_maj = sigma_maj;
-          ln.c_density = dens;
+          map_fwd(G, pi_x, pi_y, pi_z, cp[0], cp[1], cp[2]);
+          c_sigma_maj = sigma_maj;
+          c_density = dens;
           hit = true;
         }
       } else {
@@ -595,13 +618,13 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
 
     if (hit && !ln.shadow) {
       // worker.cpp:148-188
-      float p_a = (S.sigma_a * ln.c_density) / ln.c_sigma_maj;
-      float p_s = (S.sigma_s * ln.c_density) / ln.c_sigma_maj;
+      float p_a = (S.sigma_a * c_density) / c_sigma_maj;
+      float p_s = (S.sigma_s * c_density) / c_sigma_maj;
       float p_n = fmaxf(1.0f - p_a - p_s, 0.0f);
-      if (S.has_temperature) {
+      if (HasTemp) {
         float tx, ty, tz, tadim, X, Y, Z;
-        map_inv(S.temperature, ln.cp[0], ln.cp[1], ln.cp[2], tx, ty, tz);
-        if (trilinear(S.temperature, ln.temp, tx, ty, tz, tadim)) ++ln.cnt.temp_stencils;
+        map_inv(S.temperature, cp[0], cp[1], cp[2], tx, ty, tz);
+        if (trilinear(S.temperature, ln.temp_cell, tx, ty, tz, tadim)) ++ln.cnt.temp_stencils;
         float tK = tadim * S.temp_scale + S.temp_offset;
         blackbody_xyz(S, tK, X, Y, Z);
         float sc = p_a * S.le_scale;
@@ -610,7 +633,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
         ln.L[2] = ln.L[2] + sc * Z;
       }
       float ue = rng_uniform(ln.rng);
-      ++ln.cnt.rng_draws;
+      if (Debug) ++ln.cnt.rng_draws;
       // sample_discrete({Null p_n, Absorption p_a, Scatter p_s}, u) (random.hpp:30-47)
       float total = ((0.0f + p_n) + p_a) + p_s;
       float uu = ue * total;
@@ -630,31 +653,28 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
           ln.terminated = 1;
           ln.state = ST_FINISH;
         } else {
-          ++ln.cnt.scatters;
-          for (int i = 0; i < 3; ++i) ln.sp[i] = ln.cp[i];
+          if (Debug) ++ln.cnt.scatters;
+          // The next primary ray starts at the scatter point (worker.cpp:179): keep it in ro.
+          for (int i = 0; i < 3; ++i) ln.ro[i] = cp[i];
           // sample_Ld (worker.cpp:52-90)
           if (S.li_zero) {
             ln.Tr = -1.0f;  // returns Li == 0 without draws
             ln.state = ST_NEE_DONE;
           } else {
             ln.Tr = 1.0f;
-            if (begin_ray(G, ln, ln.sp, S.wi)) {
-              ++ln.cnt.shadow_rays;
-              ln.shadow = 1;
-            } else {
-              ln.state = ST_NEE_DONE;
-            }
+            ln.shadow = 1;
+            ln.state = ST_RAY;
           }
         }
       }
       // ev == 0 (Null): keep drawing in the same segment.
     } else if (hit) {
       // Ratio tracking with Russian roulette (worker.cpp:68-85)
-      float sigma_n = fmaxf(0.0f, ln.c_sigma_maj - S.sigma_t * ln.c_density);
-      ln.Tr *= sigma_n / ln.c_sigma_maj;
+      float sigma_n = fmaxf(0.0f, c_sigma_maj - S.sigma_t * c_density);
+      ln.Tr *= sigma_n / c_sigma_maj;
       if (ln.Tr <= 0.05f) {
         float q = 0.75f;
-        ++ln.cnt.rng_draws;
+        if (Debug) ++ln.cnt.rng_draws;
         if (rng_uniform(ln.rng) < q)
           ln.Tr = 0.0f;
         else
@@ -674,7 +694,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     }
   }
 
-  if (ln.state == ST_NEE_DONE) {
+  if (go(ST_NEE_DONE)) {
     if (ln.Tr >= 0.0f) {
       // p * T_ray * Li with p = HG(w . wi)
       float c = ln.rd[0] * S.wi[0] + (ln.rd[1] * S.wi[1] + ln.rd[2] * S.wi[2]);
@@ -690,28 +710,37 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     }
     float u0 = rng_uniform(ln.rng);
     float u1 = rng_uniform(ln.rng);
-    ln.cnt.rng_draws += 2;
+    if (Debug) ln.cnt.rng_draws += 2;
     float nd[3];
     sample_hg(ln.rd, u0, u1, S.g_hg, nd);
-    for (int i = 0; i < 3; ++i) {
-      ln.ro[i] = ln.sp[i];
-      ln.rd[i] = nd[i];
-    }
+    for (int i = 0; i < 3; ++i) ln.rd[i] = nd[i];
     ++ln.depth;  // the for-loop increment (worker.cpp:130)
     ln.shadow = 0;
-    ln.state = ST_BOUNCE;
+    ln.state = ST_RAY;
   }
 
-  if (ln.state == ST_FINISH) {
+  if (go(ST_FINISH)) {
     if (!ln.terminated) {
       ln.L[0] = ln.L[0] + S.le_inf[0];
       ln.L[1] = ln.L[1] + S.le_inf[1];
       ln.L[2] = ln.L[2] + S.le_inf[2];
     }
-    env.film_add(S, ln);
+    // the pixel just traced is pix - 1 of the tile
+    const int32_t q = ln.pix - 1, y = q / rw;
+    env.film_add(S, ln, ln.x0 + (q - y * rw), ln.y0 + y, rw);
     ++ln.cnt.samples;
     ln.state = ST_PIXEL;
   }
+}
+
+__host__ __device__ __forceinline__ void lane_init(Lane& ln) {
+  ln.state = ST_FETCH;
+  ln.sm = SM_NEED_SEG;
+  ln.shadow = 0;
+  ln.terminated = 0;
+  ln.dens_cell.i = kNoCell;
+  ln.temp_cell.i = kNoCell;
+  ln.cnt = LaneCounters{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 }
 
 }  // namespace vpt

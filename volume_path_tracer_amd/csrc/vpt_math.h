@@ -30,30 +30,18 @@ __host__ __device__ __forceinline__ float as_f32(uint32_t u) {
 }
 
 // logf: LOGF_TABLE_BITS = 4, polynomial order 4 (glibc sysdeps/ieee754/flt-32/e_logf.c).
-struct LogfTab {
-  double invc, logc;
-};
-__host__ __device__ __forceinline__ LogfTab logf_tab(int i) {
-  // Table entries: 1/c and log(c) for the 16 sub-intervals of [0x3f330000, 2*0x3f330000).
-  switch (i) {
-    case 0: return {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2};
-    case 1: return {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2};
-    case 2: return {0x1.49539f0f010b0p+0, -0x1.01eae7f513a67p-2};
-    case 3: return {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3};
-    case 4: return {0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3};
-    case 5: return {0x1.25e227b0b8ea0p+0, -0x1.1aa2bc79c8100p-3};
-    case 6: return {0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4};
-    case 7: return {0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4};
-    case 8: return {0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5};
-    case 9: return {0x1.0000000000000p+0, 0x0.0p+0};
-    case 10: return {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5};
-    case 11: return {0x1.ca4b31f026aa0p-1, 0x1.c5e53aa362eb4p-4};
-    case 12: return {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3};
-    case 13: return {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d224770p-3};
-    case 14: return {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2};
-    default: return {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2};
-  }
-}
+// Table entries: 1/c and log(c) for the 16 sub-intervals of [0x3f330000, 2*0x3f330000).
+// A memory-resident constexpr table (emitted as device constant data): a per-lane indexed load
+// instead of a 16-way select chain that would hold all 32 doubles in registers.
+static constexpr double kLogfTab[16][2] = {
+    {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2}, {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2},
+    {0x1.49539f0f010b0p+0, -0x1.01eae7f513a67p-2}, {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3},
+    {0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3}, {0x1.25e227b0b8ea0p+0, -0x1.1aa2bc79c8100p-3},
+    {0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4}, {0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4},
+    {0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5}, {0x1.0000000000000p+0, 0x0.0p+0},
+    {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5},  {0x1.ca4b31f026aa0p-1, 0x1.c5e53aa362eb4p-4},
+    {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3},  {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d224770p-3},
+    {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2},  {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2}};
 
 // glibc logf for x > 0 finite (the integrator only takes log(1 - u), u in [0, 1 - 2^-24]).
 __host__ __device__ __forceinline__ float logf_glibc(float x) {
@@ -73,10 +61,10 @@ __host__ __device__ __forceinline__ float logf_glibc(float x) {
   int i = (int)((tmp >> (23 - 4)) % 16u);
   int k = (int32_t)tmp >> 23;
   uint32_t iz = ix - (tmp & (0x1ffu << 23));
-  LogfTab t = logf_tab(i);
+  const double invc = kLogfTab[i][0], logc = kLogfTab[i][1];
   double z = (double)as_f32(iz);
-  double r = __builtin_fma(z, t.invc, -1.0);
-  double y0 = __builtin_fma((double)k, Ln2, t.logc);
+  double r = __builtin_fma(z, invc, -1.0);
+  double y0 = __builtin_fma((double)k, Ln2, logc);
   double r2 = r * r;
   double y = __builtin_fma(A1, r, A2);
   y = __builtin_fma(A0, r2, y);
@@ -85,78 +73,65 @@ __host__ __device__ __forceinline__ float logf_glibc(float x) {
 }
 
 // sinf / cosf (glibc sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c, sincosf.h), for |x| < 120.
-struct SinCosTab {
-  double sign0, sign1, sign2, sign3, hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4;
-};
-__host__ __device__ __forceinline__ SinCosTab sincos_tab(int which) {
-  if (which == 0)
-    return {1.0, -1.0, -1.0, 1.0, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, 0x1p0, -0x1.ffffffd0c621cp-2,
-            -0x1.555545995a603p-3, 0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10,
-            -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16};
-  return {1.0, -1.0, -1.0, 1.0, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, -0x1p0, 0x1.ffffffd0c621cp-2,
-          -0x1.555545995a603p-3, -0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10,
-          -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16};
-}
+// glibc's __sincosf_table[1] is table[0] with the cosine coefficients negated; since
+// fma(a, -b, -c) == -fma(a, b, c) exactly, using table[0] and negating the cosine result when
+// (n & 2) gives bit-identical values without selecting between two coefficient sets.
+namespace sc {
+constexpr double hpi_inv = 0x1.45f306dc9c883p+23, hpi = 0x1.921fb54442d18p+0;
+constexpr double c0 = 0x1p0, c1 = -0x1.ffffffd0c621cp-2, c2 = 0x1.55553e1068f19p-5, c3 = -0x1.6c087e89a359dp-10,
+                 c4 = 0x1.99343027bf8c3p-16;
+constexpr double s1 = -0x1.555545995a603p-3, s2 = 0x1.1107605230bc4p-7, s3 = -0x1.994eb3774cf24p-13;
+}  // namespace sc
 __host__ __device__ __forceinline__ uint32_t abstop12(float x) { return (as_u32(x) >> 20) & 0x7ff; }
-__host__ __device__ __forceinline__ float sinf_poly(double x, double x2, const SinCosTab& p, int n) {
+// sinf_poly(x, x2, table[neg], n): n even -> sine polynomial, odd -> cosine polynomial.
+__host__ __device__ __forceinline__ float sinf_poly(double x, double x2, bool neg_cos, int n) {
   if ((n & 1) == 0) {
     double x3 = x * x2;
-    double s1 = __builtin_fma(x2, p.s3, p.s2);
+    double s1 = __builtin_fma(x2, sc::s3, sc::s2);
     double x7 = x3 * x2;
-    double s = __builtin_fma(x3, p.s1, x);
+    double s = __builtin_fma(x3, sc::s1, x);
     return (float)__builtin_fma(x7, s1, s);
   }
   double x4 = x2 * x2;
-  double c2 = __builtin_fma(x2, p.c4, p.c3);
-  double c1 = __builtin_fma(x2, p.c1, p.c0);
+  double c2 = __builtin_fma(x2, sc::c4, sc::c3);
+  double c1 = __builtin_fma(x2, sc::c1, sc::c0);
   double x6 = x4 * x2;
-  double c = __builtin_fma(x4, p.c2, c1);
-  return (float)__builtin_fma(x6, c2, c);
+  double c = __builtin_fma(x4, sc::c2, c1);
+  double r = __builtin_fma(x6, c2, c);
+  return (float)(neg_cos ? -r : r);
 }
-__host__ __device__ __forceinline__ double reduce_fast(double x, const SinCosTab& p, int* np) {
-  double r = x * p.hpi_inv;
+__host__ __device__ __forceinline__ double reduce_fast(double x, int* np) {
+  double r = x * sc::hpi_inv;
   int n = ((int32_t)r + 0x800000) >> 24;
   *np = n;
-  return __builtin_fma(-(double)n, p.hpi, x);
+  return __builtin_fma(-(double)n, sc::hpi, x);
 }
-__host__ __device__ __forceinline__ double quadrant_sign(const SinCosTab& p, int n) {
-  switch (n & 3) {
-    case 0: return p.sign0;
-    case 1: return p.sign1;
-    case 2: return p.sign2;
-    default: return p.sign3;
-  }
-}
+// sign[4] = {1, -1, -1, 1}
+__host__ __device__ __forceinline__ double quadrant_sign(int n) { return ((n + 1) & 2) ? -1.0 : 1.0; }
 // Valid for finite |y| < 120 (the integrator calls it with phi = 2*pi*u in [0, 2*pi)).
 __host__ __device__ __forceinline__ float sinf_glibc(float y) {
-  const uint32_t pio4_top = 0x3f4u;  // abstop12(0x1.921fb6p-1f)
   double x = y;
-  if (abstop12(y) < pio4_top) {
+  if (abstop12(y) < 0x3f4u) {  // abstop12(pi/4)
     double s = x * x;
     if (abstop12(y) < 0x398u) return y;  // abstop12(0x1p-12f)
-    return sinf_poly(x, s, sincos_tab(0), 0);
+    return sinf_poly(x, s, false, 0);
   }
   int n;
-  SinCosTab p0 = sincos_tab(0);
-  x = reduce_fast(x, p0, &n);
-  double s = quadrant_sign(p0, n);
-  SinCosTab p = (n & 2) ? sincos_tab(1) : p0;
-  return sinf_poly(x * s, x * x, p, n);
+  x = reduce_fast(x, &n);
+  double s = quadrant_sign(n);
+  return sinf_poly(x * s, x * x, (n & 2) != 0, n);
 }
 __host__ __device__ __forceinline__ float cosf_glibc(float y) {
-  const uint32_t pio4_top = 0x3f4u;
   double x = y;
-  if (abstop12(y) < pio4_top) {
+  if (abstop12(y) < 0x3f4u) {
     double x2 = x * x;
     if (abstop12(y) < 0x398u) return 1.0f;
-    return sinf_poly(x, x2, sincos_tab(0), 1);
+    return sinf_poly(x, x2, false, 1);
   }
   int n;
-  SinCosTab p0 = sincos_tab(0);
-  x = reduce_fast(x, p0, &n);
-  double s = quadrant_sign(p0, n);
-  SinCosTab p = (n & 2) ? sincos_tab(1) : p0;
-  return sinf_poly(x * s, x * x, p, n ^ 1);
+  x = reduce_fast(x, &n);
+  double s = quadrant_sign(n);
+  return sinf_poly(x * s, x * x, (n & 2) != 0, n ^ 1);
 }
 
 }  // namespace math

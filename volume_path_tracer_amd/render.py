@@ -154,6 +154,9 @@ class Integrator:
         capi.check(capi.lib().vpt_gpu_counters(self.h, C.byref(c), 1 if reset else 0), "vpt_gpu_counters")
         return c.as_dict()
 
+    def set_tuning(self, gate_min: int = 0, gate_idle: int = -1, grid_blocks: int = 0):
+        capi.check(capi.lib().vpt_gpu_set_tuning(self.h, gate_min, gate_idle, grid_blocks), "vpt_gpu_set_tuning")
+
     def launch_info(self):
         g, b = C.c_int(), C.c_int()
         capi.check(capi.lib().vpt_gpu_launch_info(self.h, C.byref(g), C.byref(b)), "vpt_gpu_launch_info")
