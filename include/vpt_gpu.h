@@ -198,9 +198,14 @@ int vpt_gpu_film_add_to_host(vpt_gpu_ctx* ctx, float* film_host_hxwx4);
 int vpt_gpu_counters(vpt_gpu_ctx* ctx, vpt_counters* out, int reset);
 /* Scheduling knobs (results never depend on them): a rare lane state (new job, new pixel, ray
  * setup, NEE completion, film write) runs when >= gate_min lanes of a wavefront wait for it or
- * fewer than gate_idle lanes are sampling; grid_blocks overrides the persistent grid size.
+ * fewer than gate_idle lanes are walking rays; a tentative collision's density evaluation waits
+ * for gate_eval lanes likewise; grid_blocks overrides the persistent grid size.
  * Pass <= 0 (gate_idle < 0) to keep a value. */
-int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_blocks);
+int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_blocks, int gate_eval);
+/* SIMT-utilisation profile of profiling builds (-DVPT_PROFILE): for each block of the lane state
+ * machine, [wave executions, active lanes] as 2*blocks uint64 (zeros in normal builds);
+ * n must be >= 2 * 14. */
+int vpt_gpu_profile(vpt_gpu_ctx* ctx, uint64_t* out, int n, int reset);
 /* Launch geometry used by the integrator kernel (for reports). */
 int vpt_gpu_launch_info(const vpt_gpu_ctx* ctx, int* grid_blocks, int* block_threads);
 

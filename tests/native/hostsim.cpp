@@ -23,6 +23,7 @@ struct HostEnv {
   float* records;
   int32_t tile_area;
   int32_t count(bool pred) { return pred ? 1 : 0; }  // one lane
+  void prof(int32_t) {}
   bool fetch_job(uint64_t& j) {
     if (next >= jid_count) return false;
     j = next++;
@@ -68,6 +69,7 @@ extern "C" int vpths_render_jobs(const vpt_configuration* cfg, const vpt_grid_de
   S.cie = vpt::cie_table();
   S.gate_min = 1;
   S.gate_idle = 1;
+  S.gate_eval = 1;
   HostEnv env{jid_begin, jid_count, 0, film, records, S.tw * S.th};
   vpt::Lane ln;
   std::memset(&ln, 0, sizeof ln);

@@ -9,6 +9,7 @@ ap.add_argument("--config", default="c3")
 ap.add_argument("--gates", default="16:16")
 ap.add_argument("--blocks", default="0")
 ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--profile", action="store_true")
 a = ap.parse_args()
 import torch
 from volume_path_tracer_amd.render import Integrator
@@ -18,15 +19,22 @@ dg = SynthGrid(wl.density_kind, wl.grid_n); tg = SynthGrid(2, wl.grid_n) if wl.t
 it = Integrator(wl.cfg, dg.grid(copy=False), tg.grid(copy=False) if tg else None)
 base_blocks = it.launch_info()[0]
 it.render_waves(1, 1); torch.cuda.synchronize()
+if a.profile:
+    it.profile(reset=True)
 for g in a.gates.split(","):
-    gm, gi = map(int, g.split(":"))
+    parts = list(map(int, g.split(":")))
+    gm, gi = parts[0], parts[1]
+    ge = parts[2] if len(parts) > 2 else 1
     for b in map(int, a.blocks.split(",")):
-        it.set_tuning(gm, gi, b if b > 0 else base_blocks)
+        it.set_tuning(gm, gi, b if b > 0 else base_blocks, ge)
         best = 1e9
         for _ in range(a.reps):
             it.film.zero_(); torch.cuda.synchronize(); t = time.perf_counter()
             it.render_waves(1, a.spp); torch.cuda.synchronize()
             best = min(best, time.perf_counter() - t)
         ms = best * 1e3
+        if a.profile:
+            prof = it.profile(reset=True)
+            print(json.dumps({"gate": g, "profile": prof}), flush=True)
         print(json.dumps({"lib": os.environ.get("VPT_LIB", "default"), "gate": g, "blocks": b or base_blocks,
                           "spp": a.spp, "ms": round(ms, 2), "Msps": round(wl.cfg.width * wl.cfg.height * a.spp / best / 1e6, 2)}), flush=True)

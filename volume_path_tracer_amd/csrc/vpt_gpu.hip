@@ -47,7 +47,19 @@ struct KernelEnv {
   float* film;
   float* records;
   int32_t tile_area;
+  unsigned long long* prof_buf;  // [PB_COUNT][2] wave executions, active lanes (VPT_PROFILE builds)
 
+  __device__ __forceinline__ void prof(int32_t id) {
+#ifdef VPT_PROFILE
+    const unsigned long long m = __ballot(1);
+    if ((__lane_id() == (uint32_t)__builtin_ctzll(m))) {
+      atomicAdd(prof_buf + 2 * id, 1ULL);
+      atomicAdd(prof_buf + 2 * id + 1, (unsigned long long)__popcll(m));
+    }
+#else
+    (void)id;
+#endif
+  }
   // lanes of this wavefront for which pred holds
   __device__ __forceinline__ int32_t count(bool pred) { return (int32_t)__popcll(__ballot(pred)); }
   __device__ __forceinline__ bool fetch_job(uint64_t& j) {
@@ -141,6 +153,7 @@ struct vpt_gpu_ctx {
   uint64_t film_count = 0;
   unsigned long long* job_counter = nullptr;
   unsigned long long* counters = nullptr;
+  unsigned long long* prof = nullptr;
   hipStream_t stream = nullptr;
   int grid_blocks = 0;
 };
@@ -163,6 +176,7 @@ void destroy(vpt_gpu_ctx* ctx) {
   (void)hipFree(ctx->film);
   (void)hipFree(ctx->job_counter);
   (void)hipFree(ctx->counters);
+  (void)hipFree(ctx->prof);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -182,6 +196,7 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.film = film ? film : ctx->film;
   env.records = records;
   env.tile_area = ctx->scene.tw * ctx->scene.th;
+  env.prof_buf = ctx->prof;
   VPT_HIP(hipMemsetAsync(ctx->job_counter, 0, sizeof(unsigned long long), s));
   const bool temp = ctx->scene.has_temperature != 0, dbg = records != nullptr;
   auto kernel = temp ? (dbg ? vpt::vpt_integrate_kernel<true, true> : vpt::vpt_integrate_kernel<true, false>)
@@ -246,6 +261,8 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   VPT_HIP(hipMalloc((void**)&ctx->job_counter, sizeof(unsigned long long)));
   VPT_HIP(hipMalloc((void**)&ctx->counters, vpt::kCounterCount * sizeof(unsigned long long)));
   VPT_HIP(hipMemset(ctx->counters, 0, vpt::kCounterCount * sizeof(unsigned long long)));
+  VPT_HIP(hipMalloc((void**)&ctx->prof, 2 * vpt::PB_COUNT * sizeof(unsigned long long)));
+  VPT_HIP(hipMemset(ctx->prof, 0, 2 * vpt::PB_COUNT * sizeof(unsigned long long)));
   VPT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
 
   // Persistent grid: as many blocks as are resident at once.
@@ -257,8 +274,11 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   VPT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
   if (per_cu < 1) per_cu = 1;
   ctx->grid_blocks = per_cu * cus;
-  ctx->scene.gate_min = 16;  // rare states run when a quarter of the wavefront waits for them
-  ctx->scene.gate_idle = 16;
+  // Scheduling defaults from tools/tune.py sweeps on MI355X (C3, 32 spp): rare states run for >= 8
+  // waiting lanes, density evaluations for >= 16, everything runs when < 8 lanes are walking.
+  ctx->scene.gate_min = 8;
+  ctx->scene.gate_idle = 8;
+  ctx->scene.gate_eval = 16;
   *out = ctx.release();
   return VPT_OK;
 }
@@ -333,11 +353,25 @@ int vpt_gpu_counters(vpt_gpu_ctx* ctx, vpt_counters* out, int reset) {
   return VPT_OK;
 }
 
-int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_blocks) {
+int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_blocks, int gate_eval) {
   if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
+  if (gate_eval > 0) ctx->scene.gate_eval = gate_eval;
   if (gate_min > 0) ctx->scene.gate_min = gate_min;
   if (gate_idle >= 0) ctx->scene.gate_idle = gate_idle;
   if (grid_blocks > 0) ctx->grid_blocks = grid_blocks;
+  return VPT_OK;
+}
+
+int vpt_gpu_profile(vpt_gpu_ctx* ctx, uint64_t* out, int n, int reset) {
+  if (!ctx || !out) return vpt::set_error(VPT_E_INVALID, "null argument");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  VPT_HIP(hipDeviceSynchronize());
+  std::vector<unsigned long long> v(2 * vpt::PB_COUNT);
+  VPT_HIP(hipMemcpy(v.data(), ctx->prof, v.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  if (n < (int)v.size()) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_profile: output too small");
+  for (size_t i = 0; i < v.size(); ++i) out[i] = v[i];
+  if (reset) VPT_HIP(hipMemset(ctx->prof, 0, v.size() * sizeof(unsigned long long)));
   return VPT_OK;
 }
 

@@ -95,10 +95,11 @@ __host__ __device__ __forceinline__ float value_at(const DevGrid& g, int32_t i, 
 // stencil every time and only remembers the last cell to count refreshes (algorithmic bytes).
 struct StencilCell {
   int32_t i, j, k;
+  int32_t code;  // cell code of the last stencil's corner cell (reused while in the same 8^3 cell)
 };
 
-__host__ __device__ __forceinline__ void fetch_stencil(const DevGrid& g, int32_t i, int32_t j, int32_t k, float v[8]) {
-  Cell c = cell_at(g, i, j, k);
+__host__ __device__ __forceinline__ void fetch_stencil(const DevGrid& g, Cell c, int32_t i, int32_t j, int32_t k,
+                                                       float v[8]) {
   if (c.code >= 0) {
     // Corner cell inside a leaf: the 9^3 apron brick holds the whole 2^3 stencil.
     const float* b = g.bricks + (int64_t)c.code * kBrickVox + (i & 7) * 81 + (j & 7) * 9 + (k & 7);
@@ -120,17 +121,28 @@ __host__ __device__ __forceinline__ void fetch_stencil(const DevGrid& g, int32_t
 // TrilinearSampler::sample: lerp(a, b, w) = a + w * (b - a), z then y then x.
 __host__ __device__ __forceinline__ float lerpf(float a, float b, float w) { return a + w * (b - a); }
 // Returns true when the cell differs from the previous evaluation (a NanoVDB stencil refresh).
+// The leaf-slot lookup is skipped while the corner cell stays in the previous one's 8^3 cell.
 __host__ __device__ __forceinline__ bool trilinear(const DevGrid& g, StencilCell& last, float x, float y, float z,
                                                    float& out) {
   float fi = floorf(x), fj = floorf(y), fk = floorf(z);
   float u = x - fi, v = y - fj, w = z - fk;
   int32_t i = (int32_t)fi, j = (int32_t)fj, k = (int32_t)fk;
   bool refresh = i != last.i || j != last.j || k != last.k;
+  const int32_t dx = (i ^ last.i) | (j ^ last.j) | (k ^ last.k);
+  const bool same_leaf = last.code >= 0 && dx >= 0 && dx < 8;  // same 8^3 cell as a leaf-backed stencil
+  Cell c;
+  if (same_leaf) {
+    c.code = last.code;
+    c.value = 0.0f;  // only read for non-leaf cells, which are never reused (code < 0 -> value_at)
+  } else {
+    c = cell_at(g, i, j, k);
+  }
   last.i = i;
   last.j = j;
   last.k = k;
+  last.code = c.code;
   float s[8];
-  fetch_stencil(g, i, j, k, s);
+  fetch_stencil(g, c, i, j, k, s);
   out = lerpf(lerpf(lerpf(s[0], s[1], w), lerpf(s[2], s[3], w), v), lerpf(lerpf(s[4], s[5], w), lerpf(s[6], s[7], w), v), u);
   return refresh;
 }
@@ -184,6 +196,7 @@ struct DevScene {
   // Wave gating of the rare states: a rare block runs when at least gate_min lanes of the wavefront
   // wait for it, or when fewer than gate_idle lanes are sampling (1/64 = always run).
   int32_t gate_min, gate_idle;
+  int32_t gate_eval;  // the density evaluation (trilinear + event) runs for >= gate_eval waiting lanes
   const float* bb;      // blackbody table [501][3] (row 500 = 0)
   const float* cie;     // [471][3] for T >= 49900 K
   float y_integral;
@@ -281,7 +294,12 @@ enum : int32_t {
   ST_FINISH = 5,  // pixel done: environment light, film
   ST_DONE = 6
 };
-enum : int32_t { SM_NEED_SEG = 0, SM_STEP = 1, SM_DRAW = 2 };
+enum : int32_t { SM_NEED_SEG = 0, SM_STEP = 1, SM_DRAW = 2, SM_EVAL = 3 };  // SM_EVAL: density at s_t0 pending
+// Block ids for the optional SIMT-utilisation profile (env.prof; a no-op unless VPT_PROFILE).
+enum : int32_t {
+  PB_ITER = 0, PB_FETCH, PB_PIXEL, PB_RAY, PB_SAMPLE, PB_NEED_SEG, PB_STEP, PB_DRAW, PB_TRILINEAR,
+  PB_EVENT, PB_SHADOW_HIT, PB_NONE, PB_NEE_DONE, PB_FINISH, PB_COUNT
+};
 
 // Event counters.  The production kernel keeps the four that price algorithmic bytes
 // (SURVEY §8d); the debug kernel (per-sample records) keeps all of them for parity checks.
@@ -378,6 +396,7 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
   }
   ln.sm = SM_NEED_SEG;
   ln.dens_cell.i = kNoCell;
+  ln.dens_cell.code = -1;
   return true;
 }
 
@@ -410,8 +429,9 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
   }
   // new_dim = max(8, getDim(floor(ray(time + 1.0001f))))
   float tl = ln.T0 + 1.0001f;
-  Cell la = cell_at(g, (int32_t)floorf(ln.e[0] + ln.d[0] * tl), (int32_t)floorf(ln.e[1] + ln.d[1] * tl),
-                    (int32_t)floorf(ln.e[2] + ln.d[2] * tl));
+  const int32_t lx = (int32_t)floorf(ln.e[0] + ln.d[0] * tl), ly = (int32_t)floorf(ln.e[1] + ln.d[1] * tl),
+                lz = (int32_t)floorf(ln.e[2] + ln.d[2] * tl);
+  Cell la = cell_at(g, lx, ly, lz);
   int32_t nd = hdda_dim_of(la);
   // HDDA::update(ray, dim)
   if (nd != ln.dim) {
@@ -426,7 +446,10 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
       ln.nxt[b] = n;
     }
   }
-  ln.maj = majorant_of(cell_at(g, ln.vox[0], ln.vox[1], ln.vox[2]));
+  // update_current_majorant at the (new) voxel: the lookahead cell answers it when both points lie
+  // in the same 8^3 cell (every query is a function of the 8^3 cell), saving a dependent load.
+  const int32_t dx = (ln.vox[0] ^ lx) | (ln.vox[1] ^ ly) | (ln.vox[2] ^ lz);
+  ln.maj = majorant_of((dx >= 0 && dx < 8) ? la : cell_at(g, ln.vox[0], ln.vox[1], ln.vox[2]));
   if (ln.maj == ln.s_dmaj) return false;
   ln.s_t1 = ln.T0;
   return true;
@@ -481,16 +504,18 @@ __host__ __device__ __forceinline__ float hg_eval(float cos_theta, float g) {
 template <bool HasTemp, bool Debug, class Env>
 __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane& ln, Env& env) {
   const DevGrid& G = S.density;
+  env.prof(PB_ITER);
   // Lanes of the wavefront sampling right now; rare states run when enough lanes wait for them
   // or the wavefront is short of sampling work (never changes a lane's own operation order).
-  const int32_t n_sampling = env.count(ln.state == ST_SAMPLE);
-  const bool starving = n_sampling < S.gate_idle;
+  const int32_t n_walking = env.count(ln.state == ST_SAMPLE && ln.sm != SM_EVAL);
+  const bool starving = n_walking < S.gate_idle;
   auto go = [&](int32_t st) -> bool {
     const int32_t n = env.count(ln.state == st);
     return n > 0 && (starving || n >= S.gate_min) && ln.state == st;
   };
 
   if (go(ST_FETCH)) {
+    env.prof(PB_FETCH);
     uint64_t j;
     if (!env.fetch_job(j)) {
       ln.state = ST_DONE;
@@ -503,7 +528,10 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     ln.x0 = (int32_t)(tile % S.ntx) * S.tw;  // TileProvider::compute_tile_rect
     ln.y0 = (int32_t)(tile / S.ntx) * S.th;
     ln.pix = 0;
-    if (HasTemp) ln.temp_cell.i = kNoCell;
+    if (HasTemp) {
+      ln.temp_cell.i = kNoCell;
+      ln.temp_cell.code = -1;
+    }
     ln.state = ST_PIXEL;
   }
 
@@ -512,6 +540,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
   const int32_t rh = min(S.H - ln.y0, S.th);
 
   if (go(ST_PIXEL)) {
+    env.prof(PB_PIXEL);
     // Skip pixels filtered by single_pixel mode without any draw (worker.cpp:113-116).
     int32_t px, py;
     while (true) {
@@ -553,6 +582,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
   }
 
   if (go(ST_RAY)) {
+    env.prof(PB_RAY);
     // Primary: for (depth < max_depth) { intersection = vol.intersect(r); if (!intersection) break; }
     // Shadow: sample_Ld's vol.intersect(Ray(pos, wi)) (worker.cpp:64-65).
     const bool shadow = ln.shadow != 0;
@@ -571,25 +601,29 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
   }
 
   if (ln.state == ST_SAMPLE) {
-    bool none = false, hit = false;
-    float cp[3], c_sigma_maj = 0.0f, c_density = 0.0f;
+    env.prof(PB_SAMPLE);
     if (ln.sm == SM_NEED_SEG) {
+      env.prof(PB_NEED_SEG);
       // RayMajorantIterator::next prologue (volume.cpp:40-51)
       if (ln.T0 >= ln.T1) {
-        none = true;
+        // the sampler ran dry: a shadow ray keeps T_ray; a primary ray did not scatter (break)
+        ln.state = ln.shadow ? ST_NEE_DONE : ST_FINISH;
+        env.prof(PB_NONE);
       } else {
         ln.s_t0 = ln.T0;
         if (ln.maj != ln.maj) ln.maj = majorant_of(cell_at(G, ln.vox[0], ln.vox[1], ln.vox[2]));
         ln.sm = SM_STEP;
       }
     }
-    if (ln.sm == SM_STEP && !none) {
+    if (ln.state == ST_SAMPLE && ln.sm == SM_STEP) {
+      env.prof(PB_STEP);
       if (hdda_step(G, ln)) {
         if (Debug) ++ln.cnt.segments;
         ln.sm = (ln.s_dmaj <= 0.0f) ? SM_NEED_SEG : SM_DRAW;  // empty segment: no draw (:32-35)
       }
     }
-    if (ln.sm == SM_DRAW && !none) {
+    if (ln.state == ST_SAMPLE && ln.sm == SM_DRAW) {
+      env.prof(PB_DRAW);
       // MajorantTransmittanceSampler::next body (majorant_transmittance_sampler.cpp:39-79)
       float sigma_maj = ln.s_dmaj * S.sigma_t;
       float u = rng_uniform(ln.rng);
@@ -600,101 +634,106 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
       float dt_m = -math::logf_glibc(1 - u) / sigma_maj;
       float t = ln.s_t0 + dt_m / ln.scale;
       if (t < ln.s_t1) {
-        ln.s_t0 = t;
-        float pi_x = ln.e[0] + ln.d[0] * t, pi_y = ln.e[1] + ln.d[1] * t, pi_z = ln.e[2] + ln.d[2] * t;
-        float dens;
-        if (Debug) ++ln.cnt.density_evals;
-        if (trilinear(G, ln.dens_cell, pi_x, pi_y, pi_z, dens)) ++ln.cnt.stencils;
-        if (dens > 0.0f) {
-          map_fwd(G, pi_x, pi_y, pi_z, cp[0], cp[1], cp[2]);
-          c_sigma_maj = sigma_maj;
-          c_density = dens;
-          hit = true;
-        }
+        ln.s_t0 = t;       // the tentative collision; its density is evaluated in SM_EVAL
+        ln.sm = SM_EVAL;
       } else {
         ln.sm = SM_NEED_SEG;
       }
     }
+  }
 
-    if (hit && !ln.shadow) {
-      // worker.cpp:148-188
-      float p_a = (S.sigma_a * c_density) / c_sigma_maj;
-      float p_s = (S.sigma_s * c_density) / c_sigma_maj;
-      float p_n = fmaxf(1.0f - p_a - p_s, 0.0f);
-      if (HasTemp) {
-        float tx, ty, tz, tadim, X, Y, Z;
-        map_inv(S.temperature, cp[0], cp[1], cp[2], tx, ty, tz);
-        if (trilinear(S.temperature, ln.temp_cell, tx, ty, tz, tadim)) ++ln.cnt.temp_stencils;
-        float tK = tadim * S.temp_scale + S.temp_offset;
-        blackbody_xyz(S, tK, X, Y, Z);
-        float sc = p_a * S.le_scale;
-        ln.L[0] = ln.L[0] + sc * X;
-        ln.L[1] = ln.L[1] + sc * Y;
-        ln.L[2] = ln.L[2] + sc * Z;
-      }
-      float ue = rng_uniform(ln.rng);
-      if (Debug) ++ln.cnt.rng_draws;
-      // sample_discrete({Null p_n, Absorption p_a, Scatter p_s}, u) (random.hpp:30-47)
-      float total = ((0.0f + p_n) + p_a) + p_s;
-      float uu = ue * total;
-      int ev;
-      uu -= p_n;
-      if (uu <= 0) {
-        ev = 0;
-      } else {
-        uu -= p_a;
-        ev = (uu <= 0) ? 1 : 2;
-      }
-      if (ev == 1) {
-        ln.terminated = 1;
-        ln.state = ST_FINISH;
-      } else if (ev == 2) {
-        if (ln.depth++ >= S.max_depth) {
+  // Tentative collisions wait until gate_eval lanes of the wavefront have one (or the walk runs
+  // short of lanes), so the stencil gathers and the event logic run on a fuller wavefront.
+  const int32_t n_eval = env.count(ln.state == ST_SAMPLE && ln.sm == SM_EVAL);
+  const bool run_eval = n_eval > 0 && (n_eval >= S.gate_eval || env.count(ln.state == ST_SAMPLE && ln.sm != SM_EVAL) < S.gate_idle);
+  if (run_eval && ln.state == ST_SAMPLE && ln.sm == SM_EVAL) {
+    env.prof(PB_TRILINEAR);
+    const float t = ln.s_t0;
+    const float sigma_maj = ln.s_dmaj * S.sigma_t;
+    float pi_x = ln.e[0] + ln.d[0] * t, pi_y = ln.e[1] + ln.d[1] * t, pi_z = ln.e[2] + ln.d[2] * t;
+    float dens;
+    if (Debug) ++ln.cnt.density_evals;
+    if (trilinear(G, ln.dens_cell, pi_x, pi_y, pi_z, dens)) ++ln.cnt.stencils;
+    ln.sm = SM_DRAW;  // density <= 0, a null event or an unkilled shadow ray: keep drawing
+    if (dens > 0.0f) {
+      float cp[3];
+      map_fwd(G, pi_x, pi_y, pi_z, cp[0], cp[1], cp[2]);
+      if (!ln.shadow) {
+        env.prof(PB_EVENT);
+        // worker.cpp:148-188
+        float p_a = (S.sigma_a * dens) / sigma_maj;
+        float p_s = (S.sigma_s * dens) / sigma_maj;
+        float p_n = fmaxf(1.0f - p_a - p_s, 0.0f);
+        if (HasTemp) {
+          float tx, ty, tz, tadim, X, Y, Z;
+          map_inv(S.temperature, cp[0], cp[1], cp[2], tx, ty, tz);
+          if (trilinear(S.temperature, ln.temp_cell, tx, ty, tz, tadim)) ++ln.cnt.temp_stencils;
+          float tK = tadim * S.temp_scale + S.temp_offset;
+          blackbody_xyz(S, tK, X, Y, Z);
+          float sc = p_a * S.le_scale;
+          ln.L[0] = ln.L[0] + sc * X;
+          ln.L[1] = ln.L[1] + sc * Y;
+          ln.L[2] = ln.L[2] + sc * Z;
+        }
+        float ue = rng_uniform(ln.rng);
+        if (Debug) ++ln.cnt.rng_draws;
+        // sample_discrete({Null p_n, Absorption p_a, Scatter p_s}, u) (random.hpp:30-47)
+        float total = ((0.0f + p_n) + p_a) + p_s;
+        float uu = ue * total;
+        int ev;
+        uu -= p_n;
+        if (uu <= 0) {
+          ev = 0;
+        } else {
+          uu -= p_a;
+          ev = (uu <= 0) ? 1 : 2;
+        }
+        if (ev == 1) {
           ln.terminated = 1;
           ln.state = ST_FINISH;
-        } else {
-          if (Debug) ++ln.cnt.scatters;
-          // The next primary ray starts at the scatter point (worker.cpp:179): keep it in ro.
-          for (int i = 0; i < 3; ++i) ln.ro[i] = cp[i];
-          // sample_Ld (worker.cpp:52-90)
-          if (S.li_zero) {
-            ln.Tr = -1.0f;  // returns Li == 0 without draws
-            ln.state = ST_NEE_DONE;
+        } else if (ev == 2) {
+          if (ln.depth++ >= S.max_depth) {
+            ln.terminated = 1;
+            ln.state = ST_FINISH;
           } else {
-            ln.Tr = 1.0f;
-            ln.shadow = 1;
-            ln.state = ST_RAY;
+            if (Debug) ++ln.cnt.scatters;
+            // The next primary ray starts at the scatter point (worker.cpp:179): keep it in ro.
+            for (int i = 0; i < 3; ++i) ln.ro[i] = cp[i];
+            // sample_Ld (worker.cpp:52-90)
+            if (S.li_zero) {
+              ln.Tr = -1.0f;  // returns Li == 0 without draws
+              ln.state = ST_NEE_DONE;
+            } else {
+              ln.Tr = 1.0f;
+              ln.shadow = 1;
+              ln.state = ST_RAY;
+            }
           }
         }
+        // ev == 0 (Null): keep drawing in the same segment.
+      } else {
+        env.prof(PB_SHADOW_HIT);
+        // Ratio tracking with Russian roulette (worker.cpp:68-85)
+        float sigma_n = fmaxf(0.0f, sigma_maj - S.sigma_t * dens);
+        ln.Tr *= sigma_n / sigma_maj;
+        if (ln.Tr <= 0.05f) {
+          float q = 0.75f;
+          if (Debug) ++ln.cnt.rng_draws;
+          if (rng_uniform(ln.rng) < q)
+            ln.Tr = 0.0f;
+          else
+            ln.Tr /= 1 - q;
+        }
+        if (ln.Tr <= 0.0f) {
+          ln.Tr = -1.0f;  // returns Zero()
+          ln.state = ST_NEE_DONE;
+        }
       }
-      // ev == 0 (Null): keep drawing in the same segment.
-    } else if (hit) {
-      // Ratio tracking with Russian roulette (worker.cpp:68-85)
-      float sigma_n = fmaxf(0.0f, c_sigma_maj - S.sigma_t * c_density);
-      ln.Tr *= sigma_n / c_sigma_maj;
-      if (ln.Tr <= 0.05f) {
-        float q = 0.75f;
-        if (Debug) ++ln.cnt.rng_draws;
-        if (rng_uniform(ln.rng) < q)
-          ln.Tr = 0.0f;
-        else
-          ln.Tr /= 1 - q;
-      }
-      if (ln.Tr <= 0.0f) {
-        ln.Tr = -1.0f;  // returns Zero()
-        ln.state = ST_NEE_DONE;
-      }
-    }
-
-    if (none) {
-      if (ln.shadow)
-        ln.state = ST_NEE_DONE;
-      else
-        ln.state = ST_FINISH;  // the sampler ran dry without scattering: break
     }
   }
 
   if (go(ST_NEE_DONE)) {
+    env.prof(PB_NEE_DONE);
     if (ln.Tr >= 0.0f) {
       // p * T_ray * Li with p = HG(w . wi)
       float c = ln.rd[0] * S.wi[0] + (ln.rd[1] * S.wi[1] + ln.rd[2] * S.wi[2]);
@@ -720,6 +759,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
   }
 
   if (go(ST_FINISH)) {
+    env.prof(PB_FINISH);
     if (!ln.terminated) {
       ln.L[0] = ln.L[0] + S.le_inf[0];
       ln.L[1] = ln.L[1] + S.le_inf[1];
@@ -739,7 +779,9 @@ __host__ __device__ __forceinline__ void lane_init(Lane& ln) {
   ln.shadow = 0;
   ln.terminated = 0;
   ln.dens_cell.i = kNoCell;
+  ln.dens_cell.code = -1;
   ln.temp_cell.i = kNoCell;
+  ln.temp_cell.code = -1;
   ln.cnt = LaneCounters{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 }
 

@@ -154,8 +154,22 @@ class Integrator:
         capi.check(capi.lib().vpt_gpu_counters(self.h, C.byref(c), 1 if reset else 0), "vpt_gpu_counters")
         return c.as_dict()
 
-    def set_tuning(self, gate_min: int = 0, gate_idle: int = -1, grid_blocks: int = 0):
-        capi.check(capi.lib().vpt_gpu_set_tuning(self.h, gate_min, gate_idle, grid_blocks), "vpt_gpu_set_tuning")
+    def set_tuning(self, gate_min: int = 0, gate_idle: int = -1, grid_blocks: int = 0, gate_eval: int = 0):
+        capi.check(capi.lib().vpt_gpu_set_tuning(self.h, gate_min, gate_idle, grid_blocks, gate_eval),
+                   "vpt_gpu_set_tuning")
+
+    PROFILE_BLOCKS = ["iter", "fetch", "pixel", "ray", "sample", "need_seg", "step", "draw", "trilinear",
+                      "event", "shadow_hit", "none", "nee_done", "finish"]
+
+    def profile(self, reset: bool = False) -> dict:
+        """SIMT profile of a -DVPT_PROFILE build: {block: (wave executions, mean active lanes)}."""
+        buf = (C.c_uint64 * 64)()
+        capi.check(capi.lib().vpt_gpu_profile(self.h, buf, 64, 1 if reset else 0), "vpt_gpu_profile")
+        out = {}
+        for i, name in enumerate(self.PROFILE_BLOCKS):
+            ex, lanes = int(buf[2 * i]), int(buf[2 * i + 1])
+            out[name] = (ex, round(lanes / ex, 2) if ex else 0.0)
+        return out
 
     def launch_info(self):
         g, b = C.c_int(), C.c_int()
