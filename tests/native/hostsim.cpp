@@ -23,6 +23,8 @@ struct HostEnv {
   float* records;
   int32_t tile_area;
   int32_t count(bool pred) { return pred ? 1 : 0; }  // one lane
+  uint64_t cnt[vpt::CNT_COUNT] = {};
+  void tally(int32_t k, int32_t w) { cnt[k] += (uint64_t)w; }
   void prof(int32_t) {}
   bool fetch_job(uint64_t& j) {
     if (next >= jid_count) return false;
@@ -79,16 +81,8 @@ extern "C" int vpths_render_jobs(const vpt_configuration* cfg, const vpt_grid_de
   else
     while (ln.state != vpt::ST_DONE) vpt::lane_iteration<false, true>(S, ln, env);
   if (counters) {
-    counters->samples += ln.cnt.samples;
-    counters->dda_steps += ln.cnt.dda_steps;
-    counters->segments += ln.cnt.segments;
-    counters->draws += ln.cnt.draws;
-    counters->stencils += ln.cnt.stencils;
-    counters->density_evals += ln.cnt.density_evals;
-    counters->temp_stencils += ln.cnt.temp_stencils;
-    counters->scatters += ln.cnt.scatters;
-    counters->shadow_rays += ln.cnt.shadow_rays;
-    counters->rng_draws += ln.cnt.rng_draws;
+    uint64_t* o = reinterpret_cast<uint64_t*>(counters);
+    for (int k = 0; k < vpt::CNT_COUNT; ++k) o[k] += env.cnt[k];
   }
   return 0;
 }

@@ -32,7 +32,7 @@ int set_error(int code, const std::string& msg) {
       return ::vpt::set_error(VPT_E_HIP, std::string(#call " failed: ") + hipGetErrorString(e_));            \
   } while (0)
 
-constexpr int kCounterCount = 10;
+constexpr int kCounterCount = CNT_COUNT;
 constexpr int kBlockThreads = 256;
 #ifdef VPT_LB
 #define VPT_LB_ARG , VPT_LB
@@ -48,6 +48,14 @@ struct KernelEnv {
   float* records;
   int32_t tile_area;
   unsigned long long* prof_buf;  // [PB_COUNT][2] wave executions, active lanes (VPT_PROFILE builds)
+  unsigned long long* lds_counters;  // this workgroup's event counters (LDS)
+
+  // Adds w for every active lane with w != 0 (w uniform per call site) to a workgroup counter.
+  __device__ __forceinline__ void tally(int32_t k, int32_t w) {
+    const unsigned long long m = __ballot(w != 0);
+    if (m && __lane_id() == (uint32_t)__builtin_ctzll(m))
+      atomicAdd(lds_counters + k, (unsigned long long)(__popcll(m) * (uint64_t)(w ? w : 1)));
+  }
 
   __device__ __forceinline__ void prof(int32_t id) {
 #ifdef VPT_PROFILE
@@ -89,14 +97,16 @@ struct KernelEnv {
 template <bool HasTemp, bool Debug>
 __global__ __launch_bounds__(kBlockThreads VPT_LB_ARG) void vpt_integrate_kernel(DevScene S, KernelEnv env,
                                                                        unsigned long long* counters) {
+  __shared__ unsigned long long wg_counters[kCounterCount];
+  if (threadIdx.x < kCounterCount) wg_counters[threadIdx.x] = 0;
+  __syncthreads();
+  env.lds_counters = wg_counters;
   Lane ln;
   lane_init(ln);
   while (ln.state != ST_DONE) lane_iteration<HasTemp, Debug>(S, ln, env);
-  const LaneCounters& c = ln.cnt;
-  const uint32_t v[kCounterCount] = {c.samples, c.dda_steps, c.segments, c.draws, c.stencils,
-                                     c.density_evals, c.temp_stencils, c.scatters, c.shadow_rays, c.rng_draws};
-  for (int i = 0; i < kCounterCount; ++i)
-    if (v[i]) atomicAdd(counters + i, (unsigned long long)v[i]);
+  __syncthreads();
+  if (threadIdx.x < kCounterCount && wg_counters[threadIdx.x])
+    atomicAdd(counters + threadIdx.x, wg_counters[threadIdx.x]);
 }
 
 // ------------------------------------------------------------------------------------------------

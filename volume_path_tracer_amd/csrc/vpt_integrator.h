@@ -112,9 +112,21 @@ __host__ __device__ __forceinline__ void fetch_stencil(const DevGrid& g, Cell c,
     v[6] = b[90];
     v[7] = b[91];
   } else {
-    for (int a = 0; a < 2; ++a)
-      for (int b = 0; b < 2; ++b)
-        for (int cc = 0; cc < 2; ++cc) v[a * 4 + b * 2 + cc] = value_at(g, i + a, j + b, k + cc);
+    // Corner cell without a leaf (tile / background cell, rare): eight getValue calls, one at a
+    // time — a compact loop whose lookups are not all in flight at once (register pressure), the
+    // result selected into statically indexed registers.
+#pragma unroll 1
+    for (int q = 0; q < 8; ++q) {
+      const float val = value_at(g, i + (q >> 2), j + ((q >> 1) & 1), k + (q & 1));
+      v[0] = q == 0 ? val : v[0];
+      v[1] = q == 1 ? val : v[1];
+      v[2] = q == 2 ? val : v[2];
+      v[3] = q == 3 ? val : v[3];
+      v[4] = q == 4 ? val : v[4];
+      v[5] = q == 5 ? val : v[5];
+      v[6] = q == 6 ? val : v[6];
+      v[7] = q == 7 ? val : v[7];
+    }
   }
 }
 
@@ -301,11 +313,12 @@ enum : int32_t {
   PB_EVENT, PB_SHADOW_HIT, PB_NONE, PB_NEE_DONE, PB_FINISH, PB_COUNT
 };
 
-// Event counters.  The production kernel keeps the four that price algorithmic bytes
-// (SURVEY §8d); the debug kernel (per-sample records) keeps all of them for parity checks.
-struct LaneCounters {
-  uint32_t samples, dda_steps, stencils, temp_stencils;
-  uint32_t segments, draws, density_evals, scatters, shadow_rays, rng_draws;
+// Event counters, in vpt_counters order.  They are tallied per wavefront (env.tally) rather than
+// held per lane.  The production kernel counts the four that price algorithmic bytes;
+// the debug kernel (per-sample records) counts all of them for parity checks.
+enum : int32_t {
+  CNT_SAMPLES = 0, CNT_DDA_STEPS, CNT_SEGMENTS, CNT_DRAWS, CNT_STENCILS, CNT_DENSITY_EVALS, CNT_TEMP_STENCILS,
+  CNT_SCATTERS, CNT_SHADOW_RAYS, CNT_RNG_DRAWS, CNT_COUNT
 };
 
 struct Lane {
@@ -327,7 +340,6 @@ struct Lane {
   // current majorant segment
   float s_t0, s_t1, s_dmaj;
   StencilCell dens_cell, temp_cell;
-  LaneCounters cnt;
 };
 
 // HDDA step direction and per-cell increment from the (normalised, index-space) direction:
@@ -404,24 +416,20 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
 // Returns true when the segment [s_t0, s_t1) with majorant s_dmaj is complete.
 __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
   ln.s_dmaj = ln.maj;
-  ++ln.cnt.dda_steps;
-  // HDDA::step(): axis = MinIndex(next); static indices keep the lane state in VGPRs.
+  // HDDA::step(): axis = MinIndex(next).  Written as selects over all three axes: branches (or an
+  // axis index) make the compiler move the HDDA state into an indexed scratch array.
   const float n0 = ln.nxt[0], n1 = ln.nxt[1], n2 = ln.nxt[2];
   const float fdim = (float)ln.dim;
-  float tn;
-  if (n0 < n1 && n0 < n2) {
-    tn = n0;
-    ln.nxt[0] = tn + fdim * fabsf(ln.inv[0]);
-    ln.vox[0] += ln.dim * hdda_stp(ln.d[0], ln.inv[0]);
-  } else if (n1 < n2) {
-    tn = n1;
-    ln.nxt[1] = tn + fdim * fabsf(ln.inv[1]);
-    ln.vox[1] += ln.dim * hdda_stp(ln.d[1], ln.inv[1]);
-  } else {
-    tn = n2;
-    ln.nxt[2] = tn + fdim * fabsf(ln.inv[2]);
-    ln.vox[2] += ln.dim * hdda_stp(ln.d[2], ln.inv[2]);
-  }
+  const bool a0 = n0 < n1 && n0 < n2;
+  const bool a1 = !a0 && n1 < n2;
+  const bool a2 = !a0 && !a1;
+  const float tn = a0 ? n0 : (a1 ? n1 : n2);
+  ln.nxt[0] = a0 ? tn + fdim * fabsf(ln.inv[0]) : n0;
+  ln.nxt[1] = a1 ? tn + fdim * fabsf(ln.inv[1]) : n1;
+  ln.nxt[2] = a2 ? tn + fdim * fabsf(ln.inv[2]) : n2;
+  ln.vox[0] += a0 ? ln.dim * hdda_stp(ln.d[0], ln.inv[0]) : 0;
+  ln.vox[1] += a1 ? ln.dim * hdda_stp(ln.d[1], ln.inv[1]) : 0;
+  ln.vox[2] += a2 ? ln.dim * hdda_stp(ln.d[2], ln.inv[2]) : 0;
   ln.T0 = tn;
   if (!(tn <= ln.T1)) {
     ln.s_t1 = ln.T1;
@@ -556,7 +564,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     }
     float jx = rng_uniform(ln.rng);
     float jy = rng_uniform(ln.rng);
-    if (Debug) ln.cnt.rng_draws += 2;
+    if (Debug) env.tally(CNT_RNG_DRAWS, 2);
     jx *= S.jitter_scale;
     jy *= S.jitter_scale;
     // Camera::generate_ray (camera.hpp:14-23)
@@ -592,7 +600,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
       float dir[3];
       for (int i = 0; i < 3; ++i) dir[i] = shadow ? S.wi[i] : ln.rd[i];
       if (begin_ray(G, ln, ln.ro, dir)) {
-        if (Debug && shadow) ++ln.cnt.shadow_rays;
+        if (Debug) env.tally(CNT_SHADOW_RAYS, shadow ? 1 : 0);
         ln.state = ST_SAMPLE;
       } else {
         ln.state = shadow ? ST_NEE_DONE : ST_FINISH;  // shadow miss: T_ray stays 1
@@ -617,8 +625,9 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     }
     if (ln.state == ST_SAMPLE && ln.sm == SM_STEP) {
       env.prof(PB_STEP);
+      env.tally(CNT_DDA_STEPS, 1);
       if (hdda_step(G, ln)) {
-        if (Debug) ++ln.cnt.segments;
+        if (Debug) env.tally(CNT_SEGMENTS, 1);
         ln.sm = (ln.s_dmaj <= 0.0f) ? SM_NEED_SEG : SM_DRAW;  // empty segment: no draw (:32-35)
       }
     }
@@ -628,8 +637,8 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
       float sigma_maj = ln.s_dmaj * S.sigma_t;
       float u = rng_uniform(ln.rng);
       if (Debug) {
-        ++ln.cnt.draws;
-        ++ln.cnt.rng_draws;
+        env.tally(CNT_DRAWS, 1);
+        env.tally(CNT_RNG_DRAWS, 1);
       }
       float dt_m = -math::logf_glibc(1 - u) / sigma_maj;
       float t = ln.s_t0 + dt_m / ln.scale;
@@ -652,8 +661,8 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     const float sigma_maj = ln.s_dmaj * S.sigma_t;
     float pi_x = ln.e[0] + ln.d[0] * t, pi_y = ln.e[1] + ln.d[1] * t, pi_z = ln.e[2] + ln.d[2] * t;
     float dens;
-    if (Debug) ++ln.cnt.density_evals;
-    if (trilinear(G, ln.dens_cell, pi_x, pi_y, pi_z, dens)) ++ln.cnt.stencils;
+    if (Debug) env.tally(CNT_DENSITY_EVALS, 1);
+    env.tally(CNT_STENCILS, trilinear(G, ln.dens_cell, pi_x, pi_y, pi_z, dens) ? 1 : 0);
     ln.sm = SM_DRAW;  // density <= 0, a null event or an unkilled shadow ray: keep drawing
     if (dens > 0.0f) {
       float cp[3];
@@ -667,7 +676,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
         if (HasTemp) {
           float tx, ty, tz, tadim, X, Y, Z;
           map_inv(S.temperature, cp[0], cp[1], cp[2], tx, ty, tz);
-          if (trilinear(S.temperature, ln.temp_cell, tx, ty, tz, tadim)) ++ln.cnt.temp_stencils;
+          env.tally(CNT_TEMP_STENCILS, trilinear(S.temperature, ln.temp_cell, tx, ty, tz, tadim) ? 1 : 0);
           float tK = tadim * S.temp_scale + S.temp_offset;
           blackbody_xyz(S, tK, X, Y, Z);
           float sc = p_a * S.le_scale;
@@ -676,7 +685,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
           ln.L[2] = ln.L[2] + sc * Z;
         }
         float ue = rng_uniform(ln.rng);
-        if (Debug) ++ln.cnt.rng_draws;
+        if (Debug) env.tally(CNT_RNG_DRAWS, 1);
         // sample_discrete({Null p_n, Absorption p_a, Scatter p_s}, u) (random.hpp:30-47)
         float total = ((0.0f + p_n) + p_a) + p_s;
         float uu = ue * total;
@@ -696,7 +705,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
             ln.terminated = 1;
             ln.state = ST_FINISH;
           } else {
-            if (Debug) ++ln.cnt.scatters;
+            if (Debug) env.tally(CNT_SCATTERS, 1);
             // The next primary ray starts at the scatter point (worker.cpp:179): keep it in ro.
             for (int i = 0; i < 3; ++i) ln.ro[i] = cp[i];
             // sample_Ld (worker.cpp:52-90)
@@ -718,7 +727,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
         ln.Tr *= sigma_n / sigma_maj;
         if (ln.Tr <= 0.05f) {
           float q = 0.75f;
-          if (Debug) ++ln.cnt.rng_draws;
+          if (Debug) env.tally(CNT_RNG_DRAWS, 1);
           if (rng_uniform(ln.rng) < q)
             ln.Tr = 0.0f;
           else
@@ -749,7 +758,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     }
     float u0 = rng_uniform(ln.rng);
     float u1 = rng_uniform(ln.rng);
-    if (Debug) ln.cnt.rng_draws += 2;
+    if (Debug) env.tally(CNT_RNG_DRAWS, 2);
     float nd[3];
     sample_hg(ln.rd, u0, u1, S.g_hg, nd);
     for (int i = 0; i < 3; ++i) ln.rd[i] = nd[i];
@@ -768,7 +777,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     // the pixel just traced is pix - 1 of the tile
     const int32_t q = ln.pix - 1, y = q / rw;
     env.film_add(S, ln, ln.x0 + (q - y * rw), ln.y0 + y, rw);
-    ++ln.cnt.samples;
+    env.tally(CNT_SAMPLES, 1);
     ln.state = ST_PIXEL;
   }
 }
@@ -782,7 +791,6 @@ __host__ __device__ __forceinline__ void lane_init(Lane& ln) {
   ln.dens_cell.code = -1;
   ln.temp_cell.i = kNoCell;
   ln.temp_cell.code = -1;
-  ln.cnt = LaneCounters{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 }
 
 }  // namespace vpt
