@@ -79,6 +79,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3")
     ap.add_argument("--spp", type=int, default=None, help="override waves per step (default: the config's)")
+    ap.add_argument("--mode", choices=["weak", "strong"], default="weak",
+                    help="weak: each rank renders its own spp waves; strong: the spp waves are dealt across ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -97,6 +99,7 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
 
+    from volume_path_tracer_amd import distributed as D
     from volume_path_tracer_amd.render import Integrator
     from volume_path_tracer_amd.scenes import SynthGrid, workload
 
@@ -110,21 +113,22 @@ def main():
         f"launch {it.launch_info()}")
 
     spp = wl.spp
-    first_wave = 1 + rank * spp  # weak scaling: each rank its own block of waves
+    ranges = D.rank_job_ranges(rank, world, spp, it.jobs_per_wave, args.mode)
+    jobs_rank = sum(n for _, n in ranges)
     stream = torch.cuda.current_stream(dev)
     launch_ms = []
 
     def step(timed: bool):
         it.film.zero_()
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        ev0.record(stream)
-        it.render_waves(first_wave, spp, stream=stream)
-        ev1.record(stream)
-        if world > 1:
-            dist.all_reduce(it.film, op=dist.ReduceOp.SUM)
-        if timed:
-            launch_ms.append((ev0, ev1))
+        for b, n in ranges:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev0.record(stream)
+            it.render_jobs(b, n, stream=stream)
+            ev1.record(stream)
+            if timed:
+                launch_ms.append((ev0, ev1))
+        D.reduce_film(it.film)
 
     for _ in range(args.warmup):
         step(False)
@@ -147,14 +151,19 @@ def main():
 
     kernel_ms = [a.elapsed_time(b) for a, b in launch_ms]
     counters = it.counters()
-    samples_rank = wl.cfg.width * wl.cfg.height * spp * args.steps
-    assert counters["samples"] == samples_rank, (counters["samples"], samples_rank)
-    total_samples = samples_rank * world
+    area = int(wl.cfg.tile_size[0] * wl.cfg.tile_size[1])
+    samples_rank = counters["samples"]
+    assert samples_rank == (wl.cfg.width * wl.cfg.height * jobs_rank // it.jobs_per_wave) * args.steps, samples_rank
+    t = torch.tensor([samples_rank], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    total_samples = int(t.item())
     value = total_samples / elapsed / 1e6
+    launches_per_step = len(ranges)
 
     if rank == 0:
         avg_launch_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-        bytes_per_launch = algorithmic_bytes(counters) / args.steps
+        bytes_per_launch = algorithmic_bytes(counters) / (args.steps * launches_per_step)
         achieved = bytes_per_launch / avg_launch_s / 1e9
         traffic = None
         pmc = sorted((ROOT / "profiles").glob("*_pmc.json"))
@@ -166,7 +175,7 @@ def main():
             except Exception:
                 traffic = None
         film = it.film_host()
-        assert (film[..., 3] == spp * world).all(), "sample-count channel mismatch"
+        assert (film[..., 3] == D.total_samples_per_pixel(world, spp, args.mode)).all(), "sample-count channel mismatch"
         out = {
             "metric": "Msamples/s (whole node) + achieved HBM GB/s, wdas_cloud 1920x1080",
             "value": round(value, 3),
@@ -176,20 +185,21 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.mode,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (512^3 procedural cloud stand-in for wdas_cloud.nvdb, SURVEY §8d)",
-            "config": {"workload": f"{args.config}: wdas_cloud.json {wl.cfg.width}x{wl.cfg.height}, "
-                                   f"{spp} spp per GPU, 8x8 tiles, seed {wl.cfg.seed}",
-                       "width": wl.cfg.width, "height": wl.cfg.height, "spp_per_gpu": spp,
-                       "jobs_per_step": it.jobs_per_wave * spp, "volume": f"synthetic {wl.grid_n}^3 kind {wl.density_kind}",
-                       "parallelism": f"wave-sharded x{world}, RCCL film all-reduce" if world > 1 else "1 GPU"},
+            "config": {"workload": f"{args.config}: {'fire' if wl.temperature else 'wdas_cloud'}.json "
+                                   f"{wl.cfg.width}x{wl.cfg.height}, {spp} spp "
+                                   f"{'per GPU' if args.mode == 'weak' else 'per image'}, 8x8 tiles, seed {wl.cfg.seed}",
+                       "width": wl.cfg.width, "height": wl.cfg.height, "spp": spp,
+                       "jobs_per_step_per_gpu": jobs_rank, "volume": f"synthetic {wl.grid_n}^3 kind {wl.density_kind}",
+                       "parallelism": f"wave-sharded x{world} ({args.mode}), RCCL film all-reduce" if world > 1 else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": "vpt_integrate_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                          "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                         "bytes_per_sample": round(bytes_per_launch / (samples_rank / args.steps), 2)},
+                         "bytes_per_sample": round(algorithmic_bytes(counters) / samples_rank, 2)},
             "counters_per_sample": {k: round(v / samples_rank, 3) for k, v in counters.items() if k != "samples"},
         }
         if world == 1 and not args.no_cpu_baseline:
