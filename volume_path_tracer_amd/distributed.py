@@ -5,8 +5,9 @@ wave balances perfectly and keeps every RNG stream identical to the 1-GPU / CPU 
 
 * ``weak``:  rank r renders its own block of ``spp`` waves, r*spp+1 .. (r+1)*spp — the per-GPU
              work is fixed as N grows and the reduced film holds N*spp samples per pixel.
-* ``strong``: the ``spp`` waves of one image are dealt round-robin, wave w -> rank (w-1) mod N
-             (SURVEY §8e), so N GPUs share one fixed image.
+* ``strong``: the ``spp`` waves of one image are split into N contiguous, balanced blocks (the
+             round-robin deal of SURVEY §8e balances the same way; contiguous blocks keep it to one
+             persistent-kernel launch per rank), so N GPUs share one fixed image.
 
 After rendering, the H*W*4 fp32 films are summed over the ranks with one all-reduce
 (RCCL over xGMI for the "nccl" backend; gloo in the CPU tests) — the only exchange the path has.
@@ -23,14 +24,10 @@ def rank_wave_ranges(rank: int, world: int, spp: int, mode: str = "weak") -> Lis
     if mode == "weak":
         return [(1 + rank * spp, spp)]
     if mode == "strong":
-        waves = [w for w in range(1, spp + 1) if (w - 1) % world == rank]
-        runs: List[Tuple[int, int]] = []
-        for w in waves:
-            if runs and runs[-1][0] + runs[-1][1] == w:
-                runs[-1] = (runs[-1][0], runs[-1][1] + 1)
-            else:
-                runs.append((w, 1))
-        return runs
+        base, extra = divmod(spp, world)
+        first = 1 + rank * base + min(rank, extra)
+        n = base + (1 if rank < extra else 0)
+        return [(first, n)] if n else []
     raise ValueError(f"unknown mode {mode!r}")
 
 
