@@ -57,6 +57,7 @@ extern "C" int vpths_render_jobs(const vpt_configuration* cfg, const vpt_grid_de
   vpt::HostGrid hd, ht;
   if ((rc = vpt::build_host_grid(*density, true, 0, hd))) return rc;
   S.density = hd.dev;
+  vpt::scene_finalize(S);
   if (temperature) {
     if ((rc = vpt::build_host_grid(*temperature, false, 0, ht))) return rc;
     S.temperature = ht.dev;
@@ -80,6 +81,8 @@ extern "C" int vpths_render_jobs(const vpt_configuration* cfg, const vpt_grid_de
     while (ln.state != vpt::ST_DONE) vpt::lane_iteration<true, true>(S, ln, env);
   else
     while (ln.state != vpt::ST_DONE) vpt::lane_iteration<false, true>(S, ln, env);
+  env.cnt[vpt::CNT_DDA_STEPS] += ln.n_dda;
+  env.cnt[vpt::CNT_STENCILS] += ln.n_stencil;
   if (counters) {
     uint64_t* o = reinterpret_cast<uint64_t*>(counters);
     for (int k = 0; k < vpt::CNT_COUNT; ++k) o[k] += env.cnt[k];
@@ -124,6 +127,7 @@ extern "C" int64_t vpths_math_mismatches(int which) {
     if (which == 0) {
       float x = 1.0f - u;
       if (vpt::math::as_u32(vpt::math::logf_glibc(x)) != vpt::math::as_u32(std::log(x))) ++bad;
+      if (vpt::math::as_u32(vpt::math::logf_glibc_unit(x)) != vpt::math::as_u32(std::log(x))) ++bad;
     } else {
       float phi = 2.0f * 3.14159274f * u;
       if (which == 1 && vpt::math::as_u32(vpt::math::sinf_glibc(phi)) != vpt::math::as_u32(std::sin(phi))) ++bad;

@@ -104,6 +104,8 @@ __global__ __launch_bounds__(kBlockThreads VPT_LB_ARG) void vpt_integrate_kernel
   Lane ln;
   lane_init(ln);
   while (ln.state != ST_DONE) lane_iteration<HasTemp, Debug>(S, ln, env);
+  atomicAdd(wg_counters + CNT_DDA_STEPS, (unsigned long long)ln.n_dda);
+  atomicAdd(wg_counters + CNT_STENCILS, (unsigned long long)ln.n_stencil);
   __syncthreads();
   if (threadIdx.x < kCounterCount && wg_counters[threadIdx.x])
     atomicAdd(counters + threadIdx.x, wg_counters[threadIdx.x]);
@@ -251,6 +253,7 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
     if ((rc = vpt::upload_grid(h, ctx->temperature))) return rc;
   }
   ctx->scene.density = ctx->density.dev;
+  vpt::scene_finalize(ctx->scene);  // uses only the density map (host copy of the values)
   ctx->scene.temperature = ctx->temperature.dev;
   ctx->scene.has_temperature = temperature ? 1 : 0;
 

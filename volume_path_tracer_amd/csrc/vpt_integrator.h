@@ -58,14 +58,14 @@ struct Cell {
 __host__ __device__ __forceinline__ Cell cell_at(const DevGrid& g, int32_t i, int32_t j, int32_t k) {
   int32_t a = (i - g.r8_org[0]) >> 3, b = (j - g.r8_org[1]) >> 3, c = (k - g.r8_org[2]) >> 3;
   if ((uint32_t)a < (uint32_t)g.r8_n[0] && (uint32_t)b < (uint32_t)g.r8_n[1] && (uint32_t)c < (uint32_t)g.r8_n[2]) {
-    int2 e = g.cells8[((int64_t)a * g.r8_n[1] + b) * g.r8_n[2] + c];
+    int2 e = g.cells8[((uint32_t)a * (uint32_t)g.r8_n[1] + (uint32_t)b) * (uint32_t)g.r8_n[2] + (uint32_t)c];
     return Cell{e.x, math::as_f32((uint32_t)e.y)};
   }
   a = (i - g.r128_org[0]) >> 7;
   b = (j - g.r128_org[1]) >> 7;
   c = (k - g.r128_org[2]) >> 7;
   if ((uint32_t)a < (uint32_t)g.r128_n[0] && (uint32_t)b < (uint32_t)g.r128_n[1] && (uint32_t)c < (uint32_t)g.r128_n[2]) {
-    int2 e = g.cells128[((int64_t)a * g.r128_n[1] + b) * g.r128_n[2] + c];
+    int2 e = g.cells128[((uint32_t)a * (uint32_t)g.r128_n[1] + (uint32_t)b) * (uint32_t)g.r128_n[2] + (uint32_t)c];
     return Cell{e.x, math::as_f32((uint32_t)e.y)};
   }
   for (int32_t r = 0; r < g.root_count; ++r) {
@@ -204,6 +204,12 @@ struct DevScene {
   float Li[3];          // distant_light.xyz * multiplier (worker.cpp:55)
   int32_t li_zero;      // Li == 0 -> sample_Ld returns before any draw (worker.cpp:57-58)
   float wi[3];          // distant_light.inv_direction.normalized() (worker.cpp:54)
+  // Shadow rays all have direction wi: their index-space direction, its reciprocal, the length
+  // factor and the iterator scale are scene constants (scene_finalize; same float operations).
+  float sh_d[3], sh_inv[3], sh_len, sh_scale;
+  // Henyey-Greenstein terms that depend on g only (random.hpp:56-84, utils.hpp:61-66): the same
+  // float values the reference recomputes at every call.
+  float hg_g2, hg_1pg2, hg_1mg2, hg_1pg, hg_2g, hg_inv2g, hg_num;
   float sigma_a, sigma_s, sigma_t, g_hg, le_scale, temp_scale, temp_offset;
   // Wave gating of the rare states: a rare block runs when at least gate_min lanes of the wavefront
   // wait for it, or when fewer than gate_idle lanes are sampling (1/64 = always run).
@@ -304,7 +310,8 @@ enum : int32_t {
   ST_SAMPLE = 3,  // inside MajorantTransmittanceSampler::next (primary or shadow ray)
   ST_NEE_DONE = 4,
   ST_FINISH = 5,  // pixel done: environment light, film
-  ST_DONE = 6
+  ST_DONE = 6,
+  ST_SHADOW = 7   // sample_Ld's Volume::intersect + iterator setup (direction wi: constants)
 };
 enum : int32_t { SM_NEED_SEG = 0, SM_STEP = 1, SM_DRAW = 2, SM_EVAL = 3 };  // SM_EVAL: density at s_t0 pending
 // Block ids for the optional SIMT-utilisation profile (env.prof; a no-op unless VPT_PROFILE).
@@ -337,29 +344,52 @@ struct Lane {
   float T0, T1;
   float nxt[3];
   int32_t vox[3];
+  float finc[3];    // HDDA: dim * delta[axis] (the float product NanoVDB adds at every step)
+  int32_t vinc[3];  // HDDA: dim * step[axis]
   // current majorant segment
   float s_t0, s_t1, s_dmaj;
   StencilCell dens_cell, temp_cell;
+  uint32_t n_dda, n_stencil;  // hot counters, per lane (flushed by the kernel at exit)
 };
 
 // HDDA step direction and per-cell increment from the (normalised, index-space) direction:
 // step = 0 if dir == 0, +1 if invDir > 0, else -1; delta = |invDir| (NanoVDB HDDA::init).
 __host__ __device__ __forceinline__ int32_t hdda_stp(float d, float inv) { return d == 0.0f ? 0 : (inv > 0 ? 1 : -1); }
 
-// Volume::intersect (volume.cpp:78-88) + RayMajorantIterator ctor (volume.cpp:90-98).
-__host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, const float o[3], const float dir[3]) {
-  // nanovdb::math::Ray<float>(eye, dir) with t0 = 1e-5 (Delta<float>), t1 = FLT_MAX; worldToIndexF.
-  float ex, ey, ez, dx, dy, dz;
-  map_inv(g, o[0], o[1], o[2], ex, ey, ez);
+// The direction-only part of Ray::worldToIndexF + RayMajorantIterator's scale: index-space unit
+// direction d, invDir = 1/d, |worldToIndexDirF(dir)| (scales t0) and m_scale.
+struct RayDir {
+  float d[3], inv[3], len, scale;
+};
+__host__ __device__ __forceinline__ RayDir ray_dir_setup(const DevGrid& g, const float dir[3]) {
+  RayDir r;
+  float dx, dy, dz;
   jac_inv(g, dir[0], dir[1], dir[2], dx, dy, dz);
   float len = sqrtf(dx * dx + dy * dy + dz * dz);
   float inv_len = 1.0f / len;
-  dx = dx * inv_len;
-  dy = dy * inv_len;
-  dz = dz * inv_len;
-  float t0 = len * 1e-5f;
+  r.d[0] = dx * inv_len;
+  r.d[1] = dy * inv_len;
+  r.d[2] = dz * inv_len;
+  r.len = len;
+  r.inv[0] = 1 / r.d[0];
+  r.inv[1] = 1 / r.d[1];
+  r.inv[2] = 1 / r.d[2];
+  // m_scale = 1 / |worldToIndexDirF(index dir)|
+  float jx, jy, jz;
+  jac_inv(g, r.d[0], r.d[1], r.d[2], jx, jy, jz);
+  r.scale = 1 / sqrtf(jx * jx + jy * jy + jz * jz);
+  return r;
+}
+
+// Volume::intersect (volume.cpp:78-88) + RayMajorantIterator ctor (volume.cpp:90-98).
+__host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, const float o[3], const RayDir& rd) {
+  // nanovdb::math::Ray<float>(eye, dir) with t0 = 1e-5 (Delta<float>), t1 = FLT_MAX; worldToIndexF.
+  float ex, ey, ez;
+  map_inv(g, o[0], o[1], o[2], ex, ey, ez);
+  const float dx = rd.d[0], dy = rd.d[1], dz = rd.d[2];
+  float t0 = rd.len * 1e-5f;
   float t1 = 3.40282347e+38f;
-  float ix = 1 / dx, iy = 1 / dy, iz = 1 / dz;
+  const float ix = rd.inv[0], iy = rd.inv[1], iz = rd.inv[2];
   // Ray::clip(indexBBox): slab test against [min, max + 1].
   const float E[3] = {ex, ey, ez}, I[3] = {ix, iy, iz};
   for (int a = 0; a < 3; ++a) {
@@ -384,10 +414,7 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
   ln.inv[0] = ix;
   ln.inv[1] = iy;
   ln.inv[2] = iz;
-  // m_scale = 1 / |worldToIndexDirF(index dir)|
-  float jx, jy, jz;
-  jac_inv(g, dx, dy, dz, jx, jy, jz);
-  ln.scale = 1 / sqrtf(jx * jx + jy * jy + jz * jz);
+  ln.scale = rd.scale;
   ln.maj = __builtin_nanf("");
   // HDDA(ray, max(8, getDim(floor(ray.start())))) -> init(ray, t0, t1, dim)
   float px = ex + dx * t0, py = ey + dy * t0, pz = ez + dz * t0;
@@ -399,6 +426,8 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
   for (int a = 0; a < 3; ++a) {
     int32_t v = ((int32_t)floorf(P[a])) & (~(dim - 1));
     ln.vox[a] = v;
+    ln.finc[a] = (float)dim * fabsf(I[a]);
+    ln.vinc[a] = dim * hdda_stp(D[a], I[a]);
     if (D[a] == 0.0f)
       ln.nxt[a] = 3.40282347e+38f;
     else if (I[a] > 0)
@@ -419,17 +448,17 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
   // HDDA::step(): axis = MinIndex(next).  Written as selects over all three axes: branches (or an
   // axis index) make the compiler move the HDDA state into an indexed scratch array.
   const float n0 = ln.nxt[0], n1 = ln.nxt[1], n2 = ln.nxt[2];
-  const float fdim = (float)ln.dim;
   const bool a0 = n0 < n1 && n0 < n2;
   const bool a1 = !a0 && n1 < n2;
   const bool a2 = !a0 && !a1;
   const float tn = a0 ? n0 : (a1 ? n1 : n2);
-  ln.nxt[0] = a0 ? tn + fdim * fabsf(ln.inv[0]) : n0;
-  ln.nxt[1] = a1 ? tn + fdim * fabsf(ln.inv[1]) : n1;
-  ln.nxt[2] = a2 ? tn + fdim * fabsf(ln.inv[2]) : n2;
-  ln.vox[0] += a0 ? ln.dim * hdda_stp(ln.d[0], ln.inv[0]) : 0;
-  ln.vox[1] += a1 ? ln.dim * hdda_stp(ln.d[1], ln.inv[1]) : 0;
-  ln.vox[2] += a2 ? ln.dim * hdda_stp(ln.d[2], ln.inv[2]) : 0;
+  // mNext[axis] += mDim * mDelta[axis]; mVoxel[axis] += mDim * mStep[axis]
+  ln.nxt[0] = a0 ? tn + ln.finc[0] : n0;
+  ln.nxt[1] = a1 ? tn + ln.finc[1] : n1;
+  ln.nxt[2] = a2 ? tn + ln.finc[2] : n2;
+  ln.vox[0] += a0 ? ln.vinc[0] : 0;
+  ln.vox[1] += a1 ? ln.vinc[1] : 0;
+  ln.vox[2] += a2 ? ln.vinc[2] : 0;
   ln.T0 = tn;
   if (!(tn <= ln.T1)) {
     ln.s_t1 = ln.T1;
@@ -448,6 +477,8 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
     for (int b = 0; b < 3; ++b) ln.vox[b] = ((int32_t)floorf(P[b])) & (~(nd - 1));
     for (int b = 0; b < 3; ++b) {
       const int32_t st = hdda_stp(ln.d[b], ln.inv[b]);
+      ln.finc[b] = (float)nd * fabsf(ln.inv[b]);
+      ln.vinc[b] = nd * st;
       if (st == 0) continue;
       float n = ln.T0 + ((float)ln.vox[b] - P[b]) * ln.inv[b];
       if (st > 0) n += (float)nd * ln.inv[b];
@@ -466,14 +497,15 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
 // ------------------------------------------------------------------------------------------------
 // Phase function helpers (random.hpp:56-84, utils.hpp:39-66)
 // ------------------------------------------------------------------------------------------------
-__host__ __device__ __forceinline__ void sample_hg(const float w[3], float u0, float u1, float g, float out[3]) {
-  float g2 = g * g;  // std::pow(g, 2.0f): the correctly rounded square (tests/test_math_clone.py)
+__host__ __device__ __forceinline__ void sample_hg(const DevScene& S, const float w[3], float u0, float u1, float out[3]) {
+  const float g = S.g_hg;
   float cos_theta;
   if (fabsf(g) < 1e-3f) {
     cos_theta = 1 - 2 * u0;
   } else {
-    float q = (1.0f - g2) / (1.0f + g - 2.0f * g * u0);
-    cos_theta = 1.0f / (2.0f * g) * (1.0f + g2 - q * q);
+    // 1/(2g) * (1 + g2 - pow((1 - g2)/(1 + g - 2g u), 2)); pow(x, 2) is the correctly rounded square
+    float q = S.hg_1mg2 / (S.hg_1pg - S.hg_2g * u0);
+    cos_theta = S.hg_inv2g * (S.hg_1pg2 - q * q);
   }
   float sin_theta = sqrtf(fmaxf(0.0f, 1.0f - cos_theta * cos_theta));
   float phi = 2.0f * 3.14159274f * u1;
@@ -498,10 +530,30 @@ __host__ __device__ __forceinline__ void sample_hg(const float w[3], float u0, f
   out[2] = (lx * X2 + ly * Y2) + lz * w[2];
 }
 
-__host__ __device__ __forceinline__ float hg_eval(float cos_theta, float g) {
-  float den = 1.0f + g * g + 2.0f * g * cos_theta;
+// henyey_greenstein(cos, g) = inv_4_pi * (1 - g*g) / (den * sqrt(max(0, den))), den = 1 + g*g + 2g cos
+__host__ __device__ __forceinline__ float hg_eval(const DevScene& S, float cos_theta) {
+  float den = S.hg_1pg2 + S.hg_2g * cos_theta;
+  return S.hg_num / (den * sqrtf(fmaxf(0.0f, den)));
+}
+
+// Scene constants that depend on the density grid's map or on g (called once on the host).
+__host__ __device__ inline void scene_finalize(DevScene& S) {
+  RayDir r = ray_dir_setup(S.density, S.wi);
+  for (int i = 0; i < 3; ++i) {
+    S.sh_d[i] = r.d[i];
+    S.sh_inv[i] = r.inv[i];
+  }
+  S.sh_len = r.len;
+  S.sh_scale = r.scale;
+  const float g = S.g_hg;
+  S.hg_g2 = g * g;
+  S.hg_1pg2 = 1.0f + S.hg_g2;
+  S.hg_1mg2 = 1.0f - S.hg_g2;
+  S.hg_1pg = 1.0f + g;
+  S.hg_2g = 2.0f * g;
+  S.hg_inv2g = 1.0f / (2.0f * g);
   const float inv_4_pi = (float)(0.318309886183790671537767526745028724 / 4.0);  // float(inv_pi / 4.0)
-  return inv_4_pi * (1.0f - g * g) / (den * sqrtf(fmaxf(0.0f, den)));
+  S.hg_num = inv_4_pi * (1.0f - g * g);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -591,20 +643,31 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
 
   if (go(ST_RAY)) {
     env.prof(PB_RAY);
-    // Primary: for (depth < max_depth) { intersection = vol.intersect(r); if (!intersection) break; }
-    // Shadow: sample_Ld's vol.intersect(Ray(pos, wi)) (worker.cpp:64-65).
-    const bool shadow = ln.shadow != 0;
-    if (!shadow && !(ln.depth < S.max_depth)) {
+    // for (depth < max_depth) { intersection = vol.intersect(r); if (!intersection) break; ... }
+    if (!(ln.depth < S.max_depth)) {
       ln.state = ST_FINISH;
+    } else if (begin_ray(G, ln, ln.ro, ray_dir_setup(G, ln.rd))) {
+      ln.state = ST_SAMPLE;
     } else {
-      float dir[3];
-      for (int i = 0; i < 3; ++i) dir[i] = shadow ? S.wi[i] : ln.rd[i];
-      if (begin_ray(G, ln, ln.ro, dir)) {
-        if (Debug) env.tally(CNT_SHADOW_RAYS, shadow ? 1 : 0);
-        ln.state = ST_SAMPLE;
-      } else {
-        ln.state = shadow ? ST_NEE_DONE : ST_FINISH;  // shadow miss: T_ray stays 1
-      }
+      ln.state = ST_FINISH;
+    }
+  }
+
+  if (go(ST_SHADOW)) {
+    env.prof(PB_RAY);
+    // sample_Ld: vol.intersect(Ray(pos, wi)) (worker.cpp:64-65); a miss keeps T_ray = 1.
+    RayDir rd;
+    for (int i = 0; i < 3; ++i) {
+      rd.d[i] = S.sh_d[i];
+      rd.inv[i] = S.sh_inv[i];
+    }
+    rd.len = S.sh_len;
+    rd.scale = S.sh_scale;
+    if (begin_ray(G, ln, ln.ro, rd)) {
+      if (Debug) env.tally(CNT_SHADOW_RAYS, 1);
+      ln.state = ST_SAMPLE;
+    } else {
+      ln.state = ST_NEE_DONE;
     }
   }
 
@@ -625,7 +688,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     }
     if (ln.state == ST_SAMPLE && ln.sm == SM_STEP) {
       env.prof(PB_STEP);
-      env.tally(CNT_DDA_STEPS, 1);
+      ++ln.n_dda;
       if (hdda_step(G, ln)) {
         if (Debug) env.tally(CNT_SEGMENTS, 1);
         ln.sm = (ln.s_dmaj <= 0.0f) ? SM_NEED_SEG : SM_DRAW;  // empty segment: no draw (:32-35)
@@ -640,7 +703,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
         env.tally(CNT_DRAWS, 1);
         env.tally(CNT_RNG_DRAWS, 1);
       }
-      float dt_m = -math::logf_glibc(1 - u) / sigma_maj;
+      float dt_m = -math::logf_glibc_unit(1 - u) / sigma_maj;
       float t = ln.s_t0 + dt_m / ln.scale;
       if (t < ln.s_t1) {
         ln.s_t0 = t;       // the tentative collision; its density is evaluated in SM_EVAL
@@ -662,7 +725,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     float pi_x = ln.e[0] + ln.d[0] * t, pi_y = ln.e[1] + ln.d[1] * t, pi_z = ln.e[2] + ln.d[2] * t;
     float dens;
     if (Debug) env.tally(CNT_DENSITY_EVALS, 1);
-    env.tally(CNT_STENCILS, trilinear(G, ln.dens_cell, pi_x, pi_y, pi_z, dens) ? 1 : 0);
+    if (trilinear(G, ln.dens_cell, pi_x, pi_y, pi_z, dens)) ++ln.n_stencil;
     ln.sm = SM_DRAW;  // density <= 0, a null event or an unkilled shadow ray: keep drawing
     if (dens > 0.0f) {
       float cp[3];
@@ -715,7 +778,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
             } else {
               ln.Tr = 1.0f;
               ln.shadow = 1;
-              ln.state = ST_RAY;
+              ln.state = ST_SHADOW;
             }
           }
         }
@@ -746,7 +809,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     if (ln.Tr >= 0.0f) {
       // p * T_ray * Li with p = HG(w . wi)
       float c = ln.rd[0] * S.wi[0] + (ln.rd[1] * S.wi[1] + ln.rd[2] * S.wi[2]);
-      float p = hg_eval(c, S.g_hg);
+      float p = hg_eval(S, c);
       float pt = p * ln.Tr;
       ln.L[0] = ln.L[0] + pt * S.Li[0];
       ln.L[1] = ln.L[1] + pt * S.Li[1];
@@ -760,7 +823,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     float u1 = rng_uniform(ln.rng);
     if (Debug) env.tally(CNT_RNG_DRAWS, 2);
     float nd[3];
-    sample_hg(ln.rd, u0, u1, S.g_hg, nd);
+    sample_hg(S, ln.rd, u0, u1, nd);
     for (int i = 0; i < 3; ++i) ln.rd[i] = nd[i];
     ++ln.depth;  // the for-loop increment (worker.cpp:130)
     ln.shadow = 0;
@@ -791,6 +854,8 @@ __host__ __device__ __forceinline__ void lane_init(Lane& ln) {
   ln.dens_cell.code = -1;
   ln.temp_cell.i = kNoCell;
   ln.temp_cell.code = -1;
+  ln.n_dda = 0;
+  ln.n_stencil = 0;
 }
 
 }  // namespace vpt

@@ -72,6 +72,29 @@ __host__ __device__ __forceinline__ float logf_glibc(float x) {
   return (float)y;
 }
 
+// The integrator only takes log(1 - u), u = uniform<float>() in [0, 1 - 2^-24], so x is a normal
+// float in [2^-24, 1]: glibc's special-case branches (zero, subnormal, inf, nan, x == 1 rounding-mode
+// sign) never fire and are omitted (x == 1 gives +0 on the main path too).  Checked against glibc
+// over every such x by tests/test_math_clone.py.
+__host__ __device__ __forceinline__ float logf_glibc_unit(float x) {
+  const double Ln2 = 0x1.62e42fefa39efp-1;
+  const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2, A2 = -0x1.ffffef20a4123p-2;
+  const uint32_t ix = as_u32(x);
+  const uint32_t tmp = ix - 0x3f330000u;
+  const int i = (int)((tmp >> (23 - 4)) % 16u);
+  const int k = (int32_t)tmp >> 23;
+  const uint32_t iz = ix - (tmp & (0x1ffu << 23));
+  const double invc = kLogfTab[i][0], logc = kLogfTab[i][1];
+  const double z = (double)as_f32(iz);
+  const double r = __builtin_fma(z, invc, -1.0);
+  const double y0 = __builtin_fma((double)k, Ln2, logc);
+  const double r2 = r * r;
+  double y = __builtin_fma(A1, r, A2);
+  y = __builtin_fma(A0, r2, y);
+  y = __builtin_fma(y, r2, y0 + r);
+  return (float)y;
+}
+
 // sinf / cosf (glibc sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c, sincosf.h), for |x| < 120.
 // glibc's __sincosf_table[1] is table[0] with the cosine coefficients negated; since
 // fma(a, -b, -c) == -fma(a, b, c) exactly, using table[0] and negating the cosine result when
