@@ -141,6 +141,12 @@ int vpt_blackbody_table(float* out_500x3);
 /* blackbody_radiation_xyz(T) on the host, for tests. */
 int vpt_blackbody_xyz(const float* table_500x3, float temperature_k, float* out_xyz);
 
+/* ---- output: film_to_image (src/main.cpp:12-24, include/vpt/color.hpp:8-30) --------------- */
+
+/* XYZ/W -> linear sRGB (3x3 matrix) -> sRGB OETF -> clamp [0,1] -> *255 -> truncate to u8.
+ * film: float[h][w][4]; out: uint8[h][w][3] (the 8-bit RGB image the reference saves as PNG). */
+int vpt_film_to_srgb8(const float* film_hxwx4, int64_t w, int64_t h, uint8_t* out_hxwx3);
+
 /* ---- the integrator ---------------------------------------------------------------------- */
 
 typedef struct vpt_gpu_ctx vpt_gpu_ctx;

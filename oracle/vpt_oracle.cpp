@@ -1196,4 +1196,21 @@ vpt_grid_desc* vpto_synth_grid(int kind, int n) {
 
 void vpto_synth_free(vpt_grid_desc* d) { delete reinterpret_cast<OwnedDesc*>(d); }
 
+// film_to_image (main.cpp:12-24) with xyz_to_linsrgb / linsrgb_to_srgb (color.hpp:8-30).
+void vpto_film_to_image(const float* film, int64_t w, int64_t h, uint8_t* out) {
+  float m[9] = {(float)3.240479, (float)-1.537150, (float)-0.498535, (float)-0.969256, (float)1.875991,
+                (float)0.041556, (float)0.055648, (float)-0.204043, (float)1.057311};
+  auto srgb = [](float x) { return x <= 0.0031308f ? (12.92f * x) : (1.055f * std::pow(x, 1.0f / 2.4f) - 0.055f); };
+  for (int64_t i = 0; i < w * h; ++i) {
+    const float* p = film + i * 4;
+    V3 xyz = v3(p[0] / p[3], p[1] / p[3], p[2] / p[3]);
+    float lin[3];
+    for (int r = 0; r < 3; ++r) lin[r] = m[r * 3] * xyz.x + (m[r * 3 + 1] * xyz.y + m[r * 3 + 2] * xyz.z);
+    for (int c = 0; c < 3; ++c) {
+      float v = std::min(std::max(srgb(lin[c]), 0.0f), 1.0f) * 255.0f;  // cwiseMax(0).cwiseMin(1) * 255
+      out[i * 3 + c] = (v == v) ? (uint8_t)(int32_t)v : (uint8_t)0;  // cast<unsigned char>
+    }
+  }
+}
+
 }  // extern "C"

@@ -79,6 +79,9 @@ double vpto_render_pool(const vpt_configuration* cfg, const vpto_grid* density,
 vpt_grid_desc* vpto_synth_grid(int kind, int n);
 void vpto_synth_free(vpt_grid_desc* d);
 
+/* film_to_image (src/main.cpp:12-24): film[h][w][4] -> rgb8[h][w][3]. */
+void vpto_film_to_image(const float* film, int64_t w, int64_t h, uint8_t* out);
+
 #ifdef __cplusplus
 }
 #endif

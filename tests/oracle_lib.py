@@ -63,6 +63,7 @@ def lib() -> C.CDLL:
     L.vpto_synth_grid.argtypes = [C.c_int, C.c_int]
     L.vpto_synth_grid.restype = gridp
     L.vpto_synth_free.argtypes = [gridp]
+    L.vpto_film_to_image.argtypes = [fp, C.c_int64, C.c_int64, C.POINTER(C.c_uint8)]
     _L = L
     return L
 
@@ -146,3 +147,12 @@ def render_pool(cfg: Configuration, density: OracleGrid, temperature: OracleGrid
                                 fptr(cie), C.c_float(yint), num_waves, num_workers, fptr(film), C.byref(cnt))
     assert ms >= 0
     return film, ms, cnt.as_dict()
+
+
+def film_to_image(film: np.ndarray) -> np.ndarray:
+    """film_to_image (main.cpp:12-24) restated: float [H][W][4] -> uint8 [H][W][3]."""
+    film = np.ascontiguousarray(film, np.float32)
+    h, w = film.shape[:2]
+    out = np.zeros((h, w, 3), np.uint8)
+    lib().vpto_film_to_image(fptr(film), w, h, out.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return out

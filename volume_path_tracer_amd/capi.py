@@ -216,6 +216,7 @@ def lib() -> C.CDLL:
     L.vpt_synth_grid.argtypes = [C.c_int, C.c_int]
     L.vpt_synth_grid.restype = gridp
     L.vpt_synth_free.argtypes = [gridp]
+    L.vpt_film_to_srgb8.argtypes = [fp, C.c_int64, C.c_int64, C.POINTER(C.c_uint8)]
     _lib = L
     return L
 
