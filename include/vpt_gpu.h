@@ -205,9 +205,11 @@ int vpt_gpu_counters(vpt_gpu_ctx* ctx, vpt_counters* out, int reset);
 /* Scheduling knobs (results never depend on them): a rare lane state (new job, new pixel, ray
  * setup, NEE completion, film write) runs when >= gate_min lanes of a wavefront wait for it or
  * fewer than gate_idle lanes are walking rays; a tentative collision's density evaluation waits
- * for gate_eval lanes likewise; grid_blocks overrides the persistent grid size.
- * Pass <= 0 (gate_idle < 0) to keep a value. */
-int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_blocks, int gate_eval);
+ * for gate_eval lanes likewise; grid_blocks overrides the persistent grid size; the ray walk
+ * repeats in an inner loop while >= gate_walk lanes walk (0: one step per pass).
+ * Pass <= 0 (gate_idle, gate_walk < 0) to keep a value. */
+int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_blocks, int gate_eval,
+                       int gate_walk);
 /* SIMT-utilisation profile of profiling builds (-DVPT_PROFILE): for each block of the lane state
  * machine, [wave executions, active lanes] as 2*blocks uint64 (zeros in normal builds);
  * n must be >= 2 * 14. */

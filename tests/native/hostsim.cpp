@@ -73,6 +73,7 @@ extern "C" int vpths_render_jobs(const vpt_configuration* cfg, const vpt_grid_de
   S.gate_min = 1;
   S.gate_idle = 1;
   S.gate_eval = 1;
+  S.gate_walk = 1;  // exercise the inner walk loop
   HostEnv env{jid_begin, jid_count, 0, film, records, S.tw * S.th};
   vpt::Lane ln;
   std::memset(&ln, 0, sizeof ln);

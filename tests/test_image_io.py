@@ -166,13 +166,14 @@ def test_cli_render_matches_oracle(tmp_path):
     (tmp_path / "scene.json").write_text(json.dumps(cfg_text))
     dens, temp = SynthGrid(1, 64).grid(copy=True), SynthGrid(2, 64).grid(copy=True)
     nvdb.write_nvdb(tmp_path / "vol.nvdb", {"density": dens, "temperature": temp})
-    r = subprocess.run([sys.executable, "-m", "volume_path_tracer_amd", str(tmp_path / "scene.json"),
-                        str(tmp_path / "o.png"), "--film-out", str(tmp_path / "film.npy")],
-                       cwd=ROOT, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stderr
+    from volume_path_tracer_amd.__main__ import main
+
+    # in-process: the test runner's own GPU context (one process on the card)
+    rc = main([str(tmp_path / "scene.json"), str(tmp_path / "o.png"), "--film-out", str(tmp_path / "film.npy")])
+    assert rc == 0
     cfg = read_configuration(tmp_path / "scene.json")
     od, ot = O.OracleGrid(dens, fix_majorants=True), O.OracleGrid(temp, fix_majorants=False)
-    jobs = cfg.jobs_per_wave * cfg.num_waves
+    jobs = cfg.jobs_per_wave() * cfg.num_waves
     ref_film, _, _ = O.render_jobs(cfg, od, ot, 0, jobs)
     film = np.load(tmp_path / "film.npy")
     assert np.array_equal(film, ref_film)

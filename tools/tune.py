@@ -25,8 +25,9 @@ for g in a.gates.split(","):
     parts = list(map(int, g.split(":")))
     gm, gi = parts[0], parts[1]
     ge = parts[2] if len(parts) > 2 else 1
+    gw = parts[3] if len(parts) > 3 else 0
     for b in map(int, a.blocks.split(",")):
-        it.set_tuning(gm, gi, b if b > 0 else base_blocks, ge)
+        it.set_tuning(gm, gi, b if b > 0 else base_blocks, ge, gw)
         best = 1e9
         for _ in range(a.reps):
             it.film.zero_(); torch.cuda.synchronize(); t = time.perf_counter()

@@ -210,7 +210,7 @@ def lib() -> C.CDLL:
     L.vpt_gpu_film_add_to_host.argtypes = [vp, fp]
     L.vpt_gpu_counters.argtypes = [vp, C.POINTER(Counters), C.c_int]
     L.vpt_gpu_profile.argtypes = [vp, C.POINTER(C.c_uint64), C.c_int, C.c_int]
-    L.vpt_gpu_set_tuning.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int]
+    L.vpt_gpu_set_tuning.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
     L.vpt_gpu_launch_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.vpt_last_error.restype = C.c_char_p
     L.vpt_synth_grid.argtypes = [C.c_int, C.c_int]

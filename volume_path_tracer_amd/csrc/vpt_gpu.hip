@@ -292,6 +292,7 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   ctx->scene.gate_min = 8;
   ctx->scene.gate_idle = 8;
   ctx->scene.gate_eval = 16;
+  ctx->scene.gate_walk = 4;
   *out = ctx.release();
   return VPT_OK;
 }
@@ -366,9 +367,10 @@ int vpt_gpu_counters(vpt_gpu_ctx* ctx, vpt_counters* out, int reset) {
   return VPT_OK;
 }
 
-int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_blocks, int gate_eval) {
+int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_blocks, int gate_eval, int gate_walk) {
   if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
   if (gate_eval > 0) ctx->scene.gate_eval = gate_eval;
+  if (gate_walk >= 0) ctx->scene.gate_walk = gate_walk;
   if (gate_min > 0) ctx->scene.gate_min = gate_min;
   if (gate_idle >= 0) ctx->scene.gate_idle = gate_idle;
   if (grid_blocks > 0) ctx->grid_blocks = grid_blocks;

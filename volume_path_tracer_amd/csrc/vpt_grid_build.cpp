@@ -69,6 +69,43 @@ inline int2 enc(int32_t code, float v) {
 
 float host_value_at(const HostGrid& g, int32_t i, int32_t j, int32_t k) { return value_at(g.dev, i, j, k); }
 
+namespace {
+// Sets the interior bit (see cell8_interior) of every cells8 entry whose 3x3x3 neighbourhood lies
+// in the table and holds only dim-8 cells (leaves: code >= 0; lower-node tiles: -16 / -17).
+void mark_interior(const DevGrid& G, std::vector<int2>& cells8, int threads) {
+  const int32_t nx = G.r8_n[0], ny = G.r8_n[1], nz = G.r8_n[2];
+  if (cells8.empty() || nx < 3 || ny < 3 || nz < 3) return;
+  auto at = [&](int32_t a, int32_t b, int32_t c) -> int32_t { return cells8[((size_t)a * ny + b) * nz + c].x; };
+  auto dim8 = [](int32_t x) { return x >= 0 || x == -16 || x == -17; };
+  // pass 1: per cell, are the 3 cells along z all dim 8; pass 2 over y, pass 3 over x
+  std::vector<uint8_t> d((size_t)nx * ny * nz), ez(d.size()), ey(d.size());
+  parallel_for(nx, threads, [&](int64_t b0, int64_t e0) {
+    for (int64_t a = b0; a < e0; ++a)
+      for (int32_t b = 0; b < ny; ++b)
+        for (int32_t c = 0; c < nz; ++c) d[((size_t)a * ny + b) * nz + c] = dim8(at((int32_t)a, b, c));
+  });
+  auto idx = [&](int64_t a, int32_t b, int32_t c) { return ((size_t)a * ny + b) * nz + c; };
+  parallel_for(nx, threads, [&](int64_t b0, int64_t e0) {
+    for (int64_t a = b0; a < e0; ++a)
+      for (int32_t b = 0; b < ny; ++b)
+        for (int32_t c = 1; c + 1 < nz; ++c) ez[idx(a, b, c)] = d[idx(a, b, c - 1)] & d[idx(a, b, c)] & d[idx(a, b, c + 1)];
+  });
+  parallel_for(nx, threads, [&](int64_t b0, int64_t e0) {
+    for (int64_t a = b0; a < e0; ++a)
+      for (int32_t b = 1; b + 1 < ny; ++b)
+        for (int32_t c = 0; c < nz; ++c) ey[idx(a, b, c)] = ez[idx(a, b - 1, c)] & ez[idx(a, b, c)] & ez[idx(a, b + 1, c)];
+  });
+  parallel_for(nx, threads, [&](int64_t b0, int64_t e0) {
+    for (int64_t a = b0; a < e0; ++a) {
+      if (a == 0 || a + 1 == nx) continue;
+      for (int32_t b = 0; b < ny; ++b)
+        for (int32_t c = 0; c < nz; ++c)
+          if (ey[idx(a - 1, b, c)] & ey[idx(a, b, c)] & ey[idx(a + 1, b, c)]) cells8[idx(a, b, c)].x ^= kInteriorBit;
+    }
+  });
+}
+}  // namespace
+
 int build_host_grid(const vpt_grid_desc& d, bool fix, int threads, HostGrid& out) {
   if (d.leaf_count && (!d.leaf_origin || !d.leaf_values || !d.leaf_max))
     return set_error(VPT_E_INVALID, "grid: leaf arrays missing");
@@ -275,6 +312,7 @@ int build_host_grid(const vpt_grid_desc& d, bool fix, int threads, HostGrid& out
       out.cells8[idx] = enc((int32_t)n, out.leaf_max[n]);
     }
   }
+  mark_interior(G, out.cells8, threads);
   return VPT_OK;
 }
 

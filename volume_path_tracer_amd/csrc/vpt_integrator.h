@@ -55,11 +55,20 @@ struct Cell {
   float value;
 };
 
+// cells8 entries carry one more bit: "interior" = this 8^3 cell and its 26 neighbours all have
+// HDDA dim 8 (leaf or lower-node tile) and lie inside the table.  It is stored as bit 30 differing
+// from the sign bit (codes are leaf indices < 2^30 or small negatives, where bit 30 == bit 31).
+constexpr int32_t kInteriorBit = 1 << 30;
+__host__ __device__ __forceinline__ int32_t cell8_code(int32_t x) {
+  return (x & ~kInteriorBit) | ((x >> 1) & kInteriorBit);
+}
+__host__ __device__ __forceinline__ bool cell8_interior(int32_t x) { return ((x ^ (x << 1)) & (1 << 31)) != 0; }
+
 __host__ __device__ __forceinline__ Cell cell_at(const DevGrid& g, int32_t i, int32_t j, int32_t k) {
   int32_t a = (i - g.r8_org[0]) >> 3, b = (j - g.r8_org[1]) >> 3, c = (k - g.r8_org[2]) >> 3;
   if ((uint32_t)a < (uint32_t)g.r8_n[0] && (uint32_t)b < (uint32_t)g.r8_n[1] && (uint32_t)c < (uint32_t)g.r8_n[2]) {
     int2 e = g.cells8[((uint32_t)a * (uint32_t)g.r8_n[1] + (uint32_t)b) * (uint32_t)g.r8_n[2] + (uint32_t)c];
-    return Cell{e.x, math::as_f32((uint32_t)e.y)};
+    return Cell{cell8_code(e.x), math::as_f32((uint32_t)e.y)};
   }
   a = (i - g.r128_org[0]) >> 7;
   b = (j - g.r128_org[1]) >> 7;
@@ -215,6 +224,7 @@ struct DevScene {
   // wait for it, or when fewer than gate_idle lanes are sampling (1/64 = always run).
   int32_t gate_min, gate_idle;
   int32_t gate_eval;  // the density evaluation (trilinear + event) runs for >= gate_eval waiting lanes
+  int32_t gate_walk;  // keep stepping in an inner loop while >= gate_walk lanes walk (0: one step)
   const float* bb;      // blackbody table [501][3] (row 500 = 0)
   const float* cie;     // [471][3] for T >= 49900 K
   float y_integral;
@@ -464,6 +474,29 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
     ln.s_t1 = ln.T1;
     return true;
   }
+#ifdef VPT_ABL_NOLOOK  // timing ablation only (wrong at dim changes): no lookahead
+  ln.maj = majorant_of(cell_at(g, ln.vox[0], ln.vox[1], ln.vox[2]));
+  if (ln.maj == ln.s_dmaj) return false;
+  ln.s_t1 = ln.T0;
+  return true;
+#endif
+#ifndef VPT_NO_INTERIOR
+  // Fast path: at dim 8 in an interior cell the lookahead point (within ~1 voxel of the cell)
+  // lies in a dim-8 cell, so getDim answers 8 == dim and HDDA::update is a no-op.
+  if (ln.dim == 8) {
+    const int32_t a = (ln.vox[0] - g.r8_org[0]) >> 3, b = (ln.vox[1] - g.r8_org[1]) >> 3,
+                  c = (ln.vox[2] - g.r8_org[2]) >> 3;
+    if ((uint32_t)a < (uint32_t)g.r8_n[0] && (uint32_t)b < (uint32_t)g.r8_n[1] && (uint32_t)c < (uint32_t)g.r8_n[2]) {
+      const int2 e = g.cells8[((uint32_t)a * (uint32_t)g.r8_n[1] + (uint32_t)b) * (uint32_t)g.r8_n[2] + (uint32_t)c];
+      if (cell8_interior(e.x)) {
+        ln.maj = majorant_of(Cell{cell8_code(e.x), math::as_f32((uint32_t)e.y)});
+        if (ln.maj == ln.s_dmaj) return false;
+        ln.s_t1 = ln.T0;
+        return true;
+      }
+    }
+  }
+#endif
   // new_dim = max(8, getDim(floor(ray(time + 1.0001f))))
   float tl = ln.T0 + 1.0001f;
   const int32_t lx = (int32_t)floorf(ln.e[0] + ln.d[0] * tl), ly = (int32_t)floorf(ln.e[1] + ln.d[1] * tl),
@@ -673,6 +706,10 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
 
   if (ln.state == ST_SAMPLE) {
     env.prof(PB_SAMPLE);
+    // The walk (segment fetch, HDDA step, free-flight draw) loops here while enough lanes of the
+    // wavefront are walking and too few wait on a density evaluation; the other states wait
+    // (their gating counts them next outer iteration).  Each lane's own op order is unchanged.
+    do {
     if (ln.sm == SM_NEED_SEG) {
       env.prof(PB_NEED_SEG);
       // RayMajorantIterator::next prologue (volume.cpp:40-51)
@@ -712,6 +749,8 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
         ln.sm = SM_NEED_SEG;
       }
     }
+    } while (S.gate_walk > 0 && env.count(ln.state == ST_SAMPLE && ln.sm != SM_EVAL) >= S.gate_walk &&
+             env.count(ln.state == ST_SAMPLE && ln.sm == SM_EVAL) < S.gate_eval);
   }
 
   // Tentative collisions wait until gate_eval lanes of the wavefront have one (or the walk runs

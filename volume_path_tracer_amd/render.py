@@ -154,8 +154,9 @@ class Integrator:
         capi.check(capi.lib().vpt_gpu_counters(self.h, C.byref(c), 1 if reset else 0), "vpt_gpu_counters")
         return c.as_dict()
 
-    def set_tuning(self, gate_min: int = 0, gate_idle: int = -1, grid_blocks: int = 0, gate_eval: int = 0):
-        capi.check(capi.lib().vpt_gpu_set_tuning(self.h, gate_min, gate_idle, grid_blocks, gate_eval),
+    def set_tuning(self, gate_min: int = 0, gate_idle: int = -1, grid_blocks: int = 0, gate_eval: int = 0,
+                   gate_walk: int = -1):
+        capi.check(capi.lib().vpt_gpu_set_tuning(self.h, gate_min, gate_idle, grid_blocks, gate_eval, gate_walk),
                    "vpt_gpu_set_tuning")
 
     PROFILE_BLOCKS = ["iter", "fetch", "pixel", "ray", "sample", "need_seg", "step", "draw", "trilinear",
