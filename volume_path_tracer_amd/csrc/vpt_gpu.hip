@@ -47,7 +47,8 @@ struct KernelEnv {
   float* film;
   float* records;
   int32_t tile_area;
-  unsigned long long* prof_buf;  // [PB_COUNT][2] wave executions, active lanes (VPT_PROFILE builds)
+  unsigned long long* prof_buf;  // [PB_COUNT][2] wave executions, active lanes; then [PT_COUNT] cycles
+  unsigned long long* lds_prof;  // this workgroup's section cycles (LDS, VPT_PROFILE builds)
   unsigned long long* lds_counters;  // this workgroup's event counters (LDS)
 
   // Adds w for every active lane with w != 0 (w uniform per call site) to a workgroup counter.
@@ -63,6 +64,21 @@ struct KernelEnv {
     if ((__lane_id() == (uint32_t)__builtin_ctzll(m))) {
       atomicAdd(prof_buf + 2 * id, 1ULL);
       atomicAdd(prof_buf + 2 * id + 1, (unsigned long long)__popcll(m));
+    }
+#else
+    (void)id;
+#endif
+  }
+  // Wave time since the previous tick, charged to section id (first active lane; VPT_PROFILE).
+  __device__ __forceinline__ void tick(int32_t id) {
+#if defined(VPT_PROFILE) || defined(VPT_PROFILE_TIME)
+    // the previous tick's time lives in LDS per wavefront (ticks may run under partial masks)
+    const unsigned long long t = clock64();
+    const unsigned long long m = __ballot(1);
+    if (__lane_id() == (uint32_t)__builtin_ctzll(m)) {
+      unsigned long long* last = lds_prof + PT_COUNT + threadIdx.x / 64;
+      atomicAdd(lds_prof + id, t - *last);
+      *last = t;
     }
 #else
     (void)id;
@@ -101,6 +117,13 @@ __global__ __launch_bounds__(kBlockThreads VPT_LB_ARG) void vpt_integrate_kernel
   if (threadIdx.x < kCounterCount) wg_counters[threadIdx.x] = 0;
   __syncthreads();
   env.lds_counters = wg_counters;
+#if defined(VPT_PROFILE) || defined(VPT_PROFILE_TIME)
+  __shared__ unsigned long long wg_prof[PT_COUNT + kBlockThreads / 64];
+  if (threadIdx.x < PT_COUNT) wg_prof[threadIdx.x] = 0;
+  __syncthreads();
+  if (threadIdx.x % 64 == 0) wg_prof[PT_COUNT + threadIdx.x / 64] = clock64();
+  env.lds_prof = wg_prof;
+#endif
   Lane ln;
   lane_init(ln);
   while (ln.state != ST_DONE) lane_iteration<HasTemp, Debug>(S, ln, env);
@@ -109,6 +132,9 @@ __global__ __launch_bounds__(kBlockThreads VPT_LB_ARG) void vpt_integrate_kernel
   __syncthreads();
   if (threadIdx.x < kCounterCount && wg_counters[threadIdx.x])
     atomicAdd(counters + threadIdx.x, wg_counters[threadIdx.x]);
+#if defined(VPT_PROFILE) || defined(VPT_PROFILE_TIME)
+  if (threadIdx.x < PT_COUNT) atomicAdd(env.prof_buf + 2 * PB_COUNT + threadIdx.x, wg_prof[threadIdx.x]);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -171,6 +197,8 @@ struct vpt_gpu_ctx {
 };
 
 namespace {
+
+constexpr int kProfWords = 2 * vpt::PB_COUNT + vpt::PT_COUNT;
 
 int ctx_device(vpt_gpu_ctx* ctx) {
   hipError_t e = hipSetDevice(ctx->device);
@@ -274,8 +302,8 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   VPT_HIP(hipMalloc((void**)&ctx->job_counter, sizeof(unsigned long long)));
   VPT_HIP(hipMalloc((void**)&ctx->counters, vpt::kCounterCount * sizeof(unsigned long long)));
   VPT_HIP(hipMemset(ctx->counters, 0, vpt::kCounterCount * sizeof(unsigned long long)));
-  VPT_HIP(hipMalloc((void**)&ctx->prof, 2 * vpt::PB_COUNT * sizeof(unsigned long long)));
-  VPT_HIP(hipMemset(ctx->prof, 0, 2 * vpt::PB_COUNT * sizeof(unsigned long long)));
+  VPT_HIP(hipMalloc((void**)&ctx->prof, kProfWords * sizeof(unsigned long long)));
+  VPT_HIP(hipMemset(ctx->prof, 0, kProfWords * sizeof(unsigned long long)));
   VPT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
 
   // Persistent grid: as many blocks as are resident at once.
@@ -290,8 +318,8 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   // Scheduling defaults from tools/tune.py sweeps on MI355X (C3, 32 spp): rare states run for >= 8
   // waiting lanes, density evaluations for >= 16, everything runs when < 8 lanes are walking.
   ctx->scene.gate_min = 8;
-  ctx->scene.gate_idle = 8;
-  ctx->scene.gate_eval = 16;
+  ctx->scene.gate_idle = 12;
+  ctx->scene.gate_eval = 24;
   ctx->scene.gate_walk = 4;
   *out = ctx.release();
   return VPT_OK;
@@ -382,7 +410,7 @@ int vpt_gpu_profile(vpt_gpu_ctx* ctx, uint64_t* out, int n, int reset) {
   int rc = ctx_device(ctx);
   if (rc) return rc;
   VPT_HIP(hipDeviceSynchronize());
-  std::vector<unsigned long long> v(2 * vpt::PB_COUNT);
+  std::vector<unsigned long long> v(kProfWords);
   VPT_HIP(hipMemcpy(v.data(), ctx->prof, v.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   if (n < (int)v.size()) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_profile: output too small");
   for (size_t i = 0; i < v.size(); ++i) out[i] = v[i];

@@ -329,6 +329,9 @@ enum : int32_t {
   PB_ITER = 0, PB_FETCH, PB_PIXEL, PB_RAY, PB_SAMPLE, PB_NEED_SEG, PB_STEP, PB_DRAW, PB_TRILINEAR,
   PB_EVENT, PB_SHADOW_HIT, PB_NONE, PB_NEE_DONE, PB_FINISH, PB_COUNT
 };
+// Section ids for the wave-time profile (env.tick: shader cycles since the previous tick, per
+// wavefront; gating ballots are charged to the section that follows them).
+enum : int32_t { PT_FETCH = 0, PT_PIXEL, PT_RAY, PT_WALK, PT_EVAL, PT_NEE, PT_FINISH, PT_SEG, PT_STEP, PT_DRAW, PT_COUNT };
 
 // Event counters, in vpt_counters order.  They are tallied per wavefront (env.tally) rather than
 // held per lane.  The production kernel counts the four that price algorithmic bytes;
@@ -425,10 +428,13 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
   ln.inv[1] = iy;
   ln.inv[2] = iz;
   ln.scale = rd.scale;
-  ln.maj = __builtin_nanf("");
   // HDDA(ray, max(8, getDim(floor(ray.start())))) -> init(ray, t0, t1, dim)
   float px = ex + dx * t0, py = ey + dy * t0, pz = ez + dz * t0;
-  int32_t dim = hdda_dim_of(cell_at(g, (int32_t)floorf(px), (int32_t)floorf(py), (int32_t)floorf(pz)));
+  const Cell c0 = cell_at(g, (int32_t)floorf(px), (int32_t)floorf(py), (int32_t)floorf(pz));
+  int32_t dim = hdda_dim_of(c0);
+  // update_current_majorant at the start voxel (floor(start) & ~(dim-1)): the cell of a dim-d
+  // voxel answers every query of its d^3 block alike, so c0 gives the first segment's majorant.
+  ln.maj = majorant_of(c0);
   ln.dim = dim;
   ln.T0 = t0;
   ln.T1 = t1;
@@ -487,10 +493,14 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
     const int32_t a = (ln.vox[0] - g.r8_org[0]) >> 3, b = (ln.vox[1] - g.r8_org[1]) >> 3,
                   c = (ln.vox[2] - g.r8_org[2]) >> 3;
     if ((uint32_t)a < (uint32_t)g.r8_n[0] && (uint32_t)b < (uint32_t)g.r8_n[1] && (uint32_t)c < (uint32_t)g.r8_n[2]) {
-      const int2 e = g.cells8[((uint32_t)a * (uint32_t)g.r8_n[1] + (uint32_t)b) * (uint32_t)g.r8_n[2] + (uint32_t)c];
-      if (cell8_interior(e.x)) {
-        ln.maj = majorant_of(Cell{cell8_code(e.x), math::as_f32((uint32_t)e.y)});
-        if (ln.maj == ln.s_dmaj) return false;
+      // one 8-byte load (code + value together)
+      const uint64_t raw = reinterpret_cast<const uint64_t*>(
+          g.cells8)[((uint32_t)a * (uint32_t)g.r8_n[1] + (uint32_t)b) * (uint32_t)g.r8_n[2] + (uint32_t)c];
+      const int32_t x = (int32_t)(uint32_t)raw;
+      const float m = majorant_of(Cell{cell8_code(x), math::as_f32((uint32_t)(raw >> 32))});
+      if (cell8_interior(x)) {
+        ln.maj = m;
+        if (m == ln.s_dmaj) return false;
         ln.s_t1 = ln.T0;
         return true;
       }
@@ -606,7 +616,56 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     const int32_t n = env.count(ln.state == st);
     return n > 0 && (starving || n >= S.gate_min) && ln.state == st;
   };
+  auto go2 = [&](int32_t st_a, int32_t st_b) -> bool {
+    const bool mine = ln.state == st_a || ln.state == st_b;
+    const int32_t n = env.count(mine);
+    return n > 0 && (starving || n >= S.gate_min) && mine;
+  };
+  // Block order follows the state flow so a lane moves on within one pass where it can:
+  // NEE completion / film write -> next job / pixel -> ray setup -> walk -> density evaluation.
 
+  if (go(ST_NEE_DONE)) {
+    env.prof(PB_NEE_DONE);
+    if (ln.Tr >= 0.0f) {
+      // p * T_ray * Li with p = HG(w . wi)
+      float c = ln.rd[0] * S.wi[0] + (ln.rd[1] * S.wi[1] + ln.rd[2] * S.wi[2]);
+      float p = hg_eval(S, c);
+      float pt = p * ln.Tr;
+      ln.L[0] = ln.L[0] + pt * S.Li[0];
+      ln.L[1] = ln.L[1] + pt * S.Li[1];
+      ln.L[2] = ln.L[2] + pt * S.Li[2];
+    } else {
+      ln.L[0] = ln.L[0] + 0.0f;
+      ln.L[1] = ln.L[1] + 0.0f;
+      ln.L[2] = ln.L[2] + 0.0f;
+    }
+    float u0 = rng_uniform(ln.rng);
+    float u1 = rng_uniform(ln.rng);
+    if (Debug) env.tally(CNT_RNG_DRAWS, 2);
+    float nd[3];
+    sample_hg(S, ln.rd, u0, u1, nd);
+    for (int i = 0; i < 3; ++i) ln.rd[i] = nd[i];
+    ++ln.depth;  // the for-loop increment (worker.cpp:130)
+    ln.shadow = 0;
+    ln.state = ST_RAY;
+  }
+
+  env.tick(PT_NEE);
+  if (go(ST_FINISH)) {
+    env.prof(PB_FINISH);
+    if (!ln.terminated) {
+      ln.L[0] = ln.L[0] + S.le_inf[0];
+      ln.L[1] = ln.L[1] + S.le_inf[1];
+      ln.L[2] = ln.L[2] + S.le_inf[2];
+    }
+    // the pixel just traced is pix - 1 of the tile
+    const int32_t rw = min(S.W - ln.x0, S.tw);
+    const int32_t q = ln.pix - 1, y = q / rw;
+    env.film_add(S, ln, ln.x0 + (q - y * rw), ln.y0 + y, rw);
+    env.tally(CNT_SAMPLES, 1);
+    ln.state = ST_PIXEL;
+  }
+  env.tick(PT_FINISH);
   if (go(ST_FETCH)) {
     env.prof(PB_FETCH);
     uint64_t j;
@@ -628,12 +687,12 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     ln.state = ST_PIXEL;
   }
 
-  // Clipped tile extent (tile_provider.cpp:102): recomputed, not stored.
-  const int32_t rw = min(S.W - ln.x0, S.tw);
-  const int32_t rh = min(S.H - ln.y0, S.th);
-
+  env.tick(PT_FETCH);
   if (go(ST_PIXEL)) {
     env.prof(PB_PIXEL);
+    // Clipped tile extent (tile_provider.cpp:102): recomputed, not stored.
+    const int32_t rw = min(S.W - ln.x0, S.tw);
+    const int32_t rh = min(S.H - ln.y0, S.th);
     // Skip pixels filtered by single_pixel mode without any draw (worker.cpp:113-116).
     int32_t px, py;
     while (true) {
@@ -674,36 +733,37 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     ln.state = ST_RAY;
   }
 
-  if (go(ST_RAY)) {
+  env.tick(PT_PIXEL);
+  // Volume::intersect + iterator setup for primary rays (top of the depth loop, worker.cpp:122-126)
+  // and sample_Ld's shadow rays (worker.cpp:64-65, direction wi: scene constants) in one block.
+  if (go2(ST_RAY, ST_SHADOW)) {
     env.prof(PB_RAY);
-    // for (depth < max_depth) { intersection = vol.intersect(r); if (!intersection) break; ... }
-    if (!(ln.depth < S.max_depth)) {
-      ln.state = ST_FINISH;
-    } else if (begin_ray(G, ln, ln.ro, ray_dir_setup(G, ln.rd))) {
-      ln.state = ST_SAMPLE;
+    const bool primary = ln.state == ST_RAY;
+    if (primary && !(ln.depth < S.max_depth)) {
+      ln.state = ST_FINISH;  // for (depth < max_depth) exhausted
     } else {
-      ln.state = ST_FINISH;
+      RayDir rd;
+      if (primary) {
+        rd = ray_dir_setup(G, ln.rd);
+      } else {
+        for (int i = 0; i < 3; ++i) {
+          rd.d[i] = S.sh_d[i];
+          rd.inv[i] = S.sh_inv[i];
+        }
+        rd.len = S.sh_len;
+        rd.scale = S.sh_scale;
+      }
+      if (begin_ray(G, ln, ln.ro, rd)) {
+        if (Debug && !primary) env.tally(CNT_SHADOW_RAYS, 1);
+        ln.state = ST_SAMPLE;
+      } else {
+        // a primary miss ends the path; a shadow miss keeps T_ray = 1
+        ln.state = primary ? ST_FINISH : ST_NEE_DONE;
+      }
     }
   }
 
-  if (go(ST_SHADOW)) {
-    env.prof(PB_RAY);
-    // sample_Ld: vol.intersect(Ray(pos, wi)) (worker.cpp:64-65); a miss keeps T_ray = 1.
-    RayDir rd;
-    for (int i = 0; i < 3; ++i) {
-      rd.d[i] = S.sh_d[i];
-      rd.inv[i] = S.sh_inv[i];
-    }
-    rd.len = S.sh_len;
-    rd.scale = S.sh_scale;
-    if (begin_ray(G, ln, ln.ro, rd)) {
-      if (Debug) env.tally(CNT_SHADOW_RAYS, 1);
-      ln.state = ST_SAMPLE;
-    } else {
-      ln.state = ST_NEE_DONE;
-    }
-  }
-
+  env.tick(PT_RAY);
   if (ln.state == ST_SAMPLE) {
     env.prof(PB_SAMPLE);
     // The walk (segment fetch, HDDA step, free-flight draw) loops here while enough lanes of the
@@ -719,10 +779,10 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
         env.prof(PB_NONE);
       } else {
         ln.s_t0 = ln.T0;
-        if (ln.maj != ln.maj) ln.maj = majorant_of(cell_at(G, ln.vox[0], ln.vox[1], ln.vox[2]));
         ln.sm = SM_STEP;
       }
     }
+    env.tick(PT_SEG);
     if (ln.state == ST_SAMPLE && ln.sm == SM_STEP) {
       env.prof(PB_STEP);
       ++ln.n_dda;
@@ -731,6 +791,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
         ln.sm = (ln.s_dmaj <= 0.0f) ? SM_NEED_SEG : SM_DRAW;  // empty segment: no draw (:32-35)
       }
     }
+    env.tick(PT_STEP);
     if (ln.state == ST_SAMPLE && ln.sm == SM_DRAW) {
       env.prof(PB_DRAW);
       // MajorantTransmittanceSampler::next body (majorant_transmittance_sampler.cpp:39-79)
@@ -740,8 +801,16 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
         env.tally(CNT_DRAWS, 1);
         env.tally(CNT_RNG_DRAWS, 1);
       }
+#if defined(VPT_ABL_CHEAPLOG)  // timing ablations only (not bit-exact)
+      float dt_m = -__logf(1 - u) / sigma_maj;
+      float t = ln.s_t0 + dt_m / ln.scale;
+#elif defined(VPT_ABL_FASTDIV)
+      float dt_m = __fdividef(-math::logf_glibc_unit(1 - u), sigma_maj);
+      float t = ln.s_t0 + __fdividef(dt_m, ln.scale);
+#else
       float dt_m = -math::logf_glibc_unit(1 - u) / sigma_maj;
       float t = ln.s_t0 + dt_m / ln.scale;
+#endif
       if (t < ln.s_t1) {
         ln.s_t0 = t;       // the tentative collision; its density is evaluated in SM_EVAL
         ln.sm = SM_EVAL;
@@ -749,10 +818,12 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
         ln.sm = SM_NEED_SEG;
       }
     }
+    env.tick(PT_DRAW);
     } while (S.gate_walk > 0 && env.count(ln.state == ST_SAMPLE && ln.sm != SM_EVAL) >= S.gate_walk &&
              env.count(ln.state == ST_SAMPLE && ln.sm == SM_EVAL) < S.gate_eval);
   }
 
+  env.tick(PT_WALK);
   // Tentative collisions wait until gate_eval lanes of the wavefront have one (or the walk runs
   // short of lanes), so the stencil gathers and the event logic run on a fuller wavefront.
   const int32_t n_eval = env.count(ln.state == ST_SAMPLE && ln.sm == SM_EVAL);
@@ -843,45 +914,7 @@ __host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane&
     }
   }
 
-  if (go(ST_NEE_DONE)) {
-    env.prof(PB_NEE_DONE);
-    if (ln.Tr >= 0.0f) {
-      // p * T_ray * Li with p = HG(w . wi)
-      float c = ln.rd[0] * S.wi[0] + (ln.rd[1] * S.wi[1] + ln.rd[2] * S.wi[2]);
-      float p = hg_eval(S, c);
-      float pt = p * ln.Tr;
-      ln.L[0] = ln.L[0] + pt * S.Li[0];
-      ln.L[1] = ln.L[1] + pt * S.Li[1];
-      ln.L[2] = ln.L[2] + pt * S.Li[2];
-    } else {
-      ln.L[0] = ln.L[0] + 0.0f;
-      ln.L[1] = ln.L[1] + 0.0f;
-      ln.L[2] = ln.L[2] + 0.0f;
-    }
-    float u0 = rng_uniform(ln.rng);
-    float u1 = rng_uniform(ln.rng);
-    if (Debug) env.tally(CNT_RNG_DRAWS, 2);
-    float nd[3];
-    sample_hg(S, ln.rd, u0, u1, nd);
-    for (int i = 0; i < 3; ++i) ln.rd[i] = nd[i];
-    ++ln.depth;  // the for-loop increment (worker.cpp:130)
-    ln.shadow = 0;
-    ln.state = ST_RAY;
-  }
-
-  if (go(ST_FINISH)) {
-    env.prof(PB_FINISH);
-    if (!ln.terminated) {
-      ln.L[0] = ln.L[0] + S.le_inf[0];
-      ln.L[1] = ln.L[1] + S.le_inf[1];
-      ln.L[2] = ln.L[2] + S.le_inf[2];
-    }
-    // the pixel just traced is pix - 1 of the tile
-    const int32_t q = ln.pix - 1, y = q / rw;
-    env.film_add(S, ln, ln.x0 + (q - y * rw), ln.y0 + y, rw);
-    env.tally(CNT_SAMPLES, 1);
-    ln.state = ST_PIXEL;
-  }
+  env.tick(PT_EVAL);
 }
 
 __host__ __device__ __forceinline__ void lane_init(Lane& ln) {

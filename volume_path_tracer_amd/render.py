@@ -162,14 +162,22 @@ class Integrator:
     PROFILE_BLOCKS = ["iter", "fetch", "pixel", "ray", "sample", "need_seg", "step", "draw", "trilinear",
                       "event", "shadow_hit", "none", "nee_done", "finish"]
 
+    PROFILE_SECTIONS = ["fetch", "pixel", "ray", "walk", "eval", "nee", "finish", "seg", "step", "draw"]
+
     def profile(self, reset: bool = False) -> dict:
-        """SIMT profile of a -DVPT_PROFILE build: {block: (wave executions, mean active lanes)}."""
+        """SIMT profile of a -DVPT_PROFILE build: {block: (wave executions, mean active lanes)} and
+        {"cycles": {section: share of wave time}}."""
         buf = (C.c_uint64 * 64)()
         capi.check(capi.lib().vpt_gpu_profile(self.h, buf, 64, 1 if reset else 0), "vpt_gpu_profile")
         out = {}
         for i, name in enumerate(self.PROFILE_BLOCKS):
             ex, lanes = int(buf[2 * i]), int(buf[2 * i + 1])
             out[name] = (ex, round(lanes / ex, 2) if ex else 0.0)
+        base = 2 * len(self.PROFILE_BLOCKS)
+        cyc = [int(buf[base + i]) for i in range(len(self.PROFILE_SECTIONS))]
+        tot = sum(cyc) or 1
+        out["cycles"] = {n: round(c / tot, 4) for n, c in zip(self.PROFILE_SECTIONS, cyc)}
+        out["cycles_total"] = tot
         return out
 
     def launch_info(self):
