@@ -80,9 +80,9 @@ extern "C" int vpths_render_jobs(const vpt_configuration* cfg, const vpt_grid_de
   std::memset(&ln, 0, sizeof ln);
   vpt::lane_init(ln);
   if (temperature)
-    while (ln.state != vpt::ST_DONE) vpt::lane_iteration<true, true>(S, ln, env);
+    while (ln.state != vpt::ST_DONE) vpt::lane_iteration<true, true>(&S, ln, env);
   else
-    while (ln.state != vpt::ST_DONE) vpt::lane_iteration<false, true>(S, ln, env);
+    while (ln.state != vpt::ST_DONE) vpt::lane_iteration<false, true>(&S, ln, env);
   env.cnt[vpt::CNT_DDA_STEPS] += ln.n_dda;
   env.cnt[vpt::CNT_STENCILS] += ln.n_stencil;
   if (counters) {

@@ -9,7 +9,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 python3 - <<'PY'
 import re
 t = open("/tmp/isa/vpt.s").read()
-for m in re.finditer(r"^(_ZN3vpt20vpt_integrate_kernelI(\w+?)EEvNS_8DevScene\w*):", t, re.M):
+for m in re.finditer(r"^(_ZN3vpt20vpt_integrate_kernelI(\w+?)EEv\w*DevScene\w*):", t, re.M):
     seg = t[m.end():]
     get = lambda k: re.search(r"; %s: (\d+)" % k, seg).group(1)
     print(m.group(2), "vgpr", get("NumVgprs"), "sgpr", get("NumSGPRsForWavesPerEU"), "scratch", get("ScratchSize"), "occ", get("Occupancy"))

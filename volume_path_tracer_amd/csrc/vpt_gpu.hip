@@ -34,10 +34,13 @@ int set_error(int code, const std::string& msg) {
 
 constexpr int kCounterCount = CNT_COUNT;
 constexpr int kBlockThreads = 256;
-#ifdef VPT_LB
-#define VPT_LB_ARG , VPT_LB
-#else
-#define VPT_LB_ARG
+// Minimum waves per SIMD (launch bounds): 5 for the production density-only kernel (97 -> 96
+// VGPRs, no spills); 4 for the temperature and per-sample-record variants, which would spill.
+#ifndef VPT_WAVES_FAST
+#define VPT_WAVES_FAST 5
+#endif
+#ifndef VPT_WAVES_SLOW
+#define VPT_WAVES_SLOW 4
 #endif
 
 struct KernelEnv {
@@ -111,7 +114,7 @@ struct KernelEnv {
 
 // counters[] order = vpt_counters field order
 template <bool HasTemp, bool Debug>
-__global__ __launch_bounds__(kBlockThreads VPT_LB_ARG) void vpt_integrate_kernel(DevScene S, KernelEnv env,
+__global__ __launch_bounds__(kBlockThreads, (HasTemp || Debug) ? VPT_WAVES_SLOW : VPT_WAVES_FAST) void vpt_integrate_kernel(const DevScene* scene, KernelEnv env,
                                                                        unsigned long long* counters) {
   __shared__ unsigned long long wg_counters[kCounterCount];
   if (threadIdx.x < kCounterCount) wg_counters[threadIdx.x] = 0;
@@ -126,7 +129,8 @@ __global__ __launch_bounds__(kBlockThreads VPT_LB_ARG) void vpt_integrate_kernel
 #endif
   Lane ln;
   lane_init(ln);
-  while (ln.state != ST_DONE) lane_iteration<HasTemp, Debug>(S, ln, env);
+  const ScenePtr sp = (ScenePtr)scene;
+  while (ln.state != ST_DONE) lane_iteration<HasTemp, Debug>(sp, ln, env);
   atomicAdd(wg_counters + CNT_DDA_STEPS, (unsigned long long)ln.n_dda);
   atomicAdd(wg_counters + CNT_STENCILS, (unsigned long long)ln.n_stencil);
   __syncthreads();
@@ -192,6 +196,7 @@ struct vpt_gpu_ctx {
   unsigned long long* job_counter = nullptr;
   unsigned long long* counters = nullptr;
   unsigned long long* prof = nullptr;
+  vpt::DevScene* scene_dev = nullptr;  // the kernel's copy of scene (read through ScenePtr)
   hipStream_t stream = nullptr;
   int grid_blocks = 0;
 };
@@ -199,6 +204,14 @@ struct vpt_gpu_ctx {
 namespace {
 
 constexpr int kProfWords = 2 * vpt::PB_COUNT + vpt::PT_COUNT;
+
+int ctx_device(vpt_gpu_ctx* ctx);
+
+// Device copy of the scene constants (between renders: a running kernel reads it).
+int push_scene(vpt_gpu_ctx* ctx) {
+  VPT_HIP(hipMemcpy(ctx->scene_dev, &ctx->scene, sizeof(vpt::DevScene), hipMemcpyHostToDevice));
+  return VPT_OK;
+}
 
 int ctx_device(vpt_gpu_ctx* ctx) {
   hipError_t e = hipSetDevice(ctx->device);
@@ -217,6 +230,7 @@ void destroy(vpt_gpu_ctx* ctx) {
   (void)hipFree(ctx->job_counter);
   (void)hipFree(ctx->counters);
   (void)hipFree(ctx->prof);
+  (void)hipFree(ctx->scene_dev);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -241,7 +255,7 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   const bool temp = ctx->scene.has_temperature != 0, dbg = records != nullptr;
   auto kernel = temp ? (dbg ? vpt::vpt_integrate_kernel<true, true> : vpt::vpt_integrate_kernel<true, false>)
                      : (dbg ? vpt::vpt_integrate_kernel<false, true> : vpt::vpt_integrate_kernel<false, false>);
-  hipLaunchKernelGGL(kernel, dim3(ctx->grid_blocks), dim3(vpt::kBlockThreads), 0, s, ctx->scene, env, ctx->counters);
+  hipLaunchKernelGGL(kernel, dim3(ctx->grid_blocks), dim3(vpt::kBlockThreads), 0, s, ctx->scene_dev, env, ctx->counters);
   VPT_HIP(hipGetLastError());
   return VPT_OK;
 }
@@ -321,6 +335,8 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   ctx->scene.gate_idle = 12;
   ctx->scene.gate_eval = 24;
   ctx->scene.gate_walk = 4;
+  VPT_HIP(hipMalloc((void**)&ctx->scene_dev, sizeof(vpt::DevScene)));
+  if ((rc = push_scene(ctx.get()))) return rc;
   *out = ctx.release();
   return VPT_OK;
 }
@@ -397,10 +413,13 @@ int vpt_gpu_counters(vpt_gpu_ctx* ctx, vpt_counters* out, int reset) {
 
 int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_blocks, int gate_eval, int gate_walk) {
   if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
   if (gate_eval > 0) ctx->scene.gate_eval = gate_eval;
   if (gate_walk >= 0) ctx->scene.gate_walk = gate_walk;
   if (gate_min > 0) ctx->scene.gate_min = gate_min;
   if (gate_idle >= 0) ctx->scene.gate_idle = gate_idle;
+  if ((rc = push_scene(ctx))) return rc;
   if (grid_blocks > 0) ctx->grid_blocks = grid_blocks;
   return VPT_OK;
 }

@@ -604,316 +604,368 @@ __host__ __device__ inline void scene_finalize(DevScene& S) {
 // film_add(S, lane, px, py, rw).  HasTemp: the scene has a temperature grid (fire).
 // Debug: keep every counter and the job index (per-sample records).
 // ------------------------------------------------------------------------------------------------
+// The scene as the kernel reads it: a pointer into the constant address space (scalar loads).
+// opaque() hides the pointer's value from the optimiser, so loads through it are not hoisted out
+// of the state-machine loop (they would pin ~100 SGPRs for the whole kernel and spill to VGPR
+// lanes); each block re-reads the few constants it uses with s_load instead.
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(4))) DevScene* ScenePtr;
+#else
+typedef const DevScene* ScenePtr;
+#endif
+__host__ __device__ __forceinline__ ScenePtr opaque(ScenePtr p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+s"(p));
+#endif
+  return p;
+}
+
 template <bool HasTemp, bool Debug, class Env>
-__host__ __device__ __forceinline__ void lane_iteration(const DevScene& S, Lane& ln, Env& env) {
-  const DevGrid& G = S.density;
+__host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, Env& env) {
   env.prof(PB_ITER);
-  // Lanes of the wavefront sampling right now; rare states run when enough lanes wait for them
-  // or the wavefront is short of sampling work (never changes a lane's own operation order).
-  const int32_t n_walking = env.count(ln.state == ST_SAMPLE && ln.sm != SM_EVAL);
-  const bool starving = n_walking < S.gate_idle;
+  // Every block reads the scene constants it needs afresh (scalar loads behind opaque(), see
+  // ScenePtr): nothing stays live in SGPRs across the whole loop, so the walk keeps its own.
+  int32_t gate_min;
+  bool starving;
+  {
+    const DevScene S = *opaque(sp);
+    gate_min = S.gate_min;
+    // Lanes of the wavefront sampling right now; rare states run when enough lanes wait for them
+    // or the wavefront is short of sampling work (never changes a lane's own operation order).
+    const int32_t n_walking = env.count(ln.state == ST_SAMPLE && ln.sm != SM_EVAL);
+    starving = n_walking < S.gate_idle;
+  }
   auto go = [&](int32_t st) -> bool {
     const int32_t n = env.count(ln.state == st);
-    return n > 0 && (starving || n >= S.gate_min) && ln.state == st;
+    return n > 0 && (starving || n >= gate_min) && ln.state == st;
   };
   auto go2 = [&](int32_t st_a, int32_t st_b) -> bool {
     const bool mine = ln.state == st_a || ln.state == st_b;
     const int32_t n = env.count(mine);
-    return n > 0 && (starving || n >= S.gate_min) && mine;
+    return n > 0 && (starving || n >= gate_min) && mine;
   };
   // Block order follows the state flow so a lane moves on within one pass where it can:
   // NEE completion / film write -> next job / pixel -> ray setup -> walk -> density evaluation.
 
-  if (go(ST_NEE_DONE)) {
-    env.prof(PB_NEE_DONE);
-    if (ln.Tr >= 0.0f) {
-      // p * T_ray * Li with p = HG(w . wi)
-      float c = ln.rd[0] * S.wi[0] + (ln.rd[1] * S.wi[1] + ln.rd[2] * S.wi[2]);
-      float p = hg_eval(S, c);
-      float pt = p * ln.Tr;
-      ln.L[0] = ln.L[0] + pt * S.Li[0];
-      ln.L[1] = ln.L[1] + pt * S.Li[1];
-      ln.L[2] = ln.L[2] + pt * S.Li[2];
-    } else {
-      ln.L[0] = ln.L[0] + 0.0f;
-      ln.L[1] = ln.L[1] + 0.0f;
-      ln.L[2] = ln.L[2] + 0.0f;
+  {
+    const DevScene S = *opaque(sp);
+    const DevGrid& G = S.density;
+    (void)G;
+    if (go(ST_NEE_DONE)) {
+      env.prof(PB_NEE_DONE);
+      if (ln.Tr >= 0.0f) {
+        // p * T_ray * Li with p = HG(w . wi)
+        float c = ln.rd[0] * S.wi[0] + (ln.rd[1] * S.wi[1] + ln.rd[2] * S.wi[2]);
+        float p = hg_eval(S, c);
+        float pt = p * ln.Tr;
+        ln.L[0] = ln.L[0] + pt * S.Li[0];
+        ln.L[1] = ln.L[1] + pt * S.Li[1];
+        ln.L[2] = ln.L[2] + pt * S.Li[2];
+      } else {
+        ln.L[0] = ln.L[0] + 0.0f;
+        ln.L[1] = ln.L[1] + 0.0f;
+        ln.L[2] = ln.L[2] + 0.0f;
+      }
+      float u0 = rng_uniform(ln.rng);
+      float u1 = rng_uniform(ln.rng);
+      if (Debug) env.tally(CNT_RNG_DRAWS, 2);
+      float nd[3];
+      sample_hg(S, ln.rd, u0, u1, nd);
+      for (int i = 0; i < 3; ++i) ln.rd[i] = nd[i];
+      ++ln.depth;  // the for-loop increment (worker.cpp:130)
+      ln.shadow = 0;
+      ln.state = ST_RAY;
     }
-    float u0 = rng_uniform(ln.rng);
-    float u1 = rng_uniform(ln.rng);
-    if (Debug) env.tally(CNT_RNG_DRAWS, 2);
-    float nd[3];
-    sample_hg(S, ln.rd, u0, u1, nd);
-    for (int i = 0; i < 3; ++i) ln.rd[i] = nd[i];
-    ++ln.depth;  // the for-loop increment (worker.cpp:130)
-    ln.shadow = 0;
-    ln.state = ST_RAY;
   }
-
   env.tick(PT_NEE);
-  if (go(ST_FINISH)) {
-    env.prof(PB_FINISH);
-    if (!ln.terminated) {
-      ln.L[0] = ln.L[0] + S.le_inf[0];
-      ln.L[1] = ln.L[1] + S.le_inf[1];
-      ln.L[2] = ln.L[2] + S.le_inf[2];
+  {
+    const DevScene S = *opaque(sp);
+    const DevGrid& G = S.density;
+    (void)G;
+    if (go(ST_FINISH)) {
+      env.prof(PB_FINISH);
+      if (!ln.terminated) {
+        ln.L[0] = ln.L[0] + S.le_inf[0];
+        ln.L[1] = ln.L[1] + S.le_inf[1];
+        ln.L[2] = ln.L[2] + S.le_inf[2];
+      }
+      // the pixel just traced is pix - 1 of the tile
+      const int32_t rw = min(S.W - ln.x0, S.tw);
+      const int32_t q = ln.pix - 1, y = q / rw;
+      env.film_add(S, ln, ln.x0 + (q - y * rw), ln.y0 + y, rw);
+      env.tally(CNT_SAMPLES, 1);
+      ln.state = ST_PIXEL;
     }
-    // the pixel just traced is pix - 1 of the tile
-    const int32_t rw = min(S.W - ln.x0, S.tw);
-    const int32_t q = ln.pix - 1, y = q / rw;
-    env.film_add(S, ln, ln.x0 + (q - y * rw), ln.y0 + y, rw);
-    env.tally(CNT_SAMPLES, 1);
-    ln.state = ST_PIXEL;
   }
   env.tick(PT_FINISH);
-  if (go(ST_FETCH)) {
-    env.prof(PB_FETCH);
-    uint64_t j;
-    if (!env.fetch_job(j)) {
-      ln.state = ST_DONE;
-      return;
-    }
-    if (Debug) ln.jid_local = j;
-    uint64_t jid = env.jid_begin + j;
-    ln.rng = job_seed(S.seed, jid);
-    uint64_t tile = jid % S.T;
-    ln.x0 = (int32_t)(tile % S.ntx) * S.tw;  // TileProvider::compute_tile_rect
-    ln.y0 = (int32_t)(tile / S.ntx) * S.th;
-    ln.pix = 0;
-    if (HasTemp) {
-      ln.temp_cell.i = kNoCell;
-      ln.temp_cell.code = -1;
-    }
-    ln.state = ST_PIXEL;
-  }
-
-  env.tick(PT_FETCH);
-  if (go(ST_PIXEL)) {
-    env.prof(PB_PIXEL);
-    // Clipped tile extent (tile_provider.cpp:102): recomputed, not stored.
-    const int32_t rw = min(S.W - ln.x0, S.tw);
-    const int32_t rh = min(S.H - ln.y0, S.th);
-    // Skip pixels filtered by single_pixel mode without any draw (worker.cpp:113-116).
-    int32_t px, py;
-    while (true) {
-      if (ln.pix >= rw * rh) {
-        ln.state = ST_FETCH;
+  {
+    const DevScene S = *opaque(sp);
+    const DevGrid& G = S.density;
+    (void)G;
+    if (go(ST_FETCH)) {
+      env.prof(PB_FETCH);
+      uint64_t j;
+      if (!env.fetch_job(j)) {
+        ln.state = ST_DONE;
         return;
       }
-      int32_t y = ln.pix / rw;
-      px = ln.x0 + (ln.pix - y * rw);
-      py = ln.y0 + y;
-      ++ln.pix;
-      if (!S.single_pixel_enabled || (px == S.sp_x && py == S.sp_y)) break;
+      if (Debug) ln.jid_local = j;
+      uint64_t jid = env.jid_begin + j;
+      ln.rng = job_seed(S.seed, jid);
+      uint64_t tile = jid % S.T;
+      ln.x0 = (int32_t)(tile % S.ntx) * S.tw;  // TileProvider::compute_tile_rect
+      ln.y0 = (int32_t)(tile / S.ntx) * S.th;
+      ln.pix = 0;
+      if (HasTemp) {
+        ln.temp_cell.i = kNoCell;
+        ln.temp_cell.code = -1;
+      }
+      ln.state = ST_PIXEL;
     }
-    float jx = rng_uniform(ln.rng);
-    float jy = rng_uniform(ln.rng);
-    if (Debug) env.tally(CNT_RNG_DRAWS, 2);
-    jx *= S.jitter_scale;
-    jy *= S.jitter_scale;
-    // Camera::generate_ray (camera.hpp:14-23)
-    float rx = ((float)px + 0.5f) + jx, ry = ((float)py + 0.5f) + jy;
-    float dv[3];
-    for (int i = 0; i < 3; ++i) dv[i] = S.cam_t[i] + (S.cam_L[i * 3] * rx + (S.cam_L[i * 3 + 1] * ry + S.cam_L[i * 3 + 2] * 0.0f));
-    float n2 = dv[0] * dv[0] + (dv[1] * dv[1] + dv[2] * dv[2]);
-    if (n2 > 0.0f) {
-      float s = sqrtf(n2);
-      dv[0] = dv[0] / s;
-      dv[1] = dv[1] / s;
-      dv[2] = dv[2] / s;
-    }
-    for (int i = 0; i < 3; ++i) {
-      ln.ro[i] = S.cam_pos[i];
-      ln.rd[i] = dv[i];
-      ln.L[i] = 0.0f;
-    }
-    ln.terminated = 0;
-    ln.depth = 0;
-    ln.shadow = 0;
-    ln.state = ST_RAY;
   }
-
+  env.tick(PT_FETCH);
+  {
+    const DevScene S = *opaque(sp);
+    const DevGrid& G = S.density;
+    (void)G;
+    if (go(ST_PIXEL)) {
+      env.prof(PB_PIXEL);
+      // Clipped tile extent (tile_provider.cpp:102): recomputed, not stored.
+      const int32_t rw = min(S.W - ln.x0, S.tw);
+      const int32_t rh = min(S.H - ln.y0, S.th);
+      // Skip pixels filtered by single_pixel mode without any draw (worker.cpp:113-116).
+      int32_t px, py;
+      while (true) {
+        if (ln.pix >= rw * rh) {
+          ln.state = ST_FETCH;
+          return;
+        }
+        int32_t y = ln.pix / rw;
+        px = ln.x0 + (ln.pix - y * rw);
+        py = ln.y0 + y;
+        ++ln.pix;
+        if (!S.single_pixel_enabled || (px == S.sp_x && py == S.sp_y)) break;
+      }
+      float jx = rng_uniform(ln.rng);
+      float jy = rng_uniform(ln.rng);
+      if (Debug) env.tally(CNT_RNG_DRAWS, 2);
+      jx *= S.jitter_scale;
+      jy *= S.jitter_scale;
+      // Camera::generate_ray (camera.hpp:14-23)
+      float rx = ((float)px + 0.5f) + jx, ry = ((float)py + 0.5f) + jy;
+      float dv[3];
+      for (int i = 0; i < 3; ++i) dv[i] = S.cam_t[i] + (S.cam_L[i * 3] * rx + (S.cam_L[i * 3 + 1] * ry + S.cam_L[i * 3 + 2] * 0.0f));
+      float n2 = dv[0] * dv[0] + (dv[1] * dv[1] + dv[2] * dv[2]);
+      if (n2 > 0.0f) {
+        float s = sqrtf(n2);
+        dv[0] = dv[0] / s;
+        dv[1] = dv[1] / s;
+        dv[2] = dv[2] / s;
+      }
+      for (int i = 0; i < 3; ++i) {
+        ln.ro[i] = S.cam_pos[i];
+        ln.rd[i] = dv[i];
+        ln.L[i] = 0.0f;
+      }
+      ln.terminated = 0;
+      ln.depth = 0;
+      ln.shadow = 0;
+      ln.state = ST_RAY;
+    }
+  }
   env.tick(PT_PIXEL);
-  // Volume::intersect + iterator setup for primary rays (top of the depth loop, worker.cpp:122-126)
-  // and sample_Ld's shadow rays (worker.cpp:64-65, direction wi: scene constants) in one block.
-  if (go2(ST_RAY, ST_SHADOW)) {
-    env.prof(PB_RAY);
-    const bool primary = ln.state == ST_RAY;
-    if (primary && !(ln.depth < S.max_depth)) {
-      ln.state = ST_FINISH;  // for (depth < max_depth) exhausted
-    } else {
-      RayDir rd;
-      if (primary) {
-        rd = ray_dir_setup(G, ln.rd);
+  {
+    const DevScene S = *opaque(sp);
+    const DevGrid& G = S.density;
+    (void)G;
+    // Volume::intersect + iterator setup for primary rays (top of the depth loop, worker.cpp:122-126)
+    // and sample_Ld's shadow rays (worker.cpp:64-65, direction wi: scene constants) in one block.
+    if (go2(ST_RAY, ST_SHADOW)) {
+      env.prof(PB_RAY);
+      const bool primary = ln.state == ST_RAY;
+      if (primary && !(ln.depth < S.max_depth)) {
+        ln.state = ST_FINISH;  // for (depth < max_depth) exhausted
       } else {
-        for (int i = 0; i < 3; ++i) {
-          rd.d[i] = S.sh_d[i];
-          rd.inv[i] = S.sh_inv[i];
-        }
-        rd.len = S.sh_len;
-        rd.scale = S.sh_scale;
-      }
-      if (begin_ray(G, ln, ln.ro, rd)) {
-        if (Debug && !primary) env.tally(CNT_SHADOW_RAYS, 1);
-        ln.state = ST_SAMPLE;
-      } else {
-        // a primary miss ends the path; a shadow miss keeps T_ray = 1
-        ln.state = primary ? ST_FINISH : ST_NEE_DONE;
-      }
-    }
-  }
-
-  env.tick(PT_RAY);
-  if (ln.state == ST_SAMPLE) {
-    env.prof(PB_SAMPLE);
-    // The walk (segment fetch, HDDA step, free-flight draw) loops here while enough lanes of the
-    // wavefront are walking and too few wait on a density evaluation; the other states wait
-    // (their gating counts them next outer iteration).  Each lane's own op order is unchanged.
-    do {
-    if (ln.sm == SM_NEED_SEG) {
-      env.prof(PB_NEED_SEG);
-      // RayMajorantIterator::next prologue (volume.cpp:40-51)
-      if (ln.T0 >= ln.T1) {
-        // the sampler ran dry: a shadow ray keeps T_ray; a primary ray did not scatter (break)
-        ln.state = ln.shadow ? ST_NEE_DONE : ST_FINISH;
-        env.prof(PB_NONE);
-      } else {
-        ln.s_t0 = ln.T0;
-        ln.sm = SM_STEP;
-      }
-    }
-    env.tick(PT_SEG);
-    if (ln.state == ST_SAMPLE && ln.sm == SM_STEP) {
-      env.prof(PB_STEP);
-      ++ln.n_dda;
-      if (hdda_step(G, ln)) {
-        if (Debug) env.tally(CNT_SEGMENTS, 1);
-        ln.sm = (ln.s_dmaj <= 0.0f) ? SM_NEED_SEG : SM_DRAW;  // empty segment: no draw (:32-35)
-      }
-    }
-    env.tick(PT_STEP);
-    if (ln.state == ST_SAMPLE && ln.sm == SM_DRAW) {
-      env.prof(PB_DRAW);
-      // MajorantTransmittanceSampler::next body (majorant_transmittance_sampler.cpp:39-79)
-      float sigma_maj = ln.s_dmaj * S.sigma_t;
-      float u = rng_uniform(ln.rng);
-      if (Debug) {
-        env.tally(CNT_DRAWS, 1);
-        env.tally(CNT_RNG_DRAWS, 1);
-      }
-#if defined(VPT_ABL_CHEAPLOG)  // timing ablations only (not bit-exact)
-      float dt_m = -__logf(1 - u) / sigma_maj;
-      float t = ln.s_t0 + dt_m / ln.scale;
-#elif defined(VPT_ABL_FASTDIV)
-      float dt_m = __fdividef(-math::logf_glibc_unit(1 - u), sigma_maj);
-      float t = ln.s_t0 + __fdividef(dt_m, ln.scale);
-#else
-      float dt_m = -math::logf_glibc_unit(1 - u) / sigma_maj;
-      float t = ln.s_t0 + dt_m / ln.scale;
-#endif
-      if (t < ln.s_t1) {
-        ln.s_t0 = t;       // the tentative collision; its density is evaluated in SM_EVAL
-        ln.sm = SM_EVAL;
-      } else {
-        ln.sm = SM_NEED_SEG;
-      }
-    }
-    env.tick(PT_DRAW);
-    } while (S.gate_walk > 0 && env.count(ln.state == ST_SAMPLE && ln.sm != SM_EVAL) >= S.gate_walk &&
-             env.count(ln.state == ST_SAMPLE && ln.sm == SM_EVAL) < S.gate_eval);
-  }
-
-  env.tick(PT_WALK);
-  // Tentative collisions wait until gate_eval lanes of the wavefront have one (or the walk runs
-  // short of lanes), so the stencil gathers and the event logic run on a fuller wavefront.
-  const int32_t n_eval = env.count(ln.state == ST_SAMPLE && ln.sm == SM_EVAL);
-  const bool run_eval = n_eval > 0 && (n_eval >= S.gate_eval || env.count(ln.state == ST_SAMPLE && ln.sm != SM_EVAL) < S.gate_idle);
-  if (run_eval && ln.state == ST_SAMPLE && ln.sm == SM_EVAL) {
-    env.prof(PB_TRILINEAR);
-    const float t = ln.s_t0;
-    const float sigma_maj = ln.s_dmaj * S.sigma_t;
-    float pi_x = ln.e[0] + ln.d[0] * t, pi_y = ln.e[1] + ln.d[1] * t, pi_z = ln.e[2] + ln.d[2] * t;
-    float dens;
-    if (Debug) env.tally(CNT_DENSITY_EVALS, 1);
-    if (trilinear(G, ln.dens_cell, pi_x, pi_y, pi_z, dens)) ++ln.n_stencil;
-    ln.sm = SM_DRAW;  // density <= 0, a null event or an unkilled shadow ray: keep drawing
-    if (dens > 0.0f) {
-      float cp[3];
-      map_fwd(G, pi_x, pi_y, pi_z, cp[0], cp[1], cp[2]);
-      if (!ln.shadow) {
-        env.prof(PB_EVENT);
-        // worker.cpp:148-188
-        float p_a = (S.sigma_a * dens) / sigma_maj;
-        float p_s = (S.sigma_s * dens) / sigma_maj;
-        float p_n = fmaxf(1.0f - p_a - p_s, 0.0f);
-        if (HasTemp) {
-          float tx, ty, tz, tadim, X, Y, Z;
-          map_inv(S.temperature, cp[0], cp[1], cp[2], tx, ty, tz);
-          env.tally(CNT_TEMP_STENCILS, trilinear(S.temperature, ln.temp_cell, tx, ty, tz, tadim) ? 1 : 0);
-          float tK = tadim * S.temp_scale + S.temp_offset;
-          blackbody_xyz(S, tK, X, Y, Z);
-          float sc = p_a * S.le_scale;
-          ln.L[0] = ln.L[0] + sc * X;
-          ln.L[1] = ln.L[1] + sc * Y;
-          ln.L[2] = ln.L[2] + sc * Z;
-        }
-        float ue = rng_uniform(ln.rng);
-        if (Debug) env.tally(CNT_RNG_DRAWS, 1);
-        // sample_discrete({Null p_n, Absorption p_a, Scatter p_s}, u) (random.hpp:30-47)
-        float total = ((0.0f + p_n) + p_a) + p_s;
-        float uu = ue * total;
-        int ev;
-        uu -= p_n;
-        if (uu <= 0) {
-          ev = 0;
+        RayDir rd;
+        if (primary) {
+          rd = ray_dir_setup(G, ln.rd);
         } else {
-          uu -= p_a;
-          ev = (uu <= 0) ? 1 : 2;
+          for (int i = 0; i < 3; ++i) {
+            rd.d[i] = S.sh_d[i];
+            rd.inv[i] = S.sh_inv[i];
+          }
+          rd.len = S.sh_len;
+          rd.scale = S.sh_scale;
         }
-        if (ev == 1) {
-          ln.terminated = 1;
-          ln.state = ST_FINISH;
-        } else if (ev == 2) {
-          if (ln.depth++ >= S.max_depth) {
+        if (begin_ray(G, ln, ln.ro, rd)) {
+          if (Debug && !primary) env.tally(CNT_SHADOW_RAYS, 1);
+          ln.state = ST_SAMPLE;
+        } else {
+          // a primary miss ends the path; a shadow miss keeps T_ray = 1
+          ln.state = primary ? ST_FINISH : ST_NEE_DONE;
+        }
+      }
+    }
+  }
+  env.tick(PT_RAY);
+  {
+    const DevScene S = *opaque(sp);
+    const DevGrid& G = S.density;
+    (void)G;
+    if (ln.state == ST_SAMPLE) {
+      env.prof(PB_SAMPLE);
+      // The walk (segment fetch, HDDA step, free-flight draw) loops here while enough lanes of the
+      // wavefront are walking and too few wait on a density evaluation; the other states wait
+      // (their gating counts them next outer iteration).  Each lane's own op order is unchanged.
+      do {
+      if (ln.sm == SM_NEED_SEG) {
+        env.prof(PB_NEED_SEG);
+        // RayMajorantIterator::next prologue (volume.cpp:40-51)
+        if (ln.T0 >= ln.T1) {
+          // the sampler ran dry: a shadow ray keeps T_ray; a primary ray did not scatter (break)
+          ln.state = ln.shadow ? ST_NEE_DONE : ST_FINISH;
+          env.prof(PB_NONE);
+        } else {
+          ln.s_t0 = ln.T0;
+          ln.sm = SM_STEP;
+        }
+      }
+      env.tick(PT_SEG);
+      if (ln.state == ST_SAMPLE && ln.sm == SM_STEP) {
+        env.prof(PB_STEP);
+        ++ln.n_dda;
+        if (hdda_step(G, ln)) {
+          if (Debug) env.tally(CNT_SEGMENTS, 1);
+          ln.sm = (ln.s_dmaj <= 0.0f) ? SM_NEED_SEG : SM_DRAW;  // empty segment: no draw (:32-35)
+        }
+      }
+      env.tick(PT_STEP);
+      if (ln.state == ST_SAMPLE && ln.sm == SM_DRAW) {
+        env.prof(PB_DRAW);
+        // MajorantTransmittanceSampler::next body (majorant_transmittance_sampler.cpp:39-79)
+        float sigma_maj = ln.s_dmaj * S.sigma_t;
+        float u = rng_uniform(ln.rng);
+        if (Debug) {
+          env.tally(CNT_DRAWS, 1);
+          env.tally(CNT_RNG_DRAWS, 1);
+        }
+  #if defined(VPT_ABL_CHEAPLOG)  // timing ablations only (not bit-exact)
+        float dt_m = -__logf(1 - u) / sigma_maj;
+        float t = ln.s_t0 + dt_m / ln.scale;
+  #elif defined(VPT_ABL_FASTDIV)
+        float dt_m = __fdividef(-math::logf_glibc_unit(1 - u), sigma_maj);
+        float t = ln.s_t0 + __fdividef(dt_m, ln.scale);
+  #else
+        float dt_m = -math::logf_glibc_unit(1 - u) / sigma_maj;
+        float t = ln.s_t0 + dt_m / ln.scale;
+  #endif
+        if (t < ln.s_t1) {
+          ln.s_t0 = t;       // the tentative collision; its density is evaluated in SM_EVAL
+          ln.sm = SM_EVAL;
+        } else {
+          ln.sm = SM_NEED_SEG;
+        }
+      }
+      env.tick(PT_DRAW);
+      } while (S.gate_walk > 0 && env.count(ln.state == ST_SAMPLE && ln.sm != SM_EVAL) >= S.gate_walk &&
+               env.count(ln.state == ST_SAMPLE && ln.sm == SM_EVAL) < S.gate_eval);
+    }
+  }
+  env.tick(PT_WALK);
+  {
+    const DevScene S = *opaque(sp);
+    const DevGrid& G = S.density;
+    (void)G;
+    // Tentative collisions wait until gate_eval lanes of the wavefront have one (or the walk runs
+    // short of lanes), so the stencil gathers and the event logic run on a fuller wavefront.
+    const int32_t n_eval = env.count(ln.state == ST_SAMPLE && ln.sm == SM_EVAL);
+    const bool run_eval = n_eval > 0 && (n_eval >= S.gate_eval || env.count(ln.state == ST_SAMPLE && ln.sm != SM_EVAL) < S.gate_idle);
+    if (run_eval && ln.state == ST_SAMPLE && ln.sm == SM_EVAL) {
+      env.prof(PB_TRILINEAR);
+      const float t = ln.s_t0;
+      const float sigma_maj = ln.s_dmaj * S.sigma_t;
+      float pi_x = ln.e[0] + ln.d[0] * t, pi_y = ln.e[1] + ln.d[1] * t, pi_z = ln.e[2] + ln.d[2] * t;
+      float dens;
+      if (Debug) env.tally(CNT_DENSITY_EVALS, 1);
+      if (trilinear(G, ln.dens_cell, pi_x, pi_y, pi_z, dens)) ++ln.n_stencil;
+      ln.sm = SM_DRAW;  // density <= 0, a null event or an unkilled shadow ray: keep drawing
+      if (dens > 0.0f) {
+        float cp[3];
+        map_fwd(G, pi_x, pi_y, pi_z, cp[0], cp[1], cp[2]);
+        if (!ln.shadow) {
+          env.prof(PB_EVENT);
+          // worker.cpp:148-188
+          float p_a = (S.sigma_a * dens) / sigma_maj;
+          float p_s = (S.sigma_s * dens) / sigma_maj;
+          float p_n = fmaxf(1.0f - p_a - p_s, 0.0f);
+          if (HasTemp) {
+            float tx, ty, tz, tadim, X, Y, Z;
+            map_inv(S.temperature, cp[0], cp[1], cp[2], tx, ty, tz);
+            env.tally(CNT_TEMP_STENCILS, trilinear(S.temperature, ln.temp_cell, tx, ty, tz, tadim) ? 1 : 0);
+            float tK = tadim * S.temp_scale + S.temp_offset;
+            blackbody_xyz(S, tK, X, Y, Z);
+            float sc = p_a * S.le_scale;
+            ln.L[0] = ln.L[0] + sc * X;
+            ln.L[1] = ln.L[1] + sc * Y;
+            ln.L[2] = ln.L[2] + sc * Z;
+          }
+          float ue = rng_uniform(ln.rng);
+          if (Debug) env.tally(CNT_RNG_DRAWS, 1);
+          // sample_discrete({Null p_n, Absorption p_a, Scatter p_s}, u) (random.hpp:30-47)
+          float total = ((0.0f + p_n) + p_a) + p_s;
+          float uu = ue * total;
+          int ev;
+          uu -= p_n;
+          if (uu <= 0) {
+            ev = 0;
+          } else {
+            uu -= p_a;
+            ev = (uu <= 0) ? 1 : 2;
+          }
+          if (ev == 1) {
             ln.terminated = 1;
             ln.state = ST_FINISH;
-          } else {
-            if (Debug) env.tally(CNT_SCATTERS, 1);
-            // The next primary ray starts at the scatter point (worker.cpp:179): keep it in ro.
-            for (int i = 0; i < 3; ++i) ln.ro[i] = cp[i];
-            // sample_Ld (worker.cpp:52-90)
-            if (S.li_zero) {
-              ln.Tr = -1.0f;  // returns Li == 0 without draws
-              ln.state = ST_NEE_DONE;
+          } else if (ev == 2) {
+            if (ln.depth++ >= S.max_depth) {
+              ln.terminated = 1;
+              ln.state = ST_FINISH;
             } else {
-              ln.Tr = 1.0f;
-              ln.shadow = 1;
-              ln.state = ST_SHADOW;
+              if (Debug) env.tally(CNT_SCATTERS, 1);
+              // The next primary ray starts at the scatter point (worker.cpp:179): keep it in ro.
+              for (int i = 0; i < 3; ++i) ln.ro[i] = cp[i];
+              // sample_Ld (worker.cpp:52-90)
+              if (S.li_zero) {
+                ln.Tr = -1.0f;  // returns Li == 0 without draws
+                ln.state = ST_NEE_DONE;
+              } else {
+                ln.Tr = 1.0f;
+                ln.shadow = 1;
+                ln.state = ST_SHADOW;
+              }
             }
           }
-        }
-        // ev == 0 (Null): keep drawing in the same segment.
-      } else {
-        env.prof(PB_SHADOW_HIT);
-        // Ratio tracking with Russian roulette (worker.cpp:68-85)
-        float sigma_n = fmaxf(0.0f, sigma_maj - S.sigma_t * dens);
-        ln.Tr *= sigma_n / sigma_maj;
-        if (ln.Tr <= 0.05f) {
-          float q = 0.75f;
-          if (Debug) env.tally(CNT_RNG_DRAWS, 1);
-          if (rng_uniform(ln.rng) < q)
-            ln.Tr = 0.0f;
-          else
-            ln.Tr /= 1 - q;
-        }
-        if (ln.Tr <= 0.0f) {
-          ln.Tr = -1.0f;  // returns Zero()
-          ln.state = ST_NEE_DONE;
+          // ev == 0 (Null): keep drawing in the same segment.
+        } else {
+          env.prof(PB_SHADOW_HIT);
+          // Ratio tracking with Russian roulette (worker.cpp:68-85)
+          float sigma_n = fmaxf(0.0f, sigma_maj - S.sigma_t * dens);
+          ln.Tr *= sigma_n / sigma_maj;
+          if (ln.Tr <= 0.05f) {
+            float q = 0.75f;
+            if (Debug) env.tally(CNT_RNG_DRAWS, 1);
+            if (rng_uniform(ln.rng) < q)
+              ln.Tr = 0.0f;
+            else
+              ln.Tr /= 1 - q;
+          }
+          if (ln.Tr <= 0.0f) {
+            ln.Tr = -1.0f;  // returns Zero()
+            ln.state = ST_NEE_DONE;
+          }
         }
       }
     }
   }
-
   env.tick(PT_EVAL);
 }
 
