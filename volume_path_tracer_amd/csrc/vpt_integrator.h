@@ -215,7 +215,7 @@ struct DevScene {
   float wi[3];          // distant_light.inv_direction.normalized() (worker.cpp:54)
   // Shadow rays all have direction wi: their index-space direction, its reciprocal, the length
   // factor and the iterator scale are scene constants (scene_finalize; same float operations).
-  float sh_d[3], sh_inv[3], sh_len, sh_scale;
+  float sh_d[3], sh_inv[3], sh_len, sh_scale, sh_rscale;
   // Henyey-Greenstein terms that depend on g only (random.hpp:56-84, utils.hpp:61-66): the same
   // float values the reference recomputes at every call.
   float hg_g2, hg_1pg2, hg_1mg2, hg_1pg, hg_2g, hg_inv2g, hg_num;
@@ -352,7 +352,8 @@ struct Lane {
   float Tr;            // shadow-ray transmittance (< 0: sample_Ld returns zero)
   // RayMajorantIterator: index-space ray, scale, majorant, HDDA (NanoVDB math::HDDA state)
   float e[3], d[3], inv[3];
-  float scale, maj;
+  float scale, rscale;  // m_scale and recip_for_div(m_scale)
+  float maj;
   int32_t dim;
   float T0, T1;
   float nxt[3];
@@ -372,7 +373,7 @@ __host__ __device__ __forceinline__ int32_t hdda_stp(float d, float inv) { retur
 // The direction-only part of Ray::worldToIndexF + RayMajorantIterator's scale: index-space unit
 // direction d, invDir = 1/d, |worldToIndexDirF(dir)| (scales t0) and m_scale.
 struct RayDir {
-  float d[3], inv[3], len, scale;
+  float d[3], inv[3], len, scale, rscale;
 };
 __host__ __device__ __forceinline__ RayDir ray_dir_setup(const DevGrid& g, const float dir[3]) {
   RayDir r;
@@ -391,6 +392,7 @@ __host__ __device__ __forceinline__ RayDir ray_dir_setup(const DevGrid& g, const
   float jx, jy, jz;
   jac_inv(g, r.d[0], r.d[1], r.d[2], jx, jy, jz);
   r.scale = 1 / sqrtf(jx * jx + jy * jy + jz * jz);
+  r.rscale = math::recip_for_div(r.scale);
   return r;
 }
 
@@ -428,6 +430,7 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
   ln.inv[1] = iy;
   ln.inv[2] = iz;
   ln.scale = rd.scale;
+  ln.rscale = rd.rscale;
   // HDDA(ray, max(8, getDim(floor(ray.start())))) -> init(ray, t0, t1, dim)
   float px = ex + dx * t0, py = ey + dy * t0, pz = ez + dz * t0;
   const Cell c0 = cell_at(g, (int32_t)floorf(px), (int32_t)floorf(py), (int32_t)floorf(pz));
@@ -588,6 +591,7 @@ __host__ __device__ inline void scene_finalize(DevScene& S) {
   }
   S.sh_len = r.len;
   S.sh_scale = r.scale;
+  S.sh_rscale = r.rscale;
   const float g = S.g_hg;
   S.hg_g2 = g * g;
   S.hg_1pg2 = 1.0f + S.hg_g2;
@@ -796,6 +800,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
           }
           rd.len = S.sh_len;
           rd.scale = S.sh_scale;
+          rd.rscale = S.sh_rscale;
         }
         if (begin_ray(G, ln, ln.ro, rd)) {
           if (Debug && !primary) env.tally(CNT_SHADOW_RAYS, 1);
@@ -849,16 +854,8 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
           env.tally(CNT_DRAWS, 1);
           env.tally(CNT_RNG_DRAWS, 1);
         }
-  #if defined(VPT_ABL_CHEAPLOG)  // timing ablations only (not bit-exact)
-        float dt_m = -__logf(1 - u) / sigma_maj;
-        float t = ln.s_t0 + dt_m / ln.scale;
-  #elif defined(VPT_ABL_FASTDIV)
-        float dt_m = __fdividef(-math::logf_glibc_unit(1 - u), sigma_maj);
-        float t = ln.s_t0 + __fdividef(dt_m, ln.scale);
-  #else
         float dt_m = -math::logf_glibc_unit(1 - u) / sigma_maj;
-        float t = ln.s_t0 + dt_m / ln.scale;
-  #endif
+        float t = ln.s_t0 + math::div_by_recip(dt_m, ln.scale, ln.rscale);  // == dt_m / m_scale
         if (t < ln.s_t1) {
           ln.s_t0 = t;       // the tentative collision; its density is evaluated in SM_EVAL
           ln.sm = SM_EVAL;

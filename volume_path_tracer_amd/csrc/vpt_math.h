@@ -157,5 +157,25 @@ __host__ __device__ __forceinline__ float cosf_glibc(float y) {
   return sinf_poly(x * s, x * x, (n & 2) != 0, n ^ 1);
 }
 
+// RN(a / b) from y = RN(1 / b) with two fmas (Markstein's correction step):
+//   q = RN(a*y); r = a - q*b (exact, fma); RN(q + r*y) == RN(a/b)
+// for every pair of normal a, b whose quotient is normal -- checked exhaustively on MI355X over
+// all 2^46 significand pairs (tools/proofs/recip_div.hip; exponents scale exactly).  The caller
+// guarantees b in [2^-20, 2^20] (so y is normal); q outside [2^-100, 2^100] (this also catches
+// a = 0, inf, NaN, and keeps a normal) takes the correctly rounded division instead.
+__host__ __device__ __forceinline__ bool recip_div_ok(float q) {
+  return (as_u32(q) & 0x7fffffffu) - 0x0d800000u < 0x64000000u;  // |q| in [2^-100, 2^100)
+}
+__host__ __device__ __forceinline__ float div_by_recip(float a, float b, float y) {
+  const float q = a * y;
+  if (recip_div_ok(q)) return fmaf(fmaf(-q, b, a), y, q);
+  return a / b;
+}
+// y = RN(1/b) when b is in [2^-20, 2^20] (div_by_recip's domain), else NaN (then every
+// div_by_recip(a, b, y) takes the division).
+__host__ __device__ __forceinline__ float recip_for_div(float b) {
+  const uint32_t e = (as_u32(b) >> 23) & 0xffu;
+  return (e >= 127u - 20u && e < 127u + 20u) ? 1.0f / b : __builtin_nanf("");
+}
 }  // namespace math
 }  // namespace vpt
