@@ -193,6 +193,37 @@ int vpt_gpu_render_jobs(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count
 int vpt_gpu_render_jobs_records(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count,
                                 float* film_device, float* records_device, void* hip_stream);
 
+/* ---- debug traces ------------------------------------------------------------ */
+
+/* One line of the reference's event log (Logger<true>, src/worker.cpp:16-48 -> log.csv). */
+enum {
+  VPT_EV_NEW_RAY = 0,            /* v = camera ray origin xyz, direction xyz (worker.cpp:125)    */
+  VPT_EV_SAMPLED_POINT = 1,      /* v = collision point xyz (world), density (worker.cpp:145)    */
+  VPT_EV_NULL = 2,               /* (worker.cpp:164)                                             */
+  VPT_EV_SCATTER_TERMINATED = 3, /* (worker.cpp:168)                                             */
+  VPT_EV_SCATTER = 4,            /* v = new ray origin xyz, direction xyz (worker.cpp:180)       */
+  VPT_EV_ABSORBED = 5            /* (worker.cpp:185)                                             */
+};
+typedef struct vpt_event {
+  uint64_t jid;    /* job id                                                    */
+  uint32_t pixel;  /* pixel within the job's clipped tile rect, y * width + x   */
+  uint32_t seq;    /* order of the event within its job                         */
+  uint32_t type;   /* VPT_EV_*                                                   */
+  float v[7];
+} vpt_event;     /* 48 bytes */
+
+/* Render jobs like vpt_gpu_render_jobs and append every Logger event to events_device (capacity
+ * entries, unordered across jobs: sort by (jid, seq)).  *count = events produced (may exceed
+ * capacity; the excess is dropped).  Synchronous. */
+int vpt_gpu_trace_jobs(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film_device,
+                       vpt_event* events_device, uint64_t capacity, uint64_t* count, void* hip_stream);
+
+/* Volume::log_majorant_trace (src/volume.cpp:176-192) for one world ray: per RayMajorantIterator
+ * segment the row X0,Y0,Z0,X1,Y1,Z1,T0,T1,Majorant (index-space end points, world-space t).
+ * rows_host: [max_rows][9]; *n_rows = segments (0 if the ray misses the volume).  Synchronous. */
+int vpt_gpu_majorant_trace(vpt_gpu_ctx* ctx, const float origin[3], const float direction[3],
+                           float* rows_host, int max_rows, int* n_rows);
+
 int vpt_gpu_sync(vpt_gpu_ctx* ctx);
 /* Zero the context's own film. */
 int vpt_gpu_film_clear(vpt_gpu_ctx* ctx);

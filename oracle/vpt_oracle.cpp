@@ -689,8 +689,35 @@ V3 sample_Ld(const Scene& S, Rng& rng, V3 pos, V3 w, vpt_counters* cnt) {  // wo
 }
 
 // One (tile, wave) job: the body of `while (auto tok = tp.next())` (worker.cpp:104-207).
+// Logger<true> (worker.cpp:16-48) as records instead of log.csv lines.
+struct EventSink {
+  vpt_event* out;
+  uint64_t cap;
+  uint64_t n = 0;
+  uint32_t seq = 0;
+  void log(uint64_t jid, uint32_t pixel, uint32_t type, const V3* a, const V3* b, float x) {
+    const uint32_t sq = seq++;
+    if (n < cap) {
+      vpt_event& e = out[n];
+      e.jid = jid;
+      e.pixel = pixel;
+      e.seq = sq;
+      e.type = type;
+      const float av[3] = {a ? a->x : 0.0f, a ? a->y : 0.0f, a ? a->z : 0.0f};
+      const float bv[3] = {b ? b->x : x, b ? b->y : 0.0f, b ? b->z : 0.0f};
+      for (int i = 0; i < 3; ++i) {
+        e.v[i] = av[i];
+        e.v[3 + i] = bv[i];
+      }
+      e.v[6] = 0.0f;
+    }
+    ++n;
+  }
+};
+
 void run_job(const Scene& S, uint64_t jid, float* film, float* records, uint64_t record_base,
-             vpt_counters* cnt) {
+             vpt_counters* cnt, EventSink* log = nullptr) {
+  if (log) log->seq = 0;
   const vpt_configuration& cfg = *S.cfg;
   const vpt_worker_params& P = cfg.worker_parameters;
   const vpt_volume_params& VP = cfg.volume_parameters;
@@ -722,6 +749,8 @@ void run_job(const Scene& S, uint64_t jid, float* film, float* records, uint64_t
       jy *= js;
       V3 r_o = S.cam.position;
       V3 r_d = camera_dir(S.cam, px, py, jx, jy);
+      const uint32_t pix = (uint32_t)(y * rw + x);
+      if (log) log->log(jid, pix, VPT_EV_NEW_RAY, &r_o, &r_d, 0.0f);
       V3 L = v3(0, 0, 0);
       bool terminated = false;
       for (unsigned int depth = 0; depth < P.max_depth; ++depth) {
@@ -732,6 +761,7 @@ void run_job(const Scene& S, uint64_t jid, float* film, float* records, uint64_t
         MajorantTransmittanceSampler sampler(it, rng, S.density, sigma_t, cnt);
         MediumProperties props;
         while (sampler.next(props)) {
+          if (log) log->log(jid, pix, VPT_EV_SAMPLED_POINT, &props.point, nullptr, props.density);
           float p_a = (VP.sigma_a * props.density) / props.sigma_maj;
           float p_s = (VP.sigma_s * props.density) / props.sigma_maj;
           float p_n = std::max<float>(1.0f - p_a - p_s, 0.0f);
@@ -747,9 +777,11 @@ void run_job(const Scene& S, uint64_t jid, float* film, float* records, uint64_t
           if (cnt) ++cnt->rng_draws;
           ScatterEvent ev = sample_discrete3(p_n, p_a, p_s, ue);
           if (ev == ScatterEvent::Null) {
+            if (log) log->log(jid, pix, VPT_EV_NULL, nullptr, nullptr, 0.0f);
             continue;
           } else if (ev == ScatterEvent::Scatter) {
             if (depth++ >= P.max_depth) {
+              if (log) log->log(jid, pix, VPT_EV_SCATTER_TERMINATED, nullptr, nullptr, 0.0f);
               terminated = true;
               break;
             }
@@ -761,9 +793,11 @@ void run_job(const Scene& S, uint64_t jid, float* film, float* records, uint64_t
             V3 nd = sample_henyey_greenstein(r_d, u0, u1, VP.henyey_greenstein_g);
             r_o = props.point;
             r_d = nd;
+            if (log) log->log(jid, pix, VPT_EV_SCATTER, &r_o, &r_d, 0.0f);
             scattered = true;
             break;
           } else {
+            if (log) log->log(jid, pix, VPT_EV_ABSORBED, nullptr, nullptr, 0.0f);
             terminated = true;
             break;
           }
@@ -1086,6 +1120,39 @@ int vpto_trace_segments(const vpto_grid* G, const float* o, const float* d, floa
       out[n * 3 + 0] = s.t0;
       out[n * 3 + 1] = s.t1;
       out[n * 3 + 2] = s.d_maj;
+    }
+    ++n;
+  }
+  return n;
+}
+
+int vpto_render_jobs_events(const vpt_configuration* cfg, const vpto_grid* density, const vpto_grid* temperature,
+                            const float* bb_table, const float* cie, float y_integral, uint64_t jid_begin,
+                            uint64_t jid_count, float* film, vpt_event* events, uint64_t capacity, uint64_t* count) {
+  if (!cfg || !density || !film || !count) return VPT_E_INVALID;
+  std::vector<float> bb(501 * 3, 0.0f);
+  if (bb_table) std::memcpy(bb.data(), bb_table, 500 * 3 * sizeof(float));
+  Scene S = make_scene(cfg, &density->g, temperature ? &temperature->g : nullptr, bb.data(), cie, y_integral);
+  EventSink sink{events, events ? capacity : 0};
+  for (uint64_t j = 0; j < jid_count; ++j) run_job(S, jid_begin + j, film, nullptr, j, nullptr, &sink);
+  *count = sink.n;
+  return VPT_OK;
+}
+
+// Volume::log_majorant_trace (volume.cpp:176-192): rows X0,Y0,Z0,X1,Y1,Z1,T0,T1,Majorant.
+int vpto_majorant_trace(const vpto_grid* G, const float* o, const float* d, float* rows, int max_rows) {
+  NRay ir(v3(0, 0, 0), v3(1, 0, 0));
+  if (!volume_intersect(G->g, v3(o[0], o[1], o[2]), v3(d[0], d[1], d[2]), ir)) return 0;
+  RayMajorantIterator it(ir, &G->g);
+  Segment sg;
+  int n = 0;
+  while (it.next(sg)) {
+    if (n < max_rows) {
+      const float w0 = sg.t0 * it.scale, w1 = sg.t1 * it.scale;  // t * idx_to_world_scale()
+      const V3 p0 = G->g.worldToIndexF(v3(o[0] + d[0] * w0, o[1] + d[1] * w0, o[2] + d[2] * w0));
+      const V3 p1 = G->g.worldToIndexF(v3(o[0] + d[0] * w1, o[1] + d[1] * w1, o[2] + d[2] * w1));
+      const float r[9] = {p0.x, p0.y, p0.z, p1.x, p1.y, p1.z, w0, w1, sg.d_maj};
+      std::memcpy(rows + 9 * n, r, sizeof r);
     }
     ++n;
   }

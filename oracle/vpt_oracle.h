@@ -63,6 +63,16 @@ int vpto_render_jobs(const vpt_configuration* cfg, const vpto_grid* density,
                      float y_integral, uint64_t jid_begin, uint64_t jid_count, float* film,
                      float* records, vpt_counters* counters);
 
+/* Same, logging every Logger event (worker.cpp:16-48) into events (capacity entries, in job order);
+ * *count = events produced. */
+int vpto_render_jobs_events(const vpt_configuration* cfg, const vpto_grid* density,
+                            const vpto_grid* temperature, const float* bb_table, const float* cie,
+                            float y_integral, uint64_t jid_begin, uint64_t jid_count, float* film,
+                            vpt_event* events, uint64_t capacity, uint64_t* count);
+/* Volume::log_majorant_trace (volume.cpp:176-192): [max_rows][9] rows; returns the segment count. */
+int vpto_majorant_trace(const vpto_grid* density, const float* origin3, const float* dir3, float* rows,
+                        int max_rows);
+
 /* The reference worker pool (src/main.cpp:62-87): num_workers threads calling run() over a
  * TileProvider(output_size, num_waves, tile_size).  Returns wall milliseconds (or <0 on error). */
 double vpto_render_pool(const vpt_configuration* cfg, const vpto_grid* density,

@@ -27,6 +27,7 @@ struct HostEnv {
   void tally(int32_t k, int32_t w) { cnt[k] += (uint64_t)w; }
   void prof(int32_t) {}
   void tick(int32_t) {}
+  void event(vpt::Lane&, uint32_t, const float*, const float*, float) {}
   bool fetch_job(uint64_t& j) {
     if (next >= jid_count) return false;
     j = next++;

@@ -1,0 +1,113 @@
+"""Debug traces: the Logger event log (src/worker.cpp:16-48) and
+Volume::log_majorant_trace (src/volume.cpp:176-192), GPU against the oracle, CSV as the reference
+prints it."""
+import subprocess
+import tempfile
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from volume_path_tracer_amd import capi, traces
+from volume_path_tracer_amd.scenes import SynthGrid, workload
+
+VALUES = [0.5, 1e-5, 123456789.0, -0.0, 3.14159265, 1e30, 1.4e-45, 0.1, 100000.0, 1000000.0, -2.5e-7,
+          float("inf"), float("-inf"), 65504.0, 0.000123456, 7.0]
+
+
+def test_fmt_matches_std_ostream(tmp_path):
+    src = tmp_path / "p.cpp"
+    lits = ", ".join(("std::numeric_limits<float>::infinity()" if v == float("inf") else
+                      "-std::numeric_limits<float>::infinity()" if v == float("-inf") else
+                      repr(float(np.float32(v))) + "f" if v != 0 else "-0.0f") for v in VALUES)
+    src.write_text("#include <iostream>\n#include <limits>\nint main(){ float v[] = {%s};\n"
+                   " for (float x : v) std::cout << x << '\\n'; }\n" % lits)
+    exe = tmp_path / "p"
+    subprocess.run(["g++", "-O0", "-o", str(exe), str(src)], check=True)
+    want = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    assert [traces.fmt(v) for v in VALUES] == want
+
+
+def _small(name="c3", w=24, h=16, spp=2, n=64):
+    wl = workload(name, width=w, height=h, spp=spp, grid_n=n)
+    dens = SynthGrid(wl.density_kind, wl.grid_n).grid()
+    temp = SynthGrid(2, wl.grid_n).grid() if wl.temperature else None
+    return wl, dens, temp
+
+
+def test_oracle_event_log_structure(tmp_path):
+    wl, dens, temp = _small()
+    od = O.OracleGrid(dens, fix_majorants=True)
+    jobs = wl.cfg.jobs_per_wave() * wl.spp
+    ev, film = O.render_jobs_events(wl.cfg, od, None, 0, jobs)
+    names = np.array(capi.EVENT_NAMES)[ev["type"]]
+    assert (names == "new_ray").sum() == wl.cfg.width * wl.cfg.height * wl.spp
+    assert {"sampled_point", "scatter", "null"} <= set(names)
+    # every job's log starts with a camera ray and its sequence numbers count up from 0
+    for j in np.unique(ev["jid"]):
+        e = ev[ev["jid"] == j]
+        assert e["type"][0] == 0 and (e["seq"] == np.arange(len(e))).all()
+    # a sampled point is followed by its decision (null / scatter / absorbed / terminated)
+    nxt = ev["type"][1:][ev["type"][:-1] == 1]
+    assert set(nxt.tolist()) <= {2, 3, 4, 5}
+    p = tmp_path / "log.csv"
+    traces.write_event_log(ev, p)
+    lines = p.read_text().splitlines()
+    assert len(lines) == len(ev) and lines[0].startswith("new_ray,") and len(lines[0].split(",")) == 7
+
+
+def test_oracle_majorant_trace_matches_segments():
+    wl, dens, _ = _small()
+    od = O.OracleGrid(dens, fix_majorants=True)
+    o = np.array(wl.cfg.camera_parameters.position, np.float32)
+    d = np.array([0.05, -0.02, 1.0], np.float32)
+    d /= np.linalg.norm(d)
+    rows = O.majorant_trace(od, o, d)
+    assert len(rows) > 3
+    assert (rows[1:, 6] == rows[:-1, 7]).all()          # segments are contiguous in t
+    assert (rows[:, 7] > rows[:, 6]).all() and (rows[:, 8] >= 0).all()
+    lines = traces.majorant_lines(rows)
+    assert lines[0] == "X0,Y0,Z0,X1,Y1,Z1,T0,T1,Majorant" and len(lines) == len(rows) + 1
+    miss = O.majorant_trace(od, o, -d)
+    assert len(miss) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c3", "c4", "c2"])
+def test_gpu_event_log_bit_exact(name):
+    from volume_path_tracer_amd.render import Integrator
+
+    wl, dens, temp = _small(name, n=32 if name == "c2" else 64)
+    it = Integrator(wl.cfg, dens, temp, device=0)
+    jobs = wl.cfg.jobs_per_wave() * wl.spp
+    ev_g = it.trace_jobs(0, jobs)
+    od = O.OracleGrid(dens, fix_majorants=True)
+    ot = O.OracleGrid(temp, fix_majorants=False) if temp is not None else None
+    ev_o, _ = O.render_jobs_events(wl.cfg, od, ot, 0, jobs)
+    assert len(ev_g) == len(ev_o)
+    assert ev_g.tobytes() == ev_o.tobytes()
+    assert traces.event_lines(ev_g) == traces.event_lines(ev_o)
+
+
+@pytest.mark.gpu
+def test_gpu_majorant_trace_bit_exact():
+    from grids import sparse_grid
+
+    from volume_path_tracer_amd.render import Integrator
+
+    dens = sparse_grid()
+    wl = workload("c3", width=16, height=16, spp=1)
+    it = Integrator(wl.cfg, dens, None, device=0)
+    od = O.OracleGrid(dens, fix_majorants=True)
+    rng = np.random.default_rng(5)
+    hits = 0
+    for _ in range(64):
+        o = rng.uniform(-600, 600, 3).astype(np.float32)
+        tgt = rng.uniform(-150, 150, 3).astype(np.float32)
+        d = (tgt - o).astype(np.float32)
+        d = (d / np.float32(np.linalg.norm(d))).astype(np.float32)
+        g, r = it.majorant_trace(o, d), O.majorant_trace(od, o, d)
+        assert g.shape == r.shape and g.tobytes() == r.tobytes()
+        hits += len(g) > 0
+    assert hits > 20

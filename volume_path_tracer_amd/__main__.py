@@ -34,9 +34,12 @@ def main(argv=None) -> int:
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--batch-waves", type=int, default=8, help="waves per kernel launch")
     ap.add_argument("--film-out", default=None, help="also save the raw XYZW film (.npy)")
+    ap.add_argument("--event-log", default=None,
+                    help="write the Logger event log (log.csv format) of the first --event-jobs jobs")
+    ap.add_argument("--event-jobs", type=int, default=1)
     args = ap.parse_args(argv)
 
-    from . import image, volumes
+    from . import image, traces, volumes
     from .render import Integrator, TileProvider, run
     from .scenes import SynthGrid, read_configuration
 
@@ -69,6 +72,9 @@ def main(argv=None) -> int:
         ms = (time.perf_counter() - t0) * 1e3
         print(f"[vpt] Rendering complete in {ms:.0f} ms ({cfg.width}x{cfg.height}, {cfg.num_waves} spp)",
               file=sys.stderr)
+        if args.event_log:
+            scratch = it.torch.zeros_like(it.film)  # the traced jobs are not part of the image
+            traces.write_event_log(it.trace_jobs(0, args.event_jobs, film=scratch), args.event_log)
         if args.film_out:
             import numpy as np
 

@@ -88,6 +88,12 @@ class Counters(C.Structure):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
 
 
+# vpt_event (include/vpt_gpu.h): one Logger line (src/worker.cpp:16-48)
+EVENT_DTYPE = np.dtype([("jid", "<u8"), ("pixel", "<u4"), ("seq", "<u4"), ("type", "<u4"), ("v", "<f4", (7,))])
+assert EVENT_DTYPE.itemsize == 48
+EVENT_NAMES = ("new_ray", "sampled_point", "null", "scatter_terminated", "scatter", "absorbed")
+
+
 def _ptr(arr, ctype):
     if arr is None:
         return C.cast(None, C.POINTER(ctype))
@@ -217,6 +223,8 @@ def lib() -> C.CDLL:
     L.vpt_synth_grid.restype = gridp
     L.vpt_synth_free.argtypes = [gridp]
     L.vpt_film_to_srgb8.argtypes = [fp, C.c_int64, C.c_int64, C.POINTER(C.c_uint8)]
+    L.vpt_gpu_trace_jobs.argtypes = [vp, C.c_uint64, C.c_uint64, vp, vp, C.c_uint64, C.POINTER(C.c_uint64), vp]
+    L.vpt_gpu_majorant_trace.argtypes = [vp, fp, fp, fp, C.c_int, C.POINTER(C.c_int)]
     _lib = L
     return L
 

@@ -7,6 +7,7 @@
 // reaches ST_DONE.  Film accumulation uses no-return fp32 atomics into the [H][W][4] XYZW film.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -53,6 +54,9 @@ struct KernelEnv {
   unsigned long long* prof_buf;  // [PB_COUNT][2] wave executions, active lanes; then [PT_COUNT] cycles
   unsigned long long* lds_prof;  // this workgroup's section cycles (LDS, VPT_PROFILE builds)
   unsigned long long* lds_counters;  // this workgroup's event counters (LDS)
+  vpt_event* events;                 // Logger events (trace launches only)
+  unsigned long long* event_count;
+  uint64_t event_cap;
 
   // Adds w for every active lane with w != 0 (w uniform per call site) to a workgroup counter.
   __device__ __forceinline__ void tally(int32_t k, int32_t w) {
@@ -86,6 +90,23 @@ struct KernelEnv {
 #else
     (void)id;
 #endif
+  }
+  // One Logger line (src/worker.cpp:16-48); a = xyz, b = xyz or (b == nullptr) x in v[3].
+  __device__ __forceinline__ void event(Lane& ln, uint32_t type, const float* a, const float* b, float x) {
+    if (!events) return;
+    const unsigned long long slot = atomicAdd(event_count, 1ULL);
+    const uint32_t seq = ln.n_events++;
+    if (slot >= event_cap) return;
+    vpt_event* e = events + slot;
+    e->jid = jid_begin + ln.jid_local;
+    e->pixel = (uint32_t)(ln.pix - 1);
+    e->seq = seq;
+    e->type = type;
+    for (int i = 0; i < 3; ++i) {
+      e->v[i] = a ? a[i] : 0.0f;
+      e->v[3 + i] = b ? b[i] : (i == 0 ? x : 0.0f);
+    }
+    e->v[6] = 0.0f;
   }
   // lanes of this wavefront for which pred holds
   __device__ __forceinline__ int32_t count(bool pred) { return (int32_t)__popcll(__ballot(pred)); }
@@ -139,6 +160,47 @@ __global__ __launch_bounds__(kBlockThreads, (HasTemp || Debug) ? VPT_WAVES_SLOW 
 #if defined(VPT_PROFILE) || defined(VPT_PROFILE_TIME)
   if (threadIdx.x < PT_COUNT) atomicAdd(env.prof_buf + 2 * PB_COUNT + threadIdx.x, wg_prof[threadIdx.x]);
 #endif
+}
+
+// Volume::log_majorant_trace (src/volume.cpp:176-192) of one world ray, on one lane: every
+// RayMajorantIterator segment as X0,Y0,Z0,X1,Y1,Z1 (density index space), T0,T1 (world), d_maj.
+__global__ void vpt_majorant_trace_kernel(const DevScene* scene, float ox, float oy, float oz, float dx, float dy,
+                                          float dz, float* rows, int max_rows, int* n_rows) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const ScenePtr sp = (ScenePtr)scene;
+  const DevScene S = *sp;
+  const DevGrid& G = S.density;
+  const float o[3] = {ox, oy, oz}, d[3] = {dx, dy, dz};
+  Lane ln;
+  lane_init(ln);
+  int n = 0;
+  if (begin_ray(G, ln, o, ray_dir_setup(G, d))) {
+    while (ln.T0 < ln.T1) {  // RayMajorantIterator::next: segments until the HDDA leaves [t0, t1]
+      ln.s_t0 = ln.T0;
+      while (!hdda_step(G, ln)) {
+      }
+      if (n < max_rows) {
+        const float w0 = ln.s_t0 * ln.scale, w1 = ln.s_t1 * ln.scale;  // t * idx_to_world_scale()
+        float p0[3], p1[3], q0[3], q1[3];
+        for (int i = 0; i < 3; ++i) {  // Ray::eval: origin + direction * t
+          p0[i] = o[i] + d[i] * w0;
+          p1[i] = o[i] + d[i] * w1;
+        }
+        map_inv(G, p0[0], p0[1], p0[2], q0[0], q0[1], q0[2]);  // world_to_density_index
+        map_inv(G, p1[0], p1[1], p1[2], q1[0], q1[1], q1[2]);
+        float* row = rows + 9 * n;
+        for (int i = 0; i < 3; ++i) {
+          row[i] = q0[i];
+          row[3 + i] = q1[i];
+        }
+        row[6] = w0;
+        row[7] = w1;
+        row[8] = ln.s_dmaj;
+      }
+      ++n;
+    }
+  }
+  *n_rows = n;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -235,7 +297,8 @@ void destroy(vpt_gpu_ctx* ctx) {
   delete ctx;
 }
 
-int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film, float* records, void* stream_ptr) {
+int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film, float* records, void* stream_ptr,
+           vpt_event* events = nullptr, uint64_t event_cap = 0) {
   if (!ctx) return vpt::set_error(VPT_E_INVALID, "render: null context");
   int rc = ctx_device(ctx);
   if (rc) return rc;
@@ -251,8 +314,11 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.records = records;
   env.tile_area = ctx->scene.tw * ctx->scene.th;
   env.prof_buf = ctx->prof;
-  VPT_HIP(hipMemsetAsync(ctx->job_counter, 0, sizeof(unsigned long long), s));
-  const bool temp = ctx->scene.has_temperature != 0, dbg = records != nullptr;
+  env.events = events;
+  env.event_count = ctx->job_counter + 1;
+  env.event_cap = event_cap;
+  VPT_HIP(hipMemsetAsync(ctx->job_counter, 0, 2 * sizeof(unsigned long long), s));
+  const bool temp = ctx->scene.has_temperature != 0, dbg = records != nullptr || events != nullptr;
   auto kernel = temp ? (dbg ? vpt::vpt_integrate_kernel<true, true> : vpt::vpt_integrate_kernel<true, false>)
                      : (dbg ? vpt::vpt_integrate_kernel<false, true> : vpt::vpt_integrate_kernel<false, false>);
   hipLaunchKernelGGL(kernel, dim3(ctx->grid_blocks), dim3(vpt::kBlockThreads), 0, s, ctx->scene_dev, env, ctx->counters);
@@ -313,7 +379,7 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   ctx->film_count = (uint64_t)cfg->output_size[0] * (uint64_t)cfg->output_size[1] * 4;
   VPT_HIP(hipMalloc((void**)&ctx->film, ctx->film_count * sizeof(float)));
   VPT_HIP(hipMemset(ctx->film, 0, ctx->film_count * sizeof(float)));
-  VPT_HIP(hipMalloc((void**)&ctx->job_counter, sizeof(unsigned long long)));
+  VPT_HIP(hipMalloc((void**)&ctx->job_counter, 2 * sizeof(unsigned long long)));  // jobs, events
   VPT_HIP(hipMalloc((void**)&ctx->counters, vpt::kCounterCount * sizeof(unsigned long long)));
   VPT_HIP(hipMemset(ctx->counters, 0, vpt::kCounterCount * sizeof(unsigned long long)));
   VPT_HIP(hipMalloc((void**)&ctx->prof, kProfWords * sizeof(unsigned long long)));
@@ -361,6 +427,47 @@ int vpt_gpu_render_jobs(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count
 int vpt_gpu_render_jobs_records(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film_device,
                                 float* records_device, void* hip_stream) {
   return render(ctx, jid_begin, jid_count, film_device, records_device, hip_stream);
+}
+
+int vpt_gpu_trace_jobs(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film_device,
+                       vpt_event* events_device, uint64_t capacity, uint64_t* count, void* hip_stream) {
+  if (!ctx || !events_device || !count) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_trace_jobs: null argument");
+  *count = 0;
+  int rc = render(ctx, jid_begin, jid_count, film_device, nullptr, hip_stream, events_device, capacity);
+  if (rc) return rc;
+  if (jid_count == 0) return VPT_OK;
+  unsigned long long n = 0;
+  VPT_HIP(hipMemcpyAsync(&n, ctx->job_counter + 1, sizeof n, hipMemcpyDeviceToHost, (hipStream_t)hip_stream));
+  VPT_HIP(hipStreamSynchronize((hipStream_t)hip_stream));
+  *count = n;
+  return VPT_OK;
+}
+
+int vpt_gpu_majorant_trace(vpt_gpu_ctx* ctx, const float origin[3], const float direction[3], float* rows_host,
+                           int max_rows, int* n_rows) {
+  if (!ctx || !origin || !direction || !n_rows || (max_rows > 0 && !rows_host) || max_rows < 0)
+    return vpt::set_error(VPT_E_INVALID, "vpt_gpu_majorant_trace: bad argument");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  float* rows = nullptr;
+  int* n = nullptr;
+  VPT_HIP(hipMalloc((void**)&rows, (size_t)(max_rows > 0 ? max_rows : 1) * 9 * sizeof(float)));
+  if (hipMalloc((void**)&n, sizeof(int)) != hipSuccess) {
+    (void)hipFree(rows);
+    return vpt::set_error(VPT_E_HIP, "vpt_gpu_majorant_trace: hipMalloc failed");
+  }
+  hipLaunchKernelGGL(vpt::vpt_majorant_trace_kernel, dim3(1), dim3(64), 0, nullptr, ctx->scene_dev, origin[0],
+                     origin[1], origin[2], direction[0], direction[1], direction[2], rows, max_rows, n);
+  hipError_t e = hipGetLastError();
+  int nn = 0;
+  if (e == hipSuccess) e = hipMemcpy(&nn, n, sizeof nn, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && max_rows > 0)
+    e = hipMemcpy(rows_host, rows, (size_t)std::min(nn, max_rows) * 9 * sizeof(float), hipMemcpyDeviceToHost);
+  (void)hipFree(rows);
+  (void)hipFree(n);
+  if (e != hipSuccess) return vpt::set_error(VPT_E_HIP, std::string("vpt_gpu_majorant_trace: ") + hipGetErrorString(e));
+  *n_rows = nn;
+  return VPT_OK;
 }
 
 int vpt_gpu_sync(vpt_gpu_ctx* ctx) {

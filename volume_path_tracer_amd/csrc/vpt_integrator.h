@@ -344,7 +344,8 @@ enum : int32_t {
 struct Lane {
   int32_t state, sm, shadow, terminated;
   uint64_t rng;
-  uint64_t jid_local;  // job index relative to jid_begin (records only)
+  uint64_t jid_local;  // job index relative to jid_begin (records / events only)
+  uint32_t n_events;   // events logged so far in this job (event traces only)
   int32_t x0, y0, pix;
   uint32_t depth;
   float L[3];
@@ -676,6 +677,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       float nd[3];
       sample_hg(S, ln.rd, u0, u1, nd);
       for (int i = 0; i < 3; ++i) ln.rd[i] = nd[i];
+      if (Debug) env.event(ln, VPT_EV_SCATTER, ln.ro, ln.rd, 0.0f);
       ++ln.depth;  // the for-loop increment (worker.cpp:130)
       ln.shadow = 0;
       ln.state = ST_RAY;
@@ -713,7 +715,10 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         ln.state = ST_DONE;
         return;
       }
-      if (Debug) ln.jid_local = j;
+      if (Debug) {
+        ln.jid_local = j;
+        ln.n_events = 0;
+      }
       uint64_t jid = env.jid_begin + j;
       ln.rng = job_seed(S.seed, jid);
       uint64_t tile = jid % S.T;
@@ -775,6 +780,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       ln.depth = 0;
       ln.shadow = 0;
       ln.state = ST_RAY;
+      if (Debug) env.event(ln, VPT_EV_NEW_RAY, ln.ro, ln.rd, 0.0f);
     }
   }
   env.tick(PT_PIXEL);
@@ -891,6 +897,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         map_fwd(G, pi_x, pi_y, pi_z, cp[0], cp[1], cp[2]);
         if (!ln.shadow) {
           env.prof(PB_EVENT);
+          if (Debug) env.event(ln, VPT_EV_SAMPLED_POINT, cp, nullptr, dens);
           // worker.cpp:148-188
           float p_a = (S.sigma_a * dens) / sigma_maj;
           float p_s = (S.sigma_s * dens) / sigma_maj;
@@ -920,10 +927,12 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
             ev = (uu <= 0) ? 1 : 2;
           }
           if (ev == 1) {
+            if (Debug) env.event(ln, VPT_EV_ABSORBED, nullptr, nullptr, 0.0f);
             ln.terminated = 1;
             ln.state = ST_FINISH;
           } else if (ev == 2) {
             if (ln.depth++ >= S.max_depth) {
+              if (Debug) env.event(ln, VPT_EV_SCATTER_TERMINATED, nullptr, nullptr, 0.0f);
               ln.terminated = 1;
               ln.state = ST_FINISH;
             } else {
@@ -942,6 +951,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
             }
           }
           // ev == 0 (Null): keep drawing in the same segment.
+          if (Debug && ev == 0) env.event(ln, VPT_EV_NULL, nullptr, nullptr, 0.0f);
         } else {
           env.prof(PB_SHADOW_HIT);
           // Ratio tracking with Russian roulette (worker.cpp:68-85)

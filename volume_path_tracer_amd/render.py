@@ -149,6 +149,35 @@ class Integrator:
         """Waves are 1-based (tile_provider.cpp:30): wave w covers jids [(w-1)*T, w*T)."""
         self.render_jobs((first_wave - 1) * self.jobs_per_wave, num_waves * self.jobs_per_wave, film, None, stream)
 
+    def trace_jobs(self, jid_begin: int, jid_count: int, capacity: int = 1 << 20, film=None, stream=None):
+        """Render jobs and return their Logger events (worker.cpp:16-48) as a numpy array of
+        capi.EVENT_DTYPE sorted by (jid, seq).  Raises if more than `capacity` events occur."""
+        torch = self.torch
+        film = self.film if film is None else film
+        buf = torch.empty((max(1, capacity), capi.EVENT_DTYPE.itemsize), dtype=torch.uint8, device=self.dev)
+        n = C.c_uint64()
+        capi.check(capi.lib().vpt_gpu_trace_jobs(self.h, jid_begin, jid_count, C.c_void_p(film.data_ptr()),
+                                                 C.c_void_p(buf.data_ptr()), capacity, C.byref(n),
+                                                 C.c_void_p(self.stream_handle(stream))), "vpt_gpu_trace_jobs")
+        if n.value > capacity:
+            raise RuntimeError(f"trace_jobs: {n.value} events exceed capacity {capacity}")
+        ev = buf[: n.value].cpu().numpy().view(capi.EVENT_DTYPE).reshape(-1)
+        return np.sort(ev, order=["jid", "seq"])
+
+    def majorant_trace(self, origin, direction, max_rows: int = 1 << 16) -> np.ndarray:
+        """Volume::log_majorant_trace (volume.cpp:176-192) rows [n][9] for one world ray."""
+        o = np.ascontiguousarray(origin, np.float32).reshape(3)
+        d = np.ascontiguousarray(direction, np.float32).reshape(3)
+        rows = np.zeros((max_rows, 9), np.float32)
+        n = C.c_int()
+        fp = C.POINTER(C.c_float)
+        capi.check(capi.lib().vpt_gpu_majorant_trace(self.h, o.ctypes.data_as(fp), d.ctypes.data_as(fp),
+                                                     rows.ctypes.data_as(fp), max_rows, C.byref(n)),
+                   "vpt_gpu_majorant_trace")
+        if n.value > max_rows:
+            raise RuntimeError(f"majorant_trace: {n.value} segments exceed max_rows {max_rows}")
+        return rows[: n.value].copy()
+
     def counters(self, reset: bool = False) -> dict:
         c = capi.Counters()
         capi.check(capi.lib().vpt_gpu_counters(self.h, C.byref(c), 1 if reset else 0), "vpt_gpu_counters")
