@@ -81,6 +81,8 @@ def main():
     ap.add_argument("--spp", type=int, default=None, help="override waves per step (default: the config's)")
     ap.add_argument("--mode", choices=["weak", "strong"], default="weak",
                     help="weak: each rank renders its own spp waves; strong: the spp waves are dealt across ranks")
+    ap.add_argument("--rng-mode", choices=["reference", "pixel"], default="reference",
+                    help="pixel = throughput mode (per-pixel streams; not the reference's samples)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -109,6 +111,9 @@ def main():
     tg = SynthGrid(2, wl.grid_n) if wl.temperature else None
     dens, temp = dg.grid(copy=False), (tg.grid(copy=False) if tg else None)
     it = Integrator(wl.cfg, dens, temp, device=dev.index)
+    if args.rng_mode == "pixel":
+        from volume_path_tracer_amd import capi
+        it.set_rng_mode(capi.VPT_RNG_PIXEL)
     log(f"[rank {rank}] grids ready in {time.time() - t0:.1f}s: {dens.leaf_count} leaves, "
         f"launch {it.launch_info()}")
 
@@ -194,7 +199,8 @@ def main():
                                    f"{'per GPU' if args.mode == 'weak' else 'per image'}, 8x8 tiles, seed {wl.cfg.seed}",
                        "width": wl.cfg.width, "height": wl.cfg.height, "spp": spp,
                        "jobs_per_step_per_gpu": jobs_rank, "volume": f"synthetic {wl.grid_n}^3 kind {wl.density_kind}",
-                       "parallelism": f"wave-sharded x{world} ({args.mode}), RCCL film all-reduce" if world > 1 else "1 GPU"},
+                       "parallelism": f"wave-sharded x{world} ({args.mode}), RCCL film all-reduce" if world > 1 else "1 GPU",
+                       "rng_mode": args.rng_mode},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": "vpt_integrate_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),

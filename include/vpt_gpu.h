@@ -224,6 +224,13 @@ int vpt_gpu_trace_jobs(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count,
 int vpt_gpu_majorant_trace(vpt_gpu_ctx* ctx, const float origin[3], const float direction[3],
                            float* rows_host, int max_rows, int* n_rows);
 
+/* Throughput mode.  VPT_RNG_REFERENCE (default): one pcg32_fast stream per job,
+ * hash(seed, jid), a job's pixels traced in order -- the reference's samples.  VPT_RNG_PIXEL: every
+ * pixel of a job is its own work item with stream hash(seed, jid * tile_area + pixel); it matches
+ * the reference only in expectation and is never used for parity. */
+enum { VPT_RNG_REFERENCE = 0, VPT_RNG_PIXEL = 1 };
+int vpt_gpu_set_rng_mode(vpt_gpu_ctx* ctx, int mode);
+
 int vpt_gpu_sync(vpt_gpu_ctx* ctx);
 /* Zero the context's own film. */
 int vpt_gpu_film_clear(vpt_gpu_ctx* ctx);

@@ -716,7 +716,7 @@ struct EventSink {
 };
 
 void run_job(const Scene& S, uint64_t jid, float* film, float* records, uint64_t record_base,
-             vpt_counters* cnt, EventSink* log = nullptr) {
+             vpt_counters* cnt, EventSink* log = nullptr, bool pixel_mode = false) {
   if (log) log->seq = 0;
   const vpt_configuration& cfg = *S.cfg;
   const vpt_worker_params& P = cfg.worker_parameters;
@@ -741,6 +741,8 @@ void run_job(const Scene& S, uint64_t jid, float* film, float* records, uint64_t
       if (P.single_pixel_enabled) {
         if (P.single_pixel_coord[0] != px || P.single_pixel_coord[1] != py) continue;
       }
+      // throughput mode (not the reference): one stream per pixel, hash(seed, jid * area + pixel)
+      if (pixel_mode) rng.begin_job(cfg.seed, jid * (uint64_t)(tw * th) + (uint64_t)(y * rw + x));
       float jx = rng.uniform();
       float jy = rng.uniform();
       if (cnt) cnt->rng_draws += 2;
@@ -1124,6 +1126,18 @@ int vpto_trace_segments(const vpto_grid* G, const float* o, const float* d, floa
     ++n;
   }
   return n;
+}
+
+int vpto_render_jobs_mode(const vpt_configuration* cfg, const vpto_grid* density, const vpto_grid* temperature,
+                          const float* bb_table, const float* cie, float y_integral, uint64_t jid_begin,
+                          uint64_t jid_count, int rng_mode, float* film, float* records) {
+  if (!cfg || !density || !film) return VPT_E_INVALID;
+  std::vector<float> bb(501 * 3, 0.0f);
+  if (bb_table) std::memcpy(bb.data(), bb_table, 500 * 3 * sizeof(float));
+  Scene S = make_scene(cfg, &density->g, temperature ? &temperature->g : nullptr, bb.data(), cie, y_integral);
+  for (uint64_t j = 0; j < jid_count; ++j)
+    run_job(S, jid_begin + j, film, records, j, nullptr, nullptr, rng_mode == VPT_RNG_PIXEL);
+  return VPT_OK;
 }
 
 int vpto_render_jobs_events(const vpt_configuration* cfg, const vpto_grid* density, const vpto_grid* temperature,

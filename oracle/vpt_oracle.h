@@ -63,6 +63,11 @@ int vpto_render_jobs(const vpt_configuration* cfg, const vpto_grid* density,
                      float y_integral, uint64_t jid_begin, uint64_t jid_count, float* film,
                      float* records, vpt_counters* counters);
 
+/* Same with an RNG mode (VPT_RNG_REFERENCE / VPT_RNG_PIXEL, see vpt_gpu_set_rng_mode). */
+int vpto_render_jobs_mode(const vpt_configuration* cfg, const vpto_grid* density,
+                          const vpto_grid* temperature, const float* bb_table, const float* cie,
+                          float y_integral, uint64_t jid_begin, uint64_t jid_count, int rng_mode,
+                          float* film, float* records);
 /* Same, logging every Logger event (worker.cpp:16-48) into events (capacity entries, in job order);
  * *count = events produced. */
 int vpto_render_jobs_events(const vpt_configuration* cfg, const vpto_grid* density,

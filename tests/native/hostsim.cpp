@@ -50,10 +50,11 @@ struct HostEnv {
 };
 }  // namespace
 
-extern "C" int vpths_render_jobs(const vpt_configuration* cfg, const vpt_grid_desc* density,
-                                 const vpt_grid_desc* temperature, const float* bb500, uint64_t jid_begin,
-                                 uint64_t jid_count, float* film, float* records, vpt_counters* counters) {
-  vpt::DevScene S;
+extern "C" int vpths_render_jobs_mode(const vpt_configuration* cfg, const vpt_grid_desc* density,
+                                      const vpt_grid_desc* temperature, const float* bb500, uint64_t jid_begin,
+                                      uint64_t jid_count, float* film, float* records, vpt_counters* counters,
+                                      int rng_mode) {
+  vpt::DevScene S{};
   int rc = vpt::build_scene(*cfg, S);
   if (rc) return rc;
   vpt::HostGrid hd, ht;
@@ -76,7 +77,9 @@ extern "C" int vpths_render_jobs(const vpt_configuration* cfg, const vpt_grid_de
   S.gate_idle = 1;
   S.gate_eval = 1;
   S.gate_walk = 1;  // exercise the inner walk loop
-  HostEnv env{jid_begin, jid_count, 0, film, records, S.tw * S.th};
+  S.pixel_mode = rng_mode == VPT_RNG_PIXEL ? 1 : 0;
+  S.tile_area = (uint32_t)(S.tw * S.th);
+  HostEnv env{jid_begin, S.pixel_mode ? jid_count * S.tile_area : jid_count, 0, film, records, S.tw * S.th};
   vpt::Lane ln;
   std::memset(&ln, 0, sizeof ln);
   vpt::lane_init(ln);
@@ -91,6 +94,13 @@ extern "C" int vpths_render_jobs(const vpt_configuration* cfg, const vpt_grid_de
     for (int k = 0; k < vpt::CNT_COUNT; ++k) o[k] += env.cnt[k];
   }
   return 0;
+}
+
+extern "C" int vpths_render_jobs(const vpt_configuration* cfg, const vpt_grid_desc* density,
+                                 const vpt_grid_desc* temperature, const float* bb500, uint64_t jid_begin,
+                                 uint64_t jid_count, float* film, float* records, vpt_counters* counters) {
+  return vpths_render_jobs_mode(cfg, density, temperature, bb500, jid_begin, jid_count, film, records, counters,
+                                VPT_RNG_REFERENCE);
 }
 
 // Leaf majorants after fix_majorants (product builder), for comparison with the oracle.

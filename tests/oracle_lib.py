@@ -67,6 +67,7 @@ def lib() -> C.CDLL:
     L.vpto_render_jobs_events.argtypes = [cfgp, vp, vp, fp, fp, C.c_float, C.c_uint64, C.c_uint64, fp, vp,
                                           C.c_uint64, C.POINTER(C.c_uint64)]
     L.vpto_majorant_trace.argtypes = [vp, fp, fp, fp, C.c_int]
+    L.vpto_render_jobs_mode.argtypes = [cfgp, vp, vp, fp, fp, C.c_float, C.c_uint64, C.c_uint64, C.c_int, fp, fp]
     L.vpto_majorant_trace.restype = C.c_int
     _L = L
     return L
@@ -187,3 +188,17 @@ def majorant_trace(density: OracleGrid, origin, direction, max_rows: int = 1 << 
     n = lib().vpto_majorant_trace(density.h, fptr(o), fptr(d), fptr(rows), max_rows)
     assert n <= max_rows
     return rows[:n].copy()
+
+
+def render_jobs_mode(cfg: Configuration, density: OracleGrid, temperature: OracleGrid | None, jid_begin: int,
+                     jid_count: int, rng_mode: int, records: bool = True):
+    cie, yint = load_cie()
+    bb = blackbody_table(cie, yint)
+    film = np.zeros((cfg.height, cfg.width, 4), np.float32)
+    tile_area = int(cfg.tile_size[0] * cfg.tile_size[1])
+    rec = np.full((jid_count * tile_area, 3), np.nan, np.float32) if records else None
+    rc = lib().vpto_render_jobs_mode(C.byref(cfg), density.h, temperature.h if temperature else None, fptr(bb),
+                                     fptr(cie), C.c_float(yint), jid_begin, jid_count, rng_mode, fptr(film),
+                                     fptr(rec) if rec is not None else None)
+    assert rc == 0
+    return film, rec

@@ -10,6 +10,7 @@ ap.add_argument("--gates", default="16:16")
 ap.add_argument("--blocks", default="0")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--profile", action="store_true")
+ap.add_argument("--rng-mode", default="reference")
 a = ap.parse_args()
 import torch
 from volume_path_tracer_amd.render import Integrator
@@ -18,6 +19,9 @@ wl = workload(a.config, spp=a.spp)
 dg = SynthGrid(wl.density_kind, wl.grid_n); tg = SynthGrid(2, wl.grid_n) if wl.temperature else None
 it = Integrator(wl.cfg, dg.grid(copy=False), tg.grid(copy=False) if tg else None)
 base_blocks = it.launch_info()[0]
+if a.rng_mode == "pixel":
+    from volume_path_tracer_amd import capi
+    it.set_rng_mode(capi.VPT_RNG_PIXEL)
 it.render_waves(1, 1); torch.cuda.synchronize()
 if a.profile:
     it.profile(reset=True)

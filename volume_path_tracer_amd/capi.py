@@ -91,6 +91,7 @@ class Counters(C.Structure):
 # vpt_event (include/vpt_gpu.h): one Logger line (src/worker.cpp:16-48)
 EVENT_DTYPE = np.dtype([("jid", "<u8"), ("pixel", "<u4"), ("seq", "<u4"), ("type", "<u4"), ("v", "<f4", (7,))])
 assert EVENT_DTYPE.itemsize == 48
+VPT_RNG_REFERENCE, VPT_RNG_PIXEL = 0, 1
 EVENT_NAMES = ("new_ray", "sampled_point", "null", "scatter_terminated", "scatter", "absorbed")
 
 
@@ -225,6 +226,7 @@ def lib() -> C.CDLL:
     L.vpt_film_to_srgb8.argtypes = [fp, C.c_int64, C.c_int64, C.POINTER(C.c_uint8)]
     L.vpt_gpu_trace_jobs.argtypes = [vp, C.c_uint64, C.c_uint64, vp, vp, C.c_uint64, C.POINTER(C.c_uint64), vp]
     L.vpt_gpu_majorant_trace.argtypes = [vp, fp, fp, fp, C.c_int, C.POINTER(C.c_int)]
+    L.vpt_gpu_set_rng_mode.argtypes = [vp, C.c_int]
     _lib = L
     return L
 

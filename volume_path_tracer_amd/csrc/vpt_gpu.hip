@@ -99,7 +99,7 @@ struct KernelEnv {
     if (slot >= event_cap) return;
     vpt_event* e = events + slot;
     e->jid = jid_begin + ln.jid_local;
-    e->pixel = (uint32_t)(ln.pix - 1);
+    e->pixel = (uint32_t)((ln.pix & kPixelMask) - 1);
     e->seq = seq;
     e->type = type;
     for (int i = 0; i < 3; ++i) {
@@ -269,9 +269,11 @@ constexpr int kProfWords = 2 * vpt::PB_COUNT + vpt::PT_COUNT;
 
 int ctx_device(vpt_gpu_ctx* ctx);
 
-// Device copy of the scene constants (between renders: a running kernel reads it).
+// Device copy of the scene constants (between renders: a running kernel reads it).  A pageable
+// hipMemcpy may return before its DMA lands, and the next render may run on another stream: wait.
 int push_scene(vpt_gpu_ctx* ctx) {
   VPT_HIP(hipMemcpy(ctx->scene_dev, &ctx->scene, sizeof(vpt::DevScene), hipMemcpyHostToDevice));
+  VPT_HIP(hipDeviceSynchronize());
   return VPT_OK;
 }
 
@@ -309,6 +311,10 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   vpt::KernelEnv env;
   env.jid_begin = jid_begin;
   env.jid_count = jid_count;
+  if (ctx->scene.pixel_mode) {  // work items are pixels
+    if (jid_count > UINT64_MAX / ctx->scene.tile_area) return vpt::set_error(VPT_E_INVALID, "render: job range too large");
+    env.jid_count = jid_count * ctx->scene.tile_area;
+  }
   env.job_counter = ctx->job_counter;
   env.film = film ? film : ctx->film;
   env.records = records;
@@ -401,6 +407,8 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   ctx->scene.gate_idle = 12;
   ctx->scene.gate_eval = 24;
   ctx->scene.gate_walk = 4;
+  ctx->scene.pixel_mode = 0;
+  ctx->scene.tile_area = (uint32_t)(ctx->scene.tw * ctx->scene.th);
   VPT_HIP(hipMalloc((void**)&ctx->scene_dev, sizeof(vpt::DevScene)));
   if ((rc = push_scene(ctx.get()))) return rc;
   *out = ctx.release();
@@ -468,6 +476,18 @@ int vpt_gpu_majorant_trace(vpt_gpu_ctx* ctx, const float origin[3], const float 
   if (e != hipSuccess) return vpt::set_error(VPT_E_HIP, std::string("vpt_gpu_majorant_trace: ") + hipGetErrorString(e));
   *n_rows = nn;
   return VPT_OK;
+}
+
+int vpt_gpu_set_rng_mode(vpt_gpu_ctx* ctx, int mode) {
+  if (!ctx || (mode != VPT_RNG_REFERENCE && mode != VPT_RNG_PIXEL))
+    return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_rng_mode: bad argument");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  if (mode == VPT_RNG_PIXEL && (int64_t)ctx->scene.tw * ctx->scene.th >= (int64_t)vpt::kPixelTaken)
+    return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_rng_mode: tile too large for the pixel mode");
+  ctx->scene.pixel_mode = mode == VPT_RNG_PIXEL ? 1 : 0;
+  ctx->scene.tile_area = (uint32_t)(ctx->scene.tw * ctx->scene.th);
+  return push_scene(ctx);
 }
 
 int vpt_gpu_sync(vpt_gpu_ctx* ctx) {

@@ -225,6 +225,10 @@ struct DevScene {
   int32_t gate_min, gate_idle;
   int32_t gate_eval;  // the density evaluation (trilinear + event) runs for >= gate_eval waiting lanes
   int32_t gate_walk;  // keep stepping in an inner loop while >= gate_walk lanes walk (0: one step)
+  // Throughput mode (VPT_RNG_PIXEL): the work item is one pixel of a job, its stream
+  // is hash(seed, jid * tile_area + pixel).  0 = the reference's per-job stream.
+  int32_t pixel_mode;
+  uint32_t tile_area;
   const float* bb;      // blackbody table [501][3] (row 500 = 0)
   const float* cie;     // [471][3] for T >= 49900 K
   float y_integral;
@@ -246,6 +250,12 @@ __host__ __device__ __forceinline__ uint64_t job_seed(uint64_t seed, uint64_t k)
   h ^= h >> 47;
   return h | 3ULL;  // pcg32_fast::seed: state = s | 3
 }
+// Lane::pix flags of a throughput-mode work item: trace only the pixel it names (kOnePixel), which
+// has been started (kPixelTaken); kPixelMask extracts the pixel counter.
+constexpr int32_t kOnePixel = 1 << 30;
+constexpr int32_t kPixelTaken = 1 << 29;
+constexpr int32_t kPixelMask = kPixelTaken - 1;
+
 __host__ __device__ __forceinline__ float rng_uniform(uint64_t& state) {
   uint64_t old = state;
   state = state * 6364136223846793005ULL;
@@ -697,7 +707,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       }
       // the pixel just traced is pix - 1 of the tile
       const int32_t rw = min(S.W - ln.x0, S.tw);
-      const int32_t q = ln.pix - 1, y = q / rw;
+      const int32_t q = (ln.pix & kPixelMask) - 1, y = q / rw;
       env.film_add(S, ln, ln.x0 + (q - y * rw), ln.y0 + y, rw);
       env.tally(CNT_SAMPLES, 1);
       ln.state = ST_PIXEL;
@@ -715,16 +725,21 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         ln.state = ST_DONE;
         return;
       }
+      uint32_t p = 0;
+      if (S.pixel_mode) {  // throughput mode: item = job * tile_area + pixel
+        p = (uint32_t)(j % S.tile_area);
+        j /= S.tile_area;
+      }
       if (Debug) {
         ln.jid_local = j;
         ln.n_events = 0;
       }
       uint64_t jid = env.jid_begin + j;
-      ln.rng = job_seed(S.seed, jid);
+      ln.rng = job_seed(S.seed, S.pixel_mode ? jid * S.tile_area + p : jid);
       uint64_t tile = jid % S.T;
       ln.x0 = (int32_t)(tile % S.ntx) * S.tw;  // TileProvider::compute_tile_rect
       ln.y0 = (int32_t)(tile / S.ntx) * S.th;
-      ln.pix = 0;
+      ln.pix = S.pixel_mode ? (int32_t)p | kOnePixel : 0;
       if (HasTemp) {
         ln.temp_cell.i = kNoCell;
         ln.temp_cell.code = -1;
@@ -744,15 +759,19 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       const int32_t rh = min(S.H - ln.y0, S.th);
       // Skip pixels filtered by single_pixel mode without any draw (worker.cpp:113-116).
       int32_t px, py;
+      const int32_t one = ln.pix & kOnePixel;
+      int32_t q = ln.pix & kPixelMask;
+      const int32_t end = one ? ((ln.pix & kPixelTaken) ? 0 : min(q + 1, rw * rh)) : rw * rh;
       while (true) {
-        if (ln.pix >= rw * rh) {
+        if (q >= end) {
           ln.state = ST_FETCH;
           return;
         }
-        int32_t y = ln.pix / rw;
-        px = ln.x0 + (ln.pix - y * rw);
+        int32_t y = q / rw;
+        px = ln.x0 + (q - y * rw);
         py = ln.y0 + y;
-        ++ln.pix;
+        ++q;
+        ln.pix = q | (one ? (kOnePixel | kPixelTaken) : 0);
         if (!S.single_pixel_enabled || (px == S.sp_x && py == S.sp_y)) break;
       }
       float jx = rng_uniform(ln.rng);

@@ -98,7 +98,7 @@ int build_scene(const vpt_configuration& cfg, DevScene& S) {
   const int64_t W = cfg.output_size[0], H = cfg.output_size[1];
   const int64_t tw = cfg.tile_size[0], th = cfg.tile_size[1];
   if (W <= 0 || H <= 0 || tw <= 0 || th <= 0) return set_error(VPT_E_INVALID, "output_size and tile_size must be positive");
-  if (W > (1 << 24) || H > (1 << 24) || tw > (1 << 16) || th > (1 << 16))
+  if (W > (1 << 24) || H > (1 << 24) || tw > (1 << 16) || th > (1 << 16) || tw * th >= (1 << 29))
     return set_error(VPT_E_INVALID, "output_size / tile_size too large");
   S.seed = cfg.seed;
   S.W = (int32_t)W;

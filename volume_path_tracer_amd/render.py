@@ -178,6 +178,11 @@ class Integrator:
             raise RuntimeError(f"majorant_trace: {n.value} segments exceed max_rows {max_rows}")
         return rows[: n.value].copy()
 
+    def set_rng_mode(self, mode: int) -> None:
+        """capi.VPT_RNG_REFERENCE (default, the reference's samples) or capi.VPT_RNG_PIXEL
+        (throughput mode: one stream per pixel; matches the reference only in expectation)."""
+        capi.check(capi.lib().vpt_gpu_set_rng_mode(self.h, int(mode)), "vpt_gpu_set_rng_mode")
+
     def counters(self, reset: bool = False) -> dict:
         c = capi.Counters()
         capi.check(capi.lib().vpt_gpu_counters(self.h, C.byref(c), 1 if reset else 0), "vpt_gpu_counters")
