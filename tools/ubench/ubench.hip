@@ -35,6 +35,8 @@ __global__ __launch_bounds__(256) void bench(uint32_t* out, uint32_t seed) {
       if (Op == 22) { asm volatile("v_max_f32 %0, %0, %4\n v_max_f32 %1, %1, %4\n v_max_f32 %2, %2, %4\n v_max_f32 %3, %3, %4" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3) : "v"(f0)); }
       if (Op == 23) { asm volatile("v_xor_b32 %0, %0, %4\n v_xor_b32 %1, %1, %4\n v_xor_b32 %2, %2, %4\n v_xor_b32 %3, %3, %4" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(seed)); }
       if (Op == 24) { asm volatile("v_pk_add_f32 %0, %0, %0\n v_pk_add_f32 %1, %1, %1\n v_pk_add_f32 %2, %2, %2\n v_pk_add_f32 %3, %3, %3" : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3)); }
+      if (Op == 25) { asm volatile("v_cndmask_b32_e64 %0, %0, %4, s[8:9]\n v_cndmask_b32_e64 %1, %1, %4, s[8:9]\n v_cndmask_b32_e64 %2, %2, %4, s[8:9]\n v_cndmask_b32_e64 %3, %3, %4, s[8:9]" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(seed) : "s8", "s9"); }
+      if (Op == 26) { asm volatile("v_cmp_lt_f32_e64 s[8:9], %0, %4\n v_cmp_lt_f32_e64 s[10:11], %1, %4\n v_cndmask_b32_e64 %2, %2, %4, s[8:9]\n v_cndmask_b32_e64 %3, %3, %4, s[10:11]" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3) : "v"(f0) : "s8", "s9", "s10", "s11"); }
       if (Op == 13) { asm volatile("v_cvt_f64_f32 %0, %4\n v_cvt_f64_f32 %1, %4\n v_cvt_f64_f32 %2, %4\n v_cvt_f64_f32 %3, %4" : "=v"(d0), "=v"(d1), "=v"(d2), "=v"(d3) : "v"(f0)); }
       if (Op == 3) { d0 = fma(d0, 0.999, 1e-3); d1 = fma(d1, 0.999, 1e-3); d2 = fma(d2, 0.999, 1e-3); d3 = fma(d3, 0.999, 1e-3); }
       if (Op == 4) { f0 = 1.0f / f0 + 0.5f; f1 = 1.0f / f1 + 0.5f; f2 = 1.0f / f2 + 0.5f; f3 = 1.0f / f3 + 0.5f; }
@@ -54,11 +56,11 @@ int main() {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  const char* names[] = {"v_add_f32(c)", "v_mul_lo_u32", "v_mad_u64_u32", "fma_f64(c)", "div_f32(cr)", "sqrt_f32(cr)", "logf_glibc_unit", "v_mul_u32_u24", "v_cvt_f32_u32", "v_mul_hi_u32", "v_rcp_f32", "v_add_f64", "v_add_f32(asm)", "v_cvt_f64_f32", "v_add_u32", "v_cndmask_b32", "v_cmp_lt_f32", "v_mul_f32", "v_fma_f32", "v_floor_f32", "v_and_b32", "v_mov_b32", "v_max_f32", "v_xor_b32", "v_pk_add_f32"};
-  void (*ks[])(uint32_t*, uint32_t) = {bench<0>, bench<1>, bench<2>, bench<3>, bench<4>, bench<5>, bench<6>, bench<7>, bench<8>, bench<9>, bench<10>, bench<11>, bench<12>, bench<13>, bench<14>, bench<15>, bench<16>, bench<17>, bench<18>, bench<19>, bench<20>, bench<21>, bench<22>, bench<23>, bench<24>};
+  const char* names[] = {"v_add_f32(c)", "v_mul_lo_u32", "v_mad_u64_u32", "fma_f64(c)", "div_f32(cr)", "sqrt_f32(cr)", "logf_glibc_unit", "v_mul_u32_u24", "v_cvt_f32_u32", "v_mul_hi_u32", "v_rcp_f32", "v_add_f64", "v_add_f32(asm)", "v_cvt_f64_f32", "v_add_u32", "v_cndmask_b32", "v_cmp_lt_f32", "v_mul_f32", "v_fma_f32", "v_floor_f32", "v_and_b32", "v_mov_b32", "v_max_f32", "v_xor_b32", "v_pk_add_f32", "v_cndmask_e64(sgpr)", "cmp+cndmask pairs"};
+  void (*ks[])(uint32_t*, uint32_t) = {bench<0>, bench<1>, bench<2>, bench<3>, bench<4>, bench<5>, bench<6>, bench<7>, bench<8>, bench<9>, bench<10>, bench<11>, bench<12>, bench<13>, bench<14>, bench<15>, bench<16>, bench<17>, bench<18>, bench<19>, bench<20>, bench<21>, bench<22>, bench<23>, bench<24>, bench<25>, bench<26>};
   const int blocks = 256 * 8;
   double base = 1;
-  for (int op = 0; op < 25; ++op) {
+  for (int op = 0; op < 27; ++op) {
     hipLaunchKernelGGL(ks[op], dim3(blocks), dim3(256), 0, 0, out, 1u);
     hipEventRecord(e0);
     hipLaunchKernelGGL(ks[op], dim3(blocks), dim3(256), 0, 0, out, 2u);

@@ -60,7 +60,7 @@ struct KernelEnv {
 
   // Adds w for every active lane with w != 0 (w uniform per call site) to a workgroup counter.
   __device__ __forceinline__ void tally(int32_t k, int32_t w) {
-    const unsigned long long m = __ballot(w != 0);
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(w != 0);
     if (m && __lane_id() == (uint32_t)__builtin_ctzll(m))
       atomicAdd(lds_counters + k, (unsigned long long)(__popcll(m) * (uint64_t)(w ? w : 1)));
   }
@@ -109,7 +109,8 @@ struct KernelEnv {
     e->v[6] = 0.0f;
   }
   // lanes of this wavefront for which pred holds
-  __device__ __forceinline__ int32_t count(bool pred) { return (int32_t)__popcll(__ballot(pred)); }
+  // (ballot_w64 on the bool itself: the compare folds into the mask, no materialised 0/1 VGPR)
+  __device__ __forceinline__ int32_t count(bool pred) { return (int32_t)__popcll(__builtin_amdgcn_ballot_w64(pred)); }
   __device__ __forceinline__ bool fetch_job(uint64_t& j) {
     unsigned long long v = atomicAdd(job_counter, 1ULL);
     if (v >= jid_count) return false;

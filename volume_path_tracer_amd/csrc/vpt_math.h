@@ -157,25 +157,55 @@ __host__ __device__ __forceinline__ float cosf_glibc(float y) {
   return sinf_poly(x * s, x * x, (n & 2) != 0, n ^ 1);
 }
 
-// RN(a / b) from y = RN(1 / b) with two fmas (Markstein's correction step):
-//   q = RN(a*y); r = a - q*b (exact, fma); RN(q + r*y) == RN(a/b)
-// for every pair of normal a, b whose quotient is normal -- checked exhaustively on MI355X over
-// all 2^46 significand pairs (tools/proofs/recip_div.hip; exponents scale exactly).  The caller
-// guarantees b in [2^-20, 2^20] (so y is normal); q outside [2^-100, 2^100] (this also catches
-// a = 0, inf, NaN, and keeps a normal) takes the correctly rounded division instead.
+// ---- exact short sequences for 1/x, sqrt(x) and a/b ------------------------------------------
+// The IEEE-correct f32 division and square root macros cost ~19 and ~22 v_add_f32 issue slots on
+// gfx950 (tools/ubench).  These produce the same bits with a few instructions inside the guarded
+// ranges, and fall back to the correct operation outside them:
+// * rcp_rn:  y0 = v_rcp_f32(x); RN(1/x) = fma(fma(-x, y0, 1), y0, y0) for every x with exponent
+//            field in [1, 252] (|x| in [2^-126, 2^126));
+// * sqrt_rn: y = v_rsq_f32(x); s = x*y; RN(sqrt x) = fma(fma(-s, s, x), 0.5*y, s) for every
+//            finite x >= 2^-101;
+//   both checked on MI355X over all 2^32 inputs (tools/proofs/rcp_sqrt.hip: 0 mismatches there);
+// * div_by_recip: Markstein's correction  q = RN(a*y); RN(a/b) = RN(q + fma(-q, b, a)*y)  with
+//   y = RN(1/b), exact for every pair of normal a, b with normal quotient -- checked over all 2^46
+//   significand pairs (tools/proofs/recip_div.hip).  Guard: b in [2^-26, 2^26) (via recip_for_div)
+//   and |q| in [2^-100, 2^100) keep a, y, q normal; otherwise the division runs.
+// Host builds use the plain operations (which these equal).
+__host__ __device__ __forceinline__ float rcp_rn(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (((as_u32(x) >> 23) & 0xffu) - 1u < 252u) {
+    const float y0 = __builtin_amdgcn_rcpf(x);
+    return __builtin_fmaf(__builtin_fmaf(-x, y0, 1.0f), y0, y0);
+  }
+#endif
+  return 1.0f / x;
+}
+__host__ __device__ __forceinline__ float sqrt_rn(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (as_u32(x) - 0x0d000000u < 0x7f800000u - 0x0d000000u) {  // finite, positive, >= 2^-101
+    const float y = __builtin_amdgcn_rsqf(x);
+    const float s = x * y;
+    return __builtin_fmaf(__builtin_fmaf(-s, s, x), 0.5f * y, s);
+  }
+#endif
+  return sqrtf(x);
+}
 __host__ __device__ __forceinline__ bool recip_div_ok(float q) {
   return (as_u32(q) & 0x7fffffffu) - 0x0d800000u < 0x64000000u;  // |q| in [2^-100, 2^100)
 }
+// RN(a / b), given y = recip_for_div(b).
 __host__ __device__ __forceinline__ float div_by_recip(float a, float b, float y) {
   const float q = a * y;
-  if (recip_div_ok(q)) return fmaf(fmaf(-q, b, a), y, q);
+  if (recip_div_ok(q)) return __builtin_fmaf(__builtin_fmaf(-q, b, a), y, q);
   return a / b;
 }
-// y = RN(1/b) when b is in [2^-20, 2^20] (div_by_recip's domain), else NaN (then every
+// y = RN(1/b) when |b| is in [2^-26, 2^26) (div_by_recip's domain), else NaN (then every
 // div_by_recip(a, b, y) takes the division).
 __host__ __device__ __forceinline__ float recip_for_div(float b) {
   const uint32_t e = (as_u32(b) >> 23) & 0xffu;
-  return (e >= 127u - 20u && e < 127u + 20u) ? 1.0f / b : __builtin_nanf("");
+  return (e - (127u - 26u) < 52u) ? rcp_rn(b) : __builtin_nanf("");
 }
+// RN(a / b) for any a, b.
+__host__ __device__ __forceinline__ float div_rn(float a, float b) { return div_by_recip(a, b, recip_for_div(b)); }
 }  // namespace math
 }  // namespace vpt
