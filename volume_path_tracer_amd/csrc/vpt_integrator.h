@@ -614,6 +614,99 @@ __host__ __device__ inline void scene_finalize(DevScene& S) {
   S.hg_num = inv_4_pi * (1.0f - g * g);
 }
 
+// A tentative collision at s_t0 (SM_EVAL): density, then the primary path's event
+// (worker.cpp:145-188) or the shadow ray's ratio-tracking update (worker.cpp:66-85).
+template <bool HasTemp, bool Debug, class Env>
+__host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const DevGrid& G, Lane& ln, Env& env) {
+  env.prof(PB_TRILINEAR);
+  const float t = ln.s_t0;
+  const float sigma_maj = ln.s_dmaj * S.sigma_t;
+  float pi_x = ln.e[0] + ln.d[0] * t, pi_y = ln.e[1] + ln.d[1] * t, pi_z = ln.e[2] + ln.d[2] * t;
+  float dens;
+  if (Debug) env.tally(CNT_DENSITY_EVALS, 1);
+  if (trilinear(G, ln.dens_cell, pi_x, pi_y, pi_z, dens)) ++ln.n_stencil;
+  ln.sm = SM_DRAW;  // density <= 0, a null event or an unkilled shadow ray: keep drawing
+  if (dens > 0.0f) {
+    float cp[3];
+    map_fwd(G, pi_x, pi_y, pi_z, cp[0], cp[1], cp[2]);
+    if (!ln.shadow) {
+      env.prof(PB_EVENT);
+      if (Debug) env.event(ln, VPT_EV_SAMPLED_POINT, cp, nullptr, dens);
+      // worker.cpp:148-188
+      float p_a = (S.sigma_a * dens) / sigma_maj;
+      float p_s = (S.sigma_s * dens) / sigma_maj;
+      float p_n = fmaxf(1.0f - p_a - p_s, 0.0f);
+      if (HasTemp) {
+        float tx, ty, tz, tadim, X, Y, Z;
+        map_inv(S.temperature, cp[0], cp[1], cp[2], tx, ty, tz);
+        env.tally(CNT_TEMP_STENCILS, trilinear(S.temperature, ln.temp_cell, tx, ty, tz, tadim) ? 1 : 0);
+        float tK = tadim * S.temp_scale + S.temp_offset;
+        blackbody_xyz(S, tK, X, Y, Z);
+        float sc = p_a * S.le_scale;
+        ln.L[0] = ln.L[0] + sc * X;
+        ln.L[1] = ln.L[1] + sc * Y;
+        ln.L[2] = ln.L[2] + sc * Z;
+      }
+      float ue = rng_uniform(ln.rng);
+      if (Debug) env.tally(CNT_RNG_DRAWS, 1);
+      // sample_discrete({Null p_n, Absorption p_a, Scatter p_s}, u) (random.hpp:30-47)
+      float total = ((0.0f + p_n) + p_a) + p_s;
+      float uu = ue * total;
+      int ev;
+      uu -= p_n;
+      if (uu <= 0) {
+        ev = 0;
+      } else {
+        uu -= p_a;
+        ev = (uu <= 0) ? 1 : 2;
+      }
+      if (ev == 1) {
+        if (Debug) env.event(ln, VPT_EV_ABSORBED, nullptr, nullptr, 0.0f);
+        ln.terminated = 1;
+        ln.state = ST_FINISH;
+      } else if (ev == 2) {
+        if (ln.depth++ >= S.max_depth) {
+          if (Debug) env.event(ln, VPT_EV_SCATTER_TERMINATED, nullptr, nullptr, 0.0f);
+          ln.terminated = 1;
+          ln.state = ST_FINISH;
+        } else {
+          if (Debug) env.tally(CNT_SCATTERS, 1);
+          // The next primary ray starts at the scatter point (worker.cpp:179): keep it in ro.
+          for (int i = 0; i < 3; ++i) ln.ro[i] = cp[i];
+          // sample_Ld (worker.cpp:52-90)
+          if (S.li_zero) {
+            ln.Tr = -1.0f;  // returns Li == 0 without draws
+            ln.state = ST_NEE_DONE;
+          } else {
+            ln.Tr = 1.0f;
+            ln.shadow = 1;
+            ln.state = ST_SHADOW;
+          }
+        }
+      }
+      // ev == 0 (Null): keep drawing in the same segment.
+      if (Debug && ev == 0) env.event(ln, VPT_EV_NULL, nullptr, nullptr, 0.0f);
+    } else {
+      env.prof(PB_SHADOW_HIT);
+      // Ratio tracking with Russian roulette (worker.cpp:68-85)
+      float sigma_n = fmaxf(0.0f, sigma_maj - S.sigma_t * dens);
+      ln.Tr *= sigma_n / sigma_maj;
+      if (ln.Tr <= 0.05f) {
+        float q = 0.75f;
+        if (Debug) env.tally(CNT_RNG_DRAWS, 1);
+        if (rng_uniform(ln.rng) < q)
+          ln.Tr = 0.0f;
+        else
+          ln.Tr /= 1 - q;
+      }
+      if (ln.Tr <= 0.0f) {
+        ln.Tr = -1.0f;  // returns Zero()
+        ln.state = ST_NEE_DONE;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // One iteration of the lane loop.  Env supplies fetch_job(uint64_t& jid_local) -> bool, jid_begin,
 // film_add(S, lane, px, py, rw).  HasTemp: the scene has a temperature grid (fire).
@@ -902,95 +995,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
     // short of lanes), so the stencil gathers and the event logic run on a fuller wavefront.
     const int32_t n_eval = env.count(ln.state == ST_SAMPLE && ln.sm == SM_EVAL);
     const bool run_eval = n_eval > 0 && (n_eval >= S.gate_eval || env.count(ln.state == ST_SAMPLE && ln.sm != SM_EVAL) < S.gate_idle);
-    if (run_eval && ln.state == ST_SAMPLE && ln.sm == SM_EVAL) {
-      env.prof(PB_TRILINEAR);
-      const float t = ln.s_t0;
-      const float sigma_maj = ln.s_dmaj * S.sigma_t;
-      float pi_x = ln.e[0] + ln.d[0] * t, pi_y = ln.e[1] + ln.d[1] * t, pi_z = ln.e[2] + ln.d[2] * t;
-      float dens;
-      if (Debug) env.tally(CNT_DENSITY_EVALS, 1);
-      if (trilinear(G, ln.dens_cell, pi_x, pi_y, pi_z, dens)) ++ln.n_stencil;
-      ln.sm = SM_DRAW;  // density <= 0, a null event or an unkilled shadow ray: keep drawing
-      if (dens > 0.0f) {
-        float cp[3];
-        map_fwd(G, pi_x, pi_y, pi_z, cp[0], cp[1], cp[2]);
-        if (!ln.shadow) {
-          env.prof(PB_EVENT);
-          if (Debug) env.event(ln, VPT_EV_SAMPLED_POINT, cp, nullptr, dens);
-          // worker.cpp:148-188
-          float p_a = (S.sigma_a * dens) / sigma_maj;
-          float p_s = (S.sigma_s * dens) / sigma_maj;
-          float p_n = fmaxf(1.0f - p_a - p_s, 0.0f);
-          if (HasTemp) {
-            float tx, ty, tz, tadim, X, Y, Z;
-            map_inv(S.temperature, cp[0], cp[1], cp[2], tx, ty, tz);
-            env.tally(CNT_TEMP_STENCILS, trilinear(S.temperature, ln.temp_cell, tx, ty, tz, tadim) ? 1 : 0);
-            float tK = tadim * S.temp_scale + S.temp_offset;
-            blackbody_xyz(S, tK, X, Y, Z);
-            float sc = p_a * S.le_scale;
-            ln.L[0] = ln.L[0] + sc * X;
-            ln.L[1] = ln.L[1] + sc * Y;
-            ln.L[2] = ln.L[2] + sc * Z;
-          }
-          float ue = rng_uniform(ln.rng);
-          if (Debug) env.tally(CNT_RNG_DRAWS, 1);
-          // sample_discrete({Null p_n, Absorption p_a, Scatter p_s}, u) (random.hpp:30-47)
-          float total = ((0.0f + p_n) + p_a) + p_s;
-          float uu = ue * total;
-          int ev;
-          uu -= p_n;
-          if (uu <= 0) {
-            ev = 0;
-          } else {
-            uu -= p_a;
-            ev = (uu <= 0) ? 1 : 2;
-          }
-          if (ev == 1) {
-            if (Debug) env.event(ln, VPT_EV_ABSORBED, nullptr, nullptr, 0.0f);
-            ln.terminated = 1;
-            ln.state = ST_FINISH;
-          } else if (ev == 2) {
-            if (ln.depth++ >= S.max_depth) {
-              if (Debug) env.event(ln, VPT_EV_SCATTER_TERMINATED, nullptr, nullptr, 0.0f);
-              ln.terminated = 1;
-              ln.state = ST_FINISH;
-            } else {
-              if (Debug) env.tally(CNT_SCATTERS, 1);
-              // The next primary ray starts at the scatter point (worker.cpp:179): keep it in ro.
-              for (int i = 0; i < 3; ++i) ln.ro[i] = cp[i];
-              // sample_Ld (worker.cpp:52-90)
-              if (S.li_zero) {
-                ln.Tr = -1.0f;  // returns Li == 0 without draws
-                ln.state = ST_NEE_DONE;
-              } else {
-                ln.Tr = 1.0f;
-                ln.shadow = 1;
-                ln.state = ST_SHADOW;
-              }
-            }
-          }
-          // ev == 0 (Null): keep drawing in the same segment.
-          if (Debug && ev == 0) env.event(ln, VPT_EV_NULL, nullptr, nullptr, 0.0f);
-        } else {
-          env.prof(PB_SHADOW_HIT);
-          // Ratio tracking with Russian roulette (worker.cpp:68-85)
-          float sigma_n = fmaxf(0.0f, sigma_maj - S.sigma_t * dens);
-          ln.Tr *= sigma_n / sigma_maj;
-          if (ln.Tr <= 0.05f) {
-            float q = 0.75f;
-            if (Debug) env.tally(CNT_RNG_DRAWS, 1);
-            if (rng_uniform(ln.rng) < q)
-              ln.Tr = 0.0f;
-            else
-              ln.Tr /= 1 - q;
-          }
-          if (ln.Tr <= 0.0f) {
-            ln.Tr = -1.0f;  // returns Zero()
-            ln.state = ST_NEE_DONE;
-          }
-        }
-      }
-    }
+    if (run_eval && ln.state == ST_SAMPLE && ln.sm == SM_EVAL) eval_collision<HasTemp, Debug>(S, G, ln, env);
   }
   env.tick(PT_EVAL);
 }
