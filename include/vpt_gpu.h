@@ -249,9 +249,9 @@ int vpt_gpu_counters(vpt_gpu_ctx* ctx, vpt_counters* out, int reset);
 int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_blocks, int gate_eval,
                        int gate_walk);
 /* SIMT-utilisation profile of profiling builds (-DVPT_PROFILE): for each block of the lane state
- * machine, [wave executions, active lanes] as 2*14 uint64, then the shader cycles the wavefronts
+ * machine, [wave executions, active lanes] as 2*21 uint64 (the last 7: lanes per state at each walk-loop iteration), then the shader cycles the wavefronts
  * spent in each of 10 sections (fetch, pixel, ray, walk-loop control, eval, nee, finish, and the
- * walk's segment / step / draw parts); zeros in normal builds.  n must be >= 2 * 14 + 10. */
+ * walk's segment / step / draw parts); zeros in normal builds.  n must be >= 2 * 21 + 10. */
 int vpt_gpu_profile(vpt_gpu_ctx* ctx, uint64_t* out, int n, int reset);
 /* Launch geometry used by the integrator kernel (for reports). */
 int vpt_gpu_launch_info(const vpt_gpu_ctx* ctx, int* grid_blocks, int* block_threads);

@@ -26,6 +26,7 @@ struct HostEnv {
   uint64_t cnt[vpt::CNT_COUNT] = {};
   void tally(int32_t k, int32_t w) { cnt[k] += (uint64_t)w; }
   void prof(int32_t) {}
+  void prof_add(int32_t, int32_t) {}
   void tick(int32_t) {}
   void event(vpt::Lane&, uint32_t, const float*, const float*, float) {}
   bool fetch_job(uint64_t& j) {

@@ -76,6 +76,19 @@ struct KernelEnv {
     (void)id;
 #endif
   }
+  // Adds n (wave-uniform) to slot id's lane total and 1 to its executions (VPT_PROFILE).
+  __device__ __forceinline__ void prof_add(int32_t id, int32_t n) {
+#ifdef VPT_PROFILE
+    const unsigned long long m = __ballot(1);
+    if ((__lane_id() == (uint32_t)__builtin_ctzll(m))) {
+      atomicAdd(prof_buf + 2 * id, 1ULL);
+      atomicAdd(prof_buf + 2 * id + 1, (unsigned long long)n);
+    }
+#else
+    (void)id;
+    (void)n;
+#endif
+  }
   // Wave time since the previous tick, charged to section id (first active lane; VPT_PROFILE).
   __device__ __forceinline__ void tick(int32_t id) {
 #if defined(VPT_PROFILE) || defined(VPT_PROFILE_TIME)

@@ -337,7 +337,9 @@ enum : int32_t { SM_NEED_SEG = 0, SM_STEP = 1, SM_DRAW = 2, SM_EVAL = 3 };  // S
 // Block ids for the optional SIMT-utilisation profile (env.prof; a no-op unless VPT_PROFILE).
 enum : int32_t {
   PB_ITER = 0, PB_FETCH, PB_PIXEL, PB_RAY, PB_SAMPLE, PB_NEED_SEG, PB_STEP, PB_DRAW, PB_TRILINEAR,
-  PB_EVENT, PB_SHADOW_HIT, PB_NONE, PB_NEE_DONE, PB_FINISH, PB_COUNT
+  PB_EVENT, PB_SHADOW_HIT, PB_NONE, PB_NEE_DONE, PB_FINISH,
+  // census of the wavefront at every walk-loop iteration (lanes per state)
+  PB_W_WALK, PB_W_EVAL, PB_W_NEE, PB_W_FIN, PB_W_RAY, PB_W_PIX, PB_W_DONE, PB_COUNT
 };
 // Section ids for the wave-time profile (env.tick: shader cycles since the previous tick, per
 // wavefront; gating ballots are charged to the section that follows them).
@@ -935,12 +937,26 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
     const DevScene S = *opaque(sp);
     const DevGrid& G = S.density;
     (void)G;
+#ifdef VPT_PROFILE
+    const int32_t c_nee = env.count(ln.state == ST_NEE_DONE), c_fin = env.count(ln.state == ST_FINISH),
+                  c_ray = env.count(ln.state == ST_RAY || ln.state == ST_SHADOW),
+                  c_pix = env.count(ln.state == ST_PIXEL || ln.state == ST_FETCH), c_done = 64 - env.count(true);
+#endif
     if (ln.state == ST_SAMPLE) {
       env.prof(PB_SAMPLE);
       // The walk (segment fetch, HDDA step, free-flight draw) loops here while enough lanes of the
       // wavefront are walking and too few wait on a density evaluation; the other states wait
       // (their gating counts them next outer iteration).  Each lane's own op order is unchanged.
       do {
+#ifdef VPT_PROFILE
+      env.prof_add(PB_W_WALK, env.count(ln.state == ST_SAMPLE && ln.sm != SM_EVAL));
+      env.prof_add(PB_W_EVAL, env.count(ln.state == ST_SAMPLE && ln.sm == SM_EVAL));
+      env.prof_add(PB_W_NEE, c_nee);
+      env.prof_add(PB_W_FIN, c_fin);
+      env.prof_add(PB_W_RAY, c_ray);
+      env.prof_add(PB_W_PIX, c_pix);
+      env.prof_add(PB_W_DONE, c_done);
+#endif
       if (ln.sm == SM_NEED_SEG) {
         env.prof(PB_NEED_SEG);
         // RayMajorantIterator::next prologue (volume.cpp:40-51)

@@ -194,15 +194,16 @@ class Integrator:
                    "vpt_gpu_set_tuning")
 
     PROFILE_BLOCKS = ["iter", "fetch", "pixel", "ray", "sample", "need_seg", "step", "draw", "trilinear",
-                      "event", "shadow_hit", "none", "nee_done", "finish"]
+                      "event", "shadow_hit", "none", "nee_done", "finish",
+                      "w_walk", "w_eval", "w_nee", "w_finish", "w_ray", "w_pixel", "w_done"]
 
     PROFILE_SECTIONS = ["fetch", "pixel", "ray", "walk", "eval", "nee", "finish", "seg", "step", "draw"]
 
     def profile(self, reset: bool = False) -> dict:
         """SIMT profile of a -DVPT_PROFILE build: {block: (wave executions, mean active lanes)} and
         {"cycles": {section: share of wave time}}."""
-        buf = (C.c_uint64 * 64)()
-        capi.check(capi.lib().vpt_gpu_profile(self.h, buf, 64, 1 if reset else 0), "vpt_gpu_profile")
+        buf = (C.c_uint64 * 128)()
+        capi.check(capi.lib().vpt_gpu_profile(self.h, buf, 128, 1 if reset else 0), "vpt_gpu_profile")
         out = {}
         for i, name in enumerate(self.PROFILE_BLOCKS):
             ex, lanes = int(buf[2 * i]), int(buf[2 * i + 1])
