@@ -32,3 +32,14 @@ def look_at(cfg, pos, look, up=(0.0, 1.0, 0.0)):
     cp.position[:] = [float(v) for v in pos]
     cp.look[:] = [float(v) for v in look]
     cp.up[:] = [float(v) for v in up]
+
+
+def tiles_only_grid() -> capi.Grid:
+    """No leaves at all: an active upper-node tile, an active root tile and a lower-node tile
+    (so every HDDA dim occurs and the leaf-slot table holds only tiles)."""
+    return capi.Grid(map_mat=[1, 0, 0, 0, 1, 0, 0, 0, 1], map_inv_mat=[1, 0, 0, 0, 1, 0, 0, 0, 1],
+                     map_vec=[-64.0, -64.0, -64.0], background=0.0, bbox_min=[0, 0, 0], bbox_max=[4095, 255, 255],
+                     leaf_origin=np.zeros((0, 3), np.int32), leaf_values=np.zeros((0, 512), np.float32),
+                     leaf_max=np.zeros(0, np.float32),
+                     tile_origin=[[0, 0, 0], [128, 0, 0], [0, 128, 8], [4096, 0, 0]],
+                     tile_level=[2, 2, 1, 3], tile_value=[0.02, 0.0, 0.5, 0.01], tile_active=[1, 0, 1, 1])

@@ -141,3 +141,51 @@ def test_gpu_film_rmse_within_north_star():
     x_g, x_o = f_g[..., :3] / f_g[..., 3:], f_o[..., :3] / f_o[..., 3:]
     rmse = float(np.sqrt(np.mean((x_g.astype(np.float64) - x_o) ** 2)))
     assert rmse < 1e-4, rmse
+
+
+def _records_equal(wl, dens, temp, jid_begin, count):
+    from volume_path_tracer_amd.render import Integrator
+
+    it = Integrator(wl.cfg, dens, temp, device=0)
+    f_g, r_g = _gpu_records(it, jid_begin, count)
+    f_o, r_o, c_o = _oracle(wl, dens, temp, jid_begin, count)
+    assert r_g.tobytes() == r_o.tobytes()
+    np.testing.assert_array_equal(f_g[..., 3], f_o[..., 3])
+    return c_o
+
+
+@pytest.mark.parametrize("case", ["tiles_only", "tiny_image", "odd_tiles", "no_jitter_single_pixel",
+                                  "unaligned_jobs", "max_depth_0", "beyond_num_waves"])
+def test_gpu_edge_cases_bit_exact(case):
+    """Edge cases of the reference loop (worker.cpp:104-207) and of the tile/job mapping."""
+    from grids import look_at, tiles_only_grid
+
+    wl = workload("c3", width=24, height=16, spp=2, grid_n=64)
+    dens = SynthGrid(1, 64).grid()
+    begin, count = 0, None
+    if case == "tiles_only":
+        dens = tiles_only_grid()
+        look_at(wl.cfg, (-500.0, 30.0, -300.0), (500.0, 30.0, 60.0))
+    elif case == "tiny_image":
+        wl.cfg.output_size[0], wl.cfg.output_size[1] = 5, 3
+    elif case == "odd_tiles":
+        wl.cfg.output_size[0], wl.cfg.output_size[1] = 37, 23
+        wl.cfg.tile_size[0], wl.cfg.tile_size[1] = 16, 3
+    elif case == "no_jitter_single_pixel":
+        wp = wl.cfg.worker_parameters
+        wp.use_jitter = 0
+        wp.single_pixel_enabled = 1
+        wp.single_pixel_coord[0], wp.single_pixel_coord[1] = 11, 7
+    elif case == "unaligned_jobs":
+        begin, count = 7, 29
+    elif case == "max_depth_0":
+        wl.cfg.worker_parameters.max_depth = 0
+    elif case == "beyond_num_waves":
+        begin = wl.cfg.jobs_per_wave() * 5  # jobs past num_waves are valid jids (waves 6, 7)
+    if count is None:
+        count = wl.cfg.jobs_per_wave() * 2
+    c = _records_equal(wl, dens, None, begin, count)
+    if case == "max_depth_0":
+        assert c["draws"] == 0 and c["scatters"] == 0
+    if case == "tiles_only":
+        assert c["draws"] > 0

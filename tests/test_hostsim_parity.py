@@ -71,3 +71,18 @@ def test_sparse_grid_all_hdda_levels():
         assert c_o[k] == c_h[k], k
     # the scene is not trivially empty: many rays hit volume
     assert c_o["density_evals"] > 1000 and c_o["dda_steps"] > 5 * c_o["samples"]
+
+
+def test_tiles_only_grid():
+    """A grid without leaves (upper/root/lower-node tiles only) through the device state machine."""
+    from grids import look_at, tiles_only_grid
+
+    dens = tiles_only_grid()
+    wl = workload("c3", width=24, height=16, spp=2)
+    look_at(wl.cfg, (-500.0, 30.0, -300.0), (500.0, 30.0, 60.0))
+    od = O.OracleGrid(dens, fix_majorants=True)
+    jobs = wl.cfg.jobs_per_wave() * 2
+    f_o, r_o, c_o = O.render_jobs(wl.cfg, od, None, 0, jobs, records=True)
+    f_h, r_h, c_h = HS.render_jobs(wl.cfg, dens, None, 0, jobs, records=True)
+    assert r_o.tobytes() == r_h.tobytes()
+    assert c_o["draws"] > 0 and c_o["draws"] == c_h["draws"]
