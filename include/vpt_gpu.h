@@ -231,6 +231,23 @@ int vpt_gpu_majorant_trace(vpt_gpu_ctx* ctx, const float origin[3], const float 
 enum { VPT_RNG_REFERENCE = 0, VPT_RNG_PIXEL = 1 };
 int vpt_gpu_set_rng_mode(vpt_gpu_ctx* ctx, int mode);
 
+/* Scheduling order of a whole-wave job range (jid_begin and jid_count multiples of T).  Results
+ * never depend on it: every job keeps its jid and RNG stream, only the fp32 atomic film-add order
+ * changes.  VPT_ORDER_JID: jid order, as TileProvider::next() hands jobs out.
+ * VPT_ORDER_COST_WAVE_MAJOR: wave by wave, each wave's tiles costliest first.
+ * VPT_ORDER_COST_TILE_MAJOR: the whole range as one costliest-first list -- tiles ranked by cost in
+ * groups of 64, each group's waves consecutively (64 lanes = 64 tiles of one wave).
+ * VPT_ORDER_COST_TAIL (default): wave-major, then the last ~6 x (resident lanes / T) waves
+ * tile-major, so the launch drains on cheap (sky) jobs without concentrating the whole launch on
+ * the densest tiles.  Costs: vpt_gpu_tile_costs.  Other ranges run in jid order. */
+enum { VPT_ORDER_JID = 0, VPT_ORDER_COST_WAVE_MAJOR = 1, VPT_ORDER_COST_TILE_MAJOR = 2, VPT_ORDER_COST_TAIL = 3 };
+int vpt_gpu_set_job_order(vpt_gpu_ctx* ctx, int mode);
+/* VPT_ORDER_COST_TAIL's tile-major wave count (0 = auto: 6 x resident lanes / T, rounded up). */
+int vpt_gpu_set_job_order_tail(vpt_gpu_ctx* ctx, int waves);
+/* The per-tile cost estimates (float[T], may be NULL) and the tile ranks by descending cost
+ * (uint32[T], may be NULL): HDDA steps + 4 x majorant optical depth of 5 primary rays per tile. */
+int vpt_gpu_tile_costs(vpt_gpu_ctx* ctx, float* cost_T, uint32_t* rank_T);
+
 int vpt_gpu_sync(vpt_gpu_ctx* ctx);
 /* Zero the context's own film. */
 int vpt_gpu_film_clear(vpt_gpu_ctx* ctx);

@@ -24,6 +24,8 @@ def lib():
         L.vpths_fixed_leaf_max.argtypes = [gp, fp]
         L.vpths_render_jobs_mode.argtypes = [cfgp, gp, gp, fp, C.c_uint64, C.c_uint64, fp, fp, C.POINTER(Counters),
                                              C.c_int]
+        L.vpths_render_jobs_order.argtypes = [cfgp, gp, gp, fp, C.c_uint64, C.c_uint64, fp, fp,
+                                              C.POINTER(Counters), C.c_int, C.POINTER(C.c_uint32), C.c_int]
         L.vpths_probe.argtypes = [gp, C.POINTER(C.c_int32), C.c_int, fp, C.POINTER(C.c_int32), fp]
         L.vpths_math_mismatches.argtypes = [C.c_int]
         L.vpths_math_mismatches.restype = C.c_int64
@@ -36,14 +38,22 @@ def fptr(a):
     return None if a is None else a.ctypes.data_as(C.POINTER(C.c_float))
 
 
-def render_jobs(cfg, density, temperature, jid_begin, jid_count, records=False, bb=None, rng_mode=0):
+def render_jobs(cfg, density, temperature, jid_begin, jid_count, records=False, bb=None, rng_mode=0, order=None,
+                tail_waves=0):
+    """order: tile ranks (uint32[T]) for a whole-wave range, taken in the GPU's job-order mapping
+    (ordered_job) with the last tail_waves waves tile-major."""
     film = np.zeros((cfg.height, cfg.width, 4), np.float32)
     tile_area = int(cfg.tile_size[0] * cfg.tile_size[1])
     rec = np.full((jid_count * tile_area, 3), np.nan, np.float32) if records else None
     cnt = Counters()
-    rc = lib().vpths_render_jobs_mode(C.byref(cfg), C.byref(density.desc),
-                                      C.byref(temperature.desc) if temperature is not None else None,
-                                      fptr(bb), jid_begin, jid_count, fptr(film), fptr(rec), C.byref(cnt), rng_mode)
+    op = None
+    if order is not None:
+        order = np.ascontiguousarray(order, np.uint32)
+        op = order.ctypes.data_as(C.POINTER(C.c_uint32))
+    rc = lib().vpths_render_jobs_order(C.byref(cfg), C.byref(density.desc),
+                                       C.byref(temperature.desc) if temperature is not None else None,
+                                       fptr(bb), jid_begin, jid_count, fptr(film), fptr(rec), C.byref(cnt), rng_mode,
+                                       op, int(tail_waves))
     assert rc == 0
     return film, rec, cnt.as_dict()
 

@@ -22,6 +22,9 @@ struct HostEnv {
   float* film;
   float* records;
   int32_t tile_area;
+  const uint32_t* order = nullptr;  // job order (see vpt_integrator.h ST_FETCH)
+  uint32_t order_tail_k0 = 0;
+  uint32_t order_tail_n = 0;
   int32_t count(bool pred) { return pred ? 1 : 0; }  // one lane
   uint64_t cnt[vpt::CNT_COUNT] = {};
   void tally(int32_t k, int32_t w) { cnt[k] += (uint64_t)w; }
@@ -51,10 +54,12 @@ struct HostEnv {
 };
 }  // namespace
 
-extern "C" int vpths_render_jobs_mode(const vpt_configuration* cfg, const vpt_grid_desc* density,
-                                      const vpt_grid_desc* temperature, const float* bb500, uint64_t jid_begin,
-                                      uint64_t jid_count, float* film, float* records, vpt_counters* counters,
-                                      int rng_mode) {
+// order != nullptr: [jid_begin, jid_begin + jid_count) is whole waves and items are taken in the
+// kernel's cost order (order = tile ranks; the last tail_waves waves tile-major, see ordered_job).
+extern "C" int vpths_render_jobs_order(const vpt_configuration* cfg, const vpt_grid_desc* density,
+                                       const vpt_grid_desc* temperature, const float* bb500, uint64_t jid_begin,
+                                       uint64_t jid_count, float* film, float* records, vpt_counters* counters,
+                                       int rng_mode, const uint32_t* order, int tail_waves) {
   vpt::DevScene S{};
   int rc = vpt::build_scene(*cfg, S);
   if (rc) return rc;
@@ -81,6 +86,11 @@ extern "C" int vpths_render_jobs_mode(const vpt_configuration* cfg, const vpt_gr
   S.pixel_mode = rng_mode == VPT_RNG_PIXEL ? 1 : 0;
   S.tile_area = (uint32_t)(S.tw * S.th);
   HostEnv env{jid_begin, S.pixel_mode ? jid_count * S.tile_area : jid_count, 0, film, records, S.tw * S.th};
+  if (order) {
+    env.order = order;
+    env.order_tail_n = (uint32_t)tail_waves;
+    env.order_tail_k0 = (uint32_t)(jid_count - (uint64_t)tail_waves * S.T);
+  }
   vpt::Lane ln;
   std::memset(&ln, 0, sizeof ln);
   vpt::lane_init(ln);
@@ -95,6 +105,14 @@ extern "C" int vpths_render_jobs_mode(const vpt_configuration* cfg, const vpt_gr
     for (int k = 0; k < vpt::CNT_COUNT; ++k) o[k] += env.cnt[k];
   }
   return 0;
+}
+
+extern "C" int vpths_render_jobs_mode(const vpt_configuration* cfg, const vpt_grid_desc* density,
+                                      const vpt_grid_desc* temperature, const float* bb500, uint64_t jid_begin,
+                                      uint64_t jid_count, float* film, float* records, vpt_counters* counters,
+                                      int rng_mode) {
+  return vpths_render_jobs_order(cfg, density, temperature, bb500, jid_begin, jid_count, film, records, counters,
+                                 rng_mode, nullptr, 0);
 }
 
 extern "C" int vpths_render_jobs(const vpt_configuration* cfg, const vpt_grid_desc* density,

@@ -189,3 +189,22 @@ def test_gpu_edge_cases_bit_exact(case):
         assert c["draws"] == 0 and c["scatters"] == 0
     if case == "tiles_only":
         assert c["draws"] > 0
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_gpu_job_order_modes_bit_exact(mode):
+    """Every scheduling order renders the same samples (records keyed by jid) as the oracle."""
+    from volume_path_tracer_amd import capi
+
+    wl = workload("c3", width=48, height=40, spp=3, grid_n=64)
+    it, dens, temp = _integrator(wl)
+    it.set_job_order(mode)
+    T = wl.cfg.jobs_per_wave()
+    f_g, r_g = _gpu_records(it, T, 2 * T)  # waves 2..3: a whole-wave range not starting at 0
+    f_o, r_o, c_o = _oracle(wl, dens, temp, T, 2 * T)
+    assert r_g.tobytes() == r_o.tobytes()
+    np.testing.assert_array_equal(f_g[..., 3], f_o[..., 3])
+    np.testing.assert_allclose(f_g[..., :3], f_o[..., :3], rtol=1e-5, atol=1e-6)
+    cost, rank = it.tile_costs()
+    assert sorted(rank.tolist()) == list(range(T))
+    assert np.all(np.diff(cost[rank]) <= 0) and cost.max() > 0 and capi.VPT_ORDER_COST_TAIL == 3

@@ -86,3 +86,22 @@ def test_tiles_only_grid():
     f_h, r_h, c_h = HS.render_jobs(wl.cfg, dens, None, 0, jobs, records=True)
     assert r_o.tobytes() == r_h.tobytes()
     assert c_o["draws"] > 0 and c_o["draws"] == c_h["draws"]
+
+
+@pytest.mark.parametrize("tail_waves", [0, 1, 3])
+@pytest.mark.parametrize("size", [(40, 24), (80, 72), (64, 64)])
+def test_job_order_permutation_keeps_samples(tail_waves, size):
+    """The kernel's cost-ordered scheduling (vpt_gpu_set_job_order) maps items onto the same jobs:
+    with any tile ranking, every sample (keyed by its jid) is bit-identical to jid order.
+    Tiles per wave: 15 (< one 64-tile group), 90 (one group + a ragged one), 64 (exactly one)."""
+    wl = workload("c3", width=size[0], height=size[1], spp=3, grid_n=64)
+    dens = SynthGrid(1, 64).grid()
+    T = wl.cfg.jobs_per_wave()
+    jobs = T * 3
+    order = np.random.default_rng(5).permutation(T).astype(np.uint32)
+    f_a, r_a, c_a = HS.render_jobs(wl.cfg, dens, None, T, jobs, records=True)
+    f_b, r_b, c_b = HS.render_jobs(wl.cfg, dens, None, T, jobs, records=True, order=order, tail_waves=tail_waves)
+    assert r_a.tobytes() == r_b.tobytes()
+    np.testing.assert_array_equal(f_a[..., 3], f_b[..., 3])
+    np.testing.assert_allclose(f_a[..., :3], f_b[..., :3], rtol=1e-5, atol=1e-6)
+    assert c_a == c_b

@@ -11,6 +11,8 @@ ap.add_argument("--blocks", default="0")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--profile", action="store_true")
 ap.add_argument("--rng-mode", default="reference")
+ap.add_argument("--order", type=int, default=-1, help="job order mode (-1: library default)")
+ap.add_argument("--tail", type=int, default=0, help="VPT_ORDER_COST_TAIL tile-major waves (0: auto)")
 a = ap.parse_args()
 import torch
 from volume_path_tracer_amd.render import Integrator
@@ -22,6 +24,9 @@ base_blocks = it.launch_info()[0]
 if a.rng_mode == "pixel":
     from volume_path_tracer_amd import capi
     it.set_rng_mode(capi.VPT_RNG_PIXEL)
+if a.order >= 0:
+    it.set_job_order(a.order)
+it.set_job_order_tail(a.tail)
 it.render_waves(1, 1); torch.cuda.synchronize()
 if a.profile:
     it.profile(reset=True)
@@ -41,5 +46,5 @@ for g in a.gates.split(","):
         if a.profile:
             prof = it.profile(reset=True)
             print(json.dumps({"gate": g, "profile": prof}), flush=True)
-        print(json.dumps({"lib": os.environ.get("VPT_LIB", "default"), "gate": g, "blocks": b or base_blocks,
+        print(json.dumps({"lib": os.environ.get("VPT_LIB", "default"), "order": a.order, "tail": a.tail, "gate": g, "blocks": b or base_blocks,
                           "spp": a.spp, "ms": round(ms, 2), "Msps": round(wl.cfg.width * wl.cfg.height * a.spp / best / 1e6, 2)}), flush=True)

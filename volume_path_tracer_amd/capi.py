@@ -92,6 +92,7 @@ class Counters(C.Structure):
 EVENT_DTYPE = np.dtype([("jid", "<u8"), ("pixel", "<u4"), ("seq", "<u4"), ("type", "<u4"), ("v", "<f4", (7,))])
 assert EVENT_DTYPE.itemsize == 48
 VPT_RNG_REFERENCE, VPT_RNG_PIXEL = 0, 1
+VPT_ORDER_JID, VPT_ORDER_COST_WAVE_MAJOR, VPT_ORDER_COST_TILE_MAJOR, VPT_ORDER_COST_TAIL = 0, 1, 2, 3
 EVENT_NAMES = ("new_ray", "sampled_point", "null", "scatter_terminated", "scatter", "absorbed")
 
 
@@ -227,6 +228,9 @@ def lib() -> C.CDLL:
     L.vpt_gpu_trace_jobs.argtypes = [vp, C.c_uint64, C.c_uint64, vp, vp, C.c_uint64, C.POINTER(C.c_uint64), vp]
     L.vpt_gpu_majorant_trace.argtypes = [vp, fp, fp, fp, C.c_int, C.POINTER(C.c_int)]
     L.vpt_gpu_set_rng_mode.argtypes = [vp, C.c_int]
+    L.vpt_gpu_set_job_order.argtypes = [vp, C.c_int]
+    L.vpt_gpu_set_job_order_tail.argtypes = [vp, C.c_int]
+    L.vpt_gpu_tile_costs.argtypes = [vp, fp, C.POINTER(C.c_uint32)]
     _lib = L
     return L
 

@@ -54,6 +54,9 @@ struct KernelEnv {
   unsigned long long* prof_buf;  // [PB_COUNT][2] wave executions, active lanes; then [PT_COUNT] cycles
   unsigned long long* lds_prof;  // this workgroup's section cycles (LDS, VPT_PROFILE builds)
   unsigned long long* lds_counters;  // this workgroup's event counters (LDS)
+  const uint32_t* order;             // job order: tile ranks (nullptr = jid order), see ordered_job
+  uint32_t order_tail_k0;
+  uint32_t order_tail_n;
   vpt_event* events;                 // Logger events (trace launches only)
   unsigned long long* event_count;
   uint64_t event_cap;
@@ -217,6 +220,44 @@ __global__ void vpt_majorant_trace_kernel(const DevScene* scene, float ox, float
   *n_rows = n;
 }
 
+// Cost estimate of every tile for the job order (vpt_gpu_set_job_order): the primary rays through
+// the tile's centre and its four quadrant centres, each costed as HDDA steps + 4 x the majorant
+// optical depth (expected free-flight draws).  Only the scheduling order depends on it.
+__global__ void vpt_tile_cost_kernel(const DevScene* scene, float* cost) {
+  const DevScene& S = *scene;
+  const uint64_t tile = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tile >= S.T) return;
+  const DevGrid& G = S.density;
+  const int32_t x0 = (int32_t)(tile % S.ntx) * S.tw, y0 = (int32_t)(tile / S.ntx) * S.th;
+  const float rw = (float)min(S.W - x0, S.tw), rh = (float)min(S.H - y0, S.th);
+  const float fx[5] = {0.5f, 0.25f, 0.75f, 0.25f, 0.75f}, fy[5] = {0.5f, 0.25f, 0.25f, 0.75f, 0.75f};
+  float c = 0.0f;
+  for (int r = 0; r < 5; ++r) {
+    const float rx = (float)x0 + fx[r] * rw, ry = (float)y0 + fy[r] * rh;
+    float dv[3];
+    for (int i = 0; i < 3; ++i) dv[i] = S.cam_t[i] + (S.cam_L[i * 3] * rx + S.cam_L[i * 3 + 1] * ry);
+    const float n = sqrtf(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2]);
+    if (!(n > 0.0f)) continue;
+    for (int i = 0; i < 3; ++i) dv[i] /= n;
+    Lane ln;
+    lane_init(ln);
+    if (!begin_ray(G, ln, S.cam_pos, ray_dir_setup(G, dv))) continue;
+    int steps = 0;
+    float tau = 0.0f;
+    while (ln.T0 < ln.T1 && steps < (1 << 16)) {
+      ln.s_t0 = ln.T0;
+      bool done;
+      do {
+        ++steps;
+        done = hdda_step(G, ln);
+      } while (!done && steps < (1 << 16));
+      tau += S.sigma_t * ln.s_dmaj * (ln.s_t1 - ln.s_t0) * ln.scale;
+    }
+    c += (float)steps + 4.0f * tau;
+  }
+  cost[tile] = c;
+}
+
 // ------------------------------------------------------------------------------------------------
 struct DeviceGrid {
   void* cells8 = nullptr;
@@ -275,6 +316,11 @@ struct vpt_gpu_ctx {
   vpt::DevScene* scene_dev = nullptr;  // the kernel's copy of scene (read through ScenePtr)
   hipStream_t stream = nullptr;
   int grid_blocks = 0;
+  int order_mode = VPT_ORDER_COST_TAIL;
+  int order_tail_waves = 0;        // VPT_ORDER_COST_TAIL: tile-major waves (0 = auto)
+  uint32_t* order = nullptr;       // tile ranks by descending cost (device), built on first use
+  std::vector<float> tile_cost;    // host copy of the estimates
+  std::vector<uint32_t> tile_rank;
 };
 
 namespace {
@@ -309,8 +355,37 @@ void destroy(vpt_gpu_ctx* ctx) {
   (void)hipFree(ctx->counters);
   (void)hipFree(ctx->prof);
   (void)hipFree(ctx->scene_dev);
+  (void)hipFree(ctx->order);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
+}
+
+// Tile costs (vpt_tile_cost_kernel) and the descending-cost tile ranks, once per context.
+int ensure_order(vpt_gpu_ctx* ctx) {
+  if (ctx->order) return VPT_OK;
+  const uint64_t T = ctx->scene.T;
+  float* cost = nullptr;
+  VPT_HIP(hipMalloc((void**)&cost, T * sizeof(float)));
+  hipLaunchKernelGGL(vpt::vpt_tile_cost_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, nullptr,
+                     ctx->scene_dev, cost);
+  ctx->tile_cost.assign(T, 0.0f);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpy(ctx->tile_cost.data(), cost, T * sizeof(float), hipMemcpyDeviceToHost);
+  (void)hipFree(cost);
+  if (e != hipSuccess) return vpt::set_error(VPT_E_HIP, std::string("tile cost pass: ") + hipGetErrorString(e));
+  ctx->tile_rank.resize(T);
+  for (uint64_t i = 0; i < T; ++i) ctx->tile_rank[i] = (uint32_t)i;
+  std::stable_sort(ctx->tile_rank.begin(), ctx->tile_rank.end(),
+                   [&](uint32_t a, uint32_t b) { return ctx->tile_cost[a] > ctx->tile_cost[b]; });
+  uint32_t* d = nullptr;
+  VPT_HIP(hipMalloc((void**)&d, T * sizeof(uint32_t)));
+  e = hipMemcpy(d, ctx->tile_rank.data(), T * sizeof(uint32_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(d);
+    return vpt::set_error(VPT_E_HIP, std::string("tile order upload: ") + hipGetErrorString(e));
+  }
+  ctx->order = d;
+  return VPT_OK;
 }
 
 int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film, float* records, void* stream_ptr,
@@ -334,6 +409,26 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.records = records;
   env.tile_area = ctx->scene.tw * ctx->scene.th;
   env.prof_buf = ctx->prof;
+  env.order = nullptr;
+  env.order_tail_k0 = 0;
+  env.order_tail_n = 0;
+  const uint64_t T = ctx->scene.T;
+  if (ctx->order_mode != VPT_ORDER_JID && jid_begin % T == 0 && jid_count % T == 0 && jid_count < (1ULL << 32)) {
+    // whole waves: take the jobs in cost order (same jobs, same samples)
+    if ((rc = ensure_order(ctx))) return rc;
+    const uint32_t n = (uint32_t)(jid_count / T);
+    uint32_t tail = 0;  // VPT_ORDER_COST_WAVE_MAJOR
+    if (ctx->order_mode == VPT_ORDER_COST_TILE_MAJOR) tail = n;
+    if (ctx->order_mode == VPT_ORDER_COST_TAIL) {
+      // the last ~6 x (resident lanes / T) waves (C3: 61 of 256): measured best of 2x..16x
+      const uint64_t lanes = (uint64_t)ctx->grid_blocks * vpt::kBlockThreads;
+      const uint64_t want = ctx->order_tail_waves > 0 ? (uint64_t)ctx->order_tail_waves : (6 * lanes + T - 1) / T;
+      tail = (uint32_t)std::min<uint64_t>(n, want);
+    }
+    env.order = ctx->order;
+    env.order_tail_n = tail;
+    env.order_tail_k0 = (n - tail) * (uint32_t)T;
+  }
   env.events = events;
   env.event_count = ctx->job_counter + 1;
   env.event_cap = event_cap;
@@ -502,6 +597,29 @@ int vpt_gpu_set_rng_mode(vpt_gpu_ctx* ctx, int mode) {
   ctx->scene.pixel_mode = mode == VPT_RNG_PIXEL ? 1 : 0;
   ctx->scene.tile_area = (uint32_t)(ctx->scene.tw * ctx->scene.th);
   return push_scene(ctx);
+}
+
+int vpt_gpu_set_job_order(vpt_gpu_ctx* ctx, int mode) {
+  if (!ctx || mode < VPT_ORDER_JID || mode > VPT_ORDER_COST_TAIL)
+    return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_job_order: bad argument");
+  ctx->order_mode = mode;
+  return VPT_OK;
+}
+
+int vpt_gpu_set_job_order_tail(vpt_gpu_ctx* ctx, int waves) {
+  if (!ctx || waves < 0) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_job_order_tail: bad argument");
+  ctx->order_tail_waves = waves;
+  return VPT_OK;
+}
+
+int vpt_gpu_tile_costs(vpt_gpu_ctx* ctx, float* cost, uint32_t* rank) {
+  if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  if ((rc = ensure_order(ctx))) return rc;
+  if (cost) std::memcpy(cost, ctx->tile_cost.data(), ctx->tile_cost.size() * sizeof(float));
+  if (rank) std::memcpy(rank, ctx->tile_rank.data(), ctx->tile_rank.size() * sizeof(uint32_t));
+  return VPT_OK;
 }
 
 int vpt_gpu_sync(vpt_gpu_ctx* ctx) {

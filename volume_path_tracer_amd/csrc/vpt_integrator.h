@@ -709,8 +709,38 @@ __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const
   }
 }
 
+// Scheduling order over a whole-wave range (never changes a job's samples, which its jid keys):
+// item k -> job (wave w, tile order[i]) with `order` = tiles by descending estimated cost.
+// Items before tail_k0 (= whole waves x T) run wave by wave, each wave costliest tile first.  The
+// last tail_n waves run as one costliest-first list, so the launch drains on cheap (sky) jobs: the
+// rank list is cut into groups of kOrderGroup tiles and a group's tail_n waves are consecutive
+// items, wave by wave -- the 64 lanes of a wavefront trace 64 different tiles (one tile per lane
+// would put the wavefront's film atomics on the same 64 addresses).
+constexpr uint32_t kOrderGroup = 64;
+__host__ __device__ __forceinline__ uint64_t ordered_job(uint32_t k, uint32_t T, const uint32_t* order, uint32_t tail_k0,
+                                                         uint32_t tail_n) {
+  if (k < tail_k0) {
+    const uint32_t w = k / T;
+    return (uint64_t)w * T + order[k - w * T];
+  }
+  k -= tail_k0;
+  const uint32_t full = T / kOrderGroup, span = kOrderGroup * tail_n;
+  uint32_t w, i;
+  if (k < full * span) {
+    const uint32_t g = k / span, r = k - g * span;
+    w = r / kOrderGroup;
+    i = g * kOrderGroup + (r - w * kOrderGroup);
+  } else {
+    const uint32_t R = T - full * kOrderGroup, r = k - full * span;
+    w = r / R;
+    i = full * kOrderGroup + (r - w * R);
+  }
+  return (uint64_t)(tail_k0 / T + w) * T + order[i];
+}
+
 // ------------------------------------------------------------------------------------------------
-// One iteration of the lane loop.  Env supplies fetch_job(uint64_t& jid_local) -> bool, jid_begin,
+// One iteration of the lane loop.  Env supplies fetch_job(uint64_t& item) -> bool, jid_begin, the
+// job order (order == nullptr: item k is job jid_begin + k; else ordered_job()),
 // film_add(S, lane, px, py, rw).  HasTemp: the scene has a temperature grid (fire).
 // Debug: keep every counter and the job index (per-sample records).
 // ------------------------------------------------------------------------------------------------
@@ -825,6 +855,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         p = (uint32_t)(j % S.tile_area);
         j /= S.tile_area;
       }
+      if (env.order) j = ordered_job((uint32_t)j, (uint32_t)S.T, env.order, env.order_tail_k0, env.order_tail_n);
       if (Debug) {
         ln.jid_local = j;
         ln.n_events = 0;

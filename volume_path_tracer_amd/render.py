@@ -183,6 +183,24 @@ class Integrator:
         (throughput mode: one stream per pixel; matches the reference only in expectation)."""
         capi.check(capi.lib().vpt_gpu_set_rng_mode(self.h, int(mode)), "vpt_gpu_set_rng_mode")
 
+    def set_job_order(self, mode: int) -> None:
+        """Scheduling order of whole-wave launches: capi.VPT_ORDER_JID (TileProvider order),
+        VPT_ORDER_COST_WAVE_MAJOR, VPT_ORDER_COST_TILE_MAJOR or VPT_ORDER_COST_TAIL (default).
+        Samples never depend on it."""
+        capi.check(capi.lib().vpt_gpu_set_job_order(self.h, int(mode)), "vpt_gpu_set_job_order")
+
+    def set_job_order_tail(self, waves: int) -> None:
+        """VPT_ORDER_COST_TAIL's tile-major wave count (0 = auto)."""
+        capi.check(capi.lib().vpt_gpu_set_job_order_tail(self.h, int(waves)), "vpt_gpu_set_job_order_tail")
+
+    def tile_costs(self):
+        """(cost float32[T], tile ranks by descending cost uint32[T]) of the job-order pass."""
+        T = self.cfg.jobs_per_wave()
+        cost, rank = np.zeros(T, np.float32), np.zeros(T, np.uint32)
+        capi.check(capi.lib().vpt_gpu_tile_costs(self.h, cost.ctypes.data_as(C.POINTER(C.c_float)),
+                                                  rank.ctypes.data_as(C.POINTER(C.c_uint32))), "vpt_gpu_tile_costs")
+        return cost, rank
+
     def counters(self, reset: bool = False) -> dict:
         c = capi.Counters()
         capi.check(capi.lib().vpt_gpu_counters(self.h, C.byref(c), 1 if reset else 0), "vpt_gpu_counters")
