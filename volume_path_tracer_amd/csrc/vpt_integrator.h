@@ -375,6 +375,7 @@ struct Lane {
   int32_t vinc[3];  // HDDA: dim * step[axis]
   // current majorant segment
   float s_t0, s_t1, s_dmaj;
+  float y_draw;  // 1 - u of a free-flight draw whose exact distance is pending (SM_EVAL)
   StencilCell dens_cell, temp_cell;
   uint32_t n_dda, n_stencil;  // hot counters, per lane (flushed by the kernel at exit)
 };
@@ -553,6 +554,9 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
   return true;
 }
 
+// Free-flight overshoot pre-test margin (SM_DRAW): RN(log2(e) * (1 + 2^-16)).
+constexpr float kOvershootC = 0x1.7155e8p+0f;
+
 // ------------------------------------------------------------------------------------------------
 // Phase function helpers (random.hpp:56-84, utils.hpp:39-66)
 // ------------------------------------------------------------------------------------------------
@@ -620,9 +624,20 @@ __host__ __device__ inline void scene_finalize(DevScene& S) {
 // (worker.cpp:145-188) or the shadow ray's ratio-tracking update (worker.cpp:66-85).
 template <bool HasTemp, bool Debug, class Env>
 __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const DevGrid& G, Lane& ln, Env& env) {
+  const float sigma_maj = ln.s_dmaj * S.sigma_t;
+  {
+    // The draw's exact free-flight distance, deferred from SM_DRAW (majorant_transmittance_sampler.cpp:44-45):
+    // dt = -log(1 - u) / sigma_maj (random.hpp:20-22), t = t0 + dt / m_scale.
+    const float dt_m = -math::logf_glibc_unit(ln.y_draw) / sigma_maj;
+    const float tc = ln.s_t0 + math::div_by_recip(dt_m, ln.scale, ln.rscale);  // == dt_m / m_scale
+    if (!(tc < ln.s_t1)) {  // overshoot after all: drop the segment
+      ln.sm = SM_NEED_SEG;
+      return;
+    }
+    ln.s_t0 = tc;  // the tentative collision
+  }
   env.prof(PB_TRILINEAR);
   const float t = ln.s_t0;
-  const float sigma_maj = ln.s_dmaj * S.sigma_t;
   float pi_x = ln.e[0] + ln.d[0] * t, pi_y = ln.e[1] + ln.d[1] * t, pi_z = ln.e[2] + ln.d[2] * t;
   float dens;
   if (Debug) env.tally(CNT_DENSITY_EVALS, 1);
@@ -1012,20 +1027,29 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       env.tick(PT_STEP);
       if (ln.state == ST_SAMPLE && ln.sm == SM_DRAW) {
         env.prof(PB_DRAW);
-        // MajorantTransmittanceSampler::next body (majorant_transmittance_sampler.cpp:39-79)
-        float sigma_maj = ln.s_dmaj * S.sigma_t;
-        float u = rng_uniform(ln.rng);
+        // MajorantTransmittanceSampler::next body (majorant_transmittance_sampler.cpp:39-79).  Most draws
+        // overshoot the segment (C3: 45 of 57 per sample) and their distance is never used, so the
+        // draw only proves the overshoot with the hardware log2: a = -v_log_f32(1 - u) satisfies
+        // a*ln2 <= X*(1 + 2.71*2^-24) for X = -logf(1 - u) as the exact path computes it, over every
+        // 1 - u (tools/proofs/log2_bound.hip).  With kOvershootC = log2(e)*(1 + 2^-16) rounded, a >
+        // thr = ((s_t1 - s_t0)*sigma_maj*m_scale)*kOvershootC then implies RN(s_t0 + RN(RN(X/sigma_maj)
+        // /m_scale)) >= s_t1 (every rounding is covered by the 2^-16 margin; the guards keep the
+        // intermediate results normal: m_scale in [2^-26, 2^26) via rscale, s_t1 - s_t0 >= 2^-96).
+        // Anything else parks in SM_EVAL, which computes the exact distance first (eval_collision).
+        const float sigma_maj = ln.s_dmaj * S.sigma_t;
+        const float u = rng_uniform(ln.rng);
         if (Debug) {
           env.tally(CNT_DRAWS, 1);
           env.tally(CNT_RNG_DRAWS, 1);
         }
-        float dt_m = -math::logf_glibc_unit(1 - u) / sigma_maj;
-        float t = ln.s_t0 + math::div_by_recip(dt_m, ln.scale, ln.rscale);  // == dt_m / m_scale
-        if (t < ln.s_t1) {
-          ln.s_t0 = t;       // the tentative collision; its density is evaluated in SM_EVAL
-          ln.sm = SM_EVAL;
-        } else {
+        const float y = 1 - u;
+        const float D = ln.s_t1 - ln.s_t0;
+        const float thr = ((D * sigma_maj) * ln.scale) * kOvershootC;
+        if (math::neg_log2_hw(y) > thr && D >= 0x1p-96f && ln.rscale == ln.rscale) {
           ln.sm = SM_NEED_SEG;
+        } else {
+          ln.y_draw = y;
+          ln.sm = SM_EVAL;
         }
       }
       env.tick(PT_DRAW);

@@ -206,6 +206,17 @@ __host__ __device__ __forceinline__ float recip_for_div(float b) {
   return (e - (127u - 26u) < 52u) ? rcp_rn(b) : __builtin_nanf("");
 }
 // RN(a / b) for any a, b.
+// -log2(x) by the hardware (v_log_f32), for the free-flight overshoot pre-test only; its error bound
+// over the integrator's inputs is measured by tools/proofs/log2_bound.hip.  Host builds return 0,
+// which never passes the pre-test (every draw takes the exact path).
+__host__ __device__ __forceinline__ float neg_log2_hw(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return -__builtin_amdgcn_logf(x);
+#else
+  (void)x;
+  return 0.0f;
+#endif
+}
 __host__ __device__ __forceinline__ float div_rn(float a, float b) { return div_by_recip(a, b, recip_for_div(b)); }
 }  // namespace math
 }  // namespace vpt
