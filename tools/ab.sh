@@ -8,7 +8,7 @@ if [ -z "${NOTEST:-}" ]; then
 fi
 for L in ${LIBS:-libvpt_amd_base libvpt_amd}; do
   for OR in ${ORDERS:--1}; do
-    VPT_LIB=$PWD/volume_path_tracer_amd/lib/$L.so timeout -k 10 300 python tools/tune.py --config ${CONFIG:-c3} --spp ${SPP:-256} --gates ${GATES:-8:12:24:4} --reps ${REPS:-3} --order $OR > $O/$L.o$OR.log 2>&1 || exit $?
+    VPT_LIB=$PWD/volume_path_tracer_amd/lib/$L.so timeout -k 10 300 python tools/tune.py --config ${CONFIG:-c3} --spp ${SPP:-256} --gates ${GATES:-8:12:32:4} --reps ${REPS:-3} --order $OR > $O/$L.o$OR.log 2>&1 || exit $?
     echo "$L order=$OR $(grep Msps $O/$L.o$OR.log | tail -1 | cut -c1-200)"
   done
 done

@@ -510,11 +510,12 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   VPT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
   if (per_cu < 1) per_cu = 1;
   ctx->grid_blocks = per_cu * cus;
-  // Scheduling defaults from tools/tune.py sweeps on MI355X (C3, 32 spp): rare states run for >= 8
-  // waiting lanes, density evaluations for >= 16, everything runs when < 8 lanes are walking.
+  // Scheduling defaults from tools/tune.py sweeps on MI355X (C3, 256 spp): rare states run for >= 8
+  // waiting lanes, density evaluations (with the deferred exact draw) for >= 32, everything runs when
+  // < 12 lanes are walking; the walk loops while >= 4 lanes walk.
   ctx->scene.gate_min = 8;
   ctx->scene.gate_idle = 12;
-  ctx->scene.gate_eval = 24;
+  ctx->scene.gate_eval = 32;
   ctx->scene.gate_walk = 4;
   ctx->scene.pixel_mode = 0;
   ctx->scene.tile_area = (uint32_t)(ctx->scene.tw * ctx->scene.th);

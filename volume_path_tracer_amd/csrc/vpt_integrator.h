@@ -303,7 +303,7 @@ __host__ __device__ inline void blackbody_xyz(const DevScene& S, float t, float&
     Z = acc[2] / S.y_integral;
     return;
   }
-  int dn = (int)(t / 100.0f);
+  int dn = (int)math::div_by_recip(t, 100.0f, 0.01f);  // t / 100 (0.01f == RN(1/100))
   while (t <= bb_idx_to_temp(dn - 1)) --dn;
   while (t >= bb_idx_to_temp(dn + 1)) ++dn;
   const float* a = S.bb + dn * 3;
@@ -313,11 +313,21 @@ __host__ __device__ inline void blackbody_xyz(const DevScene& S, float t, float&
     Z = a[2];
     return;
   }
-  float w = (t - bb_idx_to_temp(dn)) / 100.0f;
+  float w = math::div_by_recip(t - bb_idx_to_temp(dn), 100.0f, 0.01f);
   const float* b = a + 3;
   X = a[0] + (b[0] - a[0]) * w;  // vpt::lerp: a + (b - a) * t (utils.hpp:26-29)
   Y = a[1] + (b[1] - a[1]) * w;
   Z = a[2] + (b[2] - a[2]) * w;
+}
+
+// q / rw for a pixel counter q >= 0 and a row width rw >= 1.  Below 2^20 the quotient comes from the
+// hardware reciprocal: (q + 0.5) / rw lies >= 0.5 / rw from every integer and the estimate's error
+// is < 2^-22 relative (v_rcp_f32 within 1 ulp, one rounded product), i.e. < 0.25 / rw.
+__host__ __device__ __forceinline__ int32_t div_pix(int32_t q, int32_t rw) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (q < (1 << 20)) return (int32_t)(((float)q + 0.5f) * __builtin_amdgcn_rcpf((float)rw));
+#endif
+  return q / rw;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -393,19 +403,20 @@ __host__ __device__ __forceinline__ RayDir ray_dir_setup(const DevGrid& g, const
   RayDir r;
   float dx, dy, dz;
   jac_inv(g, dir[0], dir[1], dir[2], dx, dy, dz);
-  float len = sqrtf(dx * dx + dy * dy + dz * dz);
-  float inv_len = 1.0f / len;
+  // Correctly rounded sqrt / reciprocal through the short exact sequences of vpt_math.h.
+  float len = math::sqrt_rn(dx * dx + dy * dy + dz * dz);
+  float inv_len = math::rcp_rn(len);
   r.d[0] = dx * inv_len;
   r.d[1] = dy * inv_len;
   r.d[2] = dz * inv_len;
   r.len = len;
-  r.inv[0] = 1 / r.d[0];
-  r.inv[1] = 1 / r.d[1];
-  r.inv[2] = 1 / r.d[2];
+  r.inv[0] = math::rcp_rn(r.d[0]);
+  r.inv[1] = math::rcp_rn(r.d[1]);
+  r.inv[2] = math::rcp_rn(r.d[2]);
   // m_scale = 1 / |worldToIndexDirF(index dir)|
   float jx, jy, jz;
   jac_inv(g, r.d[0], r.d[1], r.d[2], jx, jy, jz);
-  r.scale = 1 / sqrtf(jx * jx + jy * jy + jz * jz);
+  r.scale = math::rcp_rn(math::sqrt_rn(jx * jx + jy * jy + jz * jz));
   r.rscale = math::recip_for_div(r.scale);
   return r;
 }
@@ -847,7 +858,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       }
       // the pixel just traced is pix - 1 of the tile
       const int32_t rw = min(S.W - ln.x0, S.tw);
-      const int32_t q = (ln.pix & kPixelMask) - 1, y = q / rw;
+      const int32_t q = (ln.pix & kPixelMask) - 1, y = div_pix(q, rw);
       env.film_add(S, ln, ln.x0 + (q - y * rw), ln.y0 + y, rw);
       env.tally(CNT_SAMPLES, 1);
       ln.state = ST_PIXEL;
@@ -908,7 +919,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
           ln.state = ST_FETCH;
           return;
         }
-        int32_t y = q / rw;
+        int32_t y = div_pix(q, rw);
         px = ln.x0 + (q - y * rw);
         py = ln.y0 + y;
         ++q;
@@ -926,10 +937,10 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       for (int i = 0; i < 3; ++i) dv[i] = S.cam_t[i] + (S.cam_L[i * 3] * rx + (S.cam_L[i * 3 + 1] * ry + S.cam_L[i * 3 + 2] * 0.0f));
       float n2 = dv[0] * dv[0] + (dv[1] * dv[1] + dv[2] * dv[2]);
       if (n2 > 0.0f) {
-        float s = sqrtf(n2);
-        dv[0] = dv[0] / s;
-        dv[1] = dv[1] / s;
-        dv[2] = dv[2] / s;
+        const float s = math::sqrt_rn(n2), rs = math::recip_for_div(s);
+        dv[0] = math::div_by_recip(dv[0], s, rs);
+        dv[1] = math::div_by_recip(dv[1], s, rs);
+        dv[2] = math::div_by_recip(dv[2], s, rs);
       }
       for (int i = 0; i < 3; ++i) {
         ln.ro[i] = S.cam_pos[i];
