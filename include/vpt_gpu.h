@@ -218,6 +218,23 @@ typedef struct vpt_event {
 int vpt_gpu_trace_jobs(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film_device,
                        vpt_event* events_device, uint64_t capacity, uint64_t* count, void* hip_stream);
 
+/* Volume::log_dda_trace (src/volume.cpp:194-225) for one world ray, on the host: the voxels of
+ * NanoVDB's unit DDA from 16 index units before to 16 after the ray's clip to the index bbox, with
+ * getValue, getDim, getNodeInfo (dim, maximum) and isActive at each (row = one dda_trace.csv line).
+ * *n_rows = voxels walked (rows beyond max_rows are not written), or -1 when the ray misses the
+ * index bbox (the reference then writes no file). */
+typedef struct vpt_dda_row {
+  int32_t ijk[3];
+  float t;
+  float value;
+  uint32_t dim_getdim;
+  uint32_t dim_nodeinfo;
+  int32_t active;
+  float maximum;
+} vpt_dda_row;
+int vpt_dda_trace(const vpt_grid_desc* density, const float origin[3], const float direction[3], vpt_dda_row* rows,
+                  int max_rows, int* n_rows);
+
 /* Volume::log_majorant_trace (src/volume.cpp:176-192) for one world ray: per RayMajorantIterator
  * segment the row X0,Y0,Z0,X1,Y1,Z1,T0,T1,Majorant (index-space end points, world-space t).
  * rows_host: [max_rows][9]; *n_rows = segments (0 if the ray misses the volume).  Synchronous. */

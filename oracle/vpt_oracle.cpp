@@ -129,12 +129,16 @@ struct Lower {  // InternalNode<Leaf, 4>: 16^3 slots of 8^3
   std::vector<int32_t> child;  // 4096, leaf index or -1
   std::vector<float> tile;
   std::vector<uint8_t> active;
+  float max = 0.0f;  // build statistic (NodeInfo::maximum), see Grid::update_stats
+  bool max_any = false;
 };
 struct Upper {  // InternalNode<Lower, 5>: 32^3 slots of 128^3
   int32_t origin[3];
   std::vector<int32_t> child;  // 32768, lower index or -1
   std::vector<float> tile;
   std::vector<uint8_t> active;
+  float max = 0.0f;
+  bool max_any = false;
 };
 struct RootTile {
   int32_t upper = -1;  // child upper index, or -1 for a value tile
@@ -162,6 +166,76 @@ struct Grid {
   std::vector<Lower> lowers;
   std::vector<Upper> uppers;
   std::map<Key, RootTile> root;
+  float root_max = 0.0f;
+
+  // NanoVDB's build statistics of the internal nodes and the root (tools/GridStats.h, restated):
+  // maximum over the children's maxima and the active tile values; 0 when a node has none.  Taken
+  // from the stored leaf maxima, i.e. before fix_majorants_for_interpolation rewrites them.
+  void update_stats() {
+    auto acc = [](float& m, bool& any, float x) {
+      m = any ? std::max(m, x) : x;
+      any = true;
+    };
+    for (Lower& l : lowers) {
+      bool any = false;
+      float m = 0.0f;
+      for (int n = 0; n < 4096; ++n) {
+        if (l.child[n] >= 0) acc(m, any, leaves[l.child[n]].max);
+        else if (l.active[n]) acc(m, any, l.tile[n]);
+      }
+      l.max = m;
+      l.max_any = any;
+    }
+    for (Upper& u : uppers) {
+      bool any = false;
+      float m = 0.0f;
+      for (int n = 0; n < 32768; ++n) {
+        if (u.child[n] >= 0) {
+          if (lowers[u.child[n]].max_any) acc(m, any, lowers[u.child[n]].max);
+        } else if (u.active[n]) {
+          acc(m, any, u.tile[n]);
+        }
+      }
+      u.max = m;
+      u.max_any = any;
+    }
+    bool any = false;
+    float m = 0.0f;
+    for (const auto& kv : root) {
+      if (kv.second.upper >= 0) {
+        if (uppers[kv.second.upper].max_any) acc(m, any, uppers[kv.second.upper].max);
+      } else if (kv.second.active) {
+        acc(m, any, kv.second.value);
+      }
+    }
+    root_max = m;
+  }
+
+  // ReadAccessor::getNodeInfo(ijk): dim and maximum of the deepest node holding ijk.
+  void node_info(int32_t i, int32_t j, int32_t k, uint32_t& dim, float& maximum) const {
+    auto it = root.find(root_key(i, j, k));
+    if (it == root.end() || it->second.upper < 0) {
+      dim = 4096u;  // RootNode: NodeInfo{LEVEL, ChildT::dim(), ...}
+      maximum = root_max;
+      return;
+    }
+    const Upper& up = uppers[it->second.upper];
+    const int32_t lo_idx = up.child[upper_offset(i, j, k)];
+    if (lo_idx < 0) {
+      dim = 4096u;
+      maximum = up.max;
+      return;
+    }
+    const Lower& lo = lowers[lo_idx];
+    const int32_t lf_idx = lo.child[lower_offset(i, j, k)];
+    if (lf_idx < 0) {
+      dim = 128u;
+      maximum = lo.max;
+      return;
+    }
+    dim = 8u;
+    maximum = leaves[lf_idx].max;  // after fix_majorants_for_interpolation (it writes the grid)
+  }
 
   // Node walk. level_out: 0 leaf, 1 lower-tile, 2 upper-tile, 3 root tile/background.
   struct Hit {
@@ -1051,6 +1125,7 @@ vpto_grid* vpto_grid_create(const vpt_grid_desc* d) {
       rt.active = act;
     }
   }
+  g.update_stats();
   return G.release();
 }
 
@@ -1170,6 +1245,59 @@ int vpto_majorant_trace(const vpto_grid* G, const float* o, const float* d, floa
     }
     ++n;
   }
+  return n;
+}
+
+// Volume::log_dda_trace (volume.cpp:194-225): NanoVDB math::DDA<Ray<float>, Coord, 1> (HDDA.h,
+// restated) over the index ray clipped to the bbox and widened by 16 at both ends.
+int vpto_dda_trace(const vpto_grid* G, const float* o, const float* d, vpt_dda_row* rows, int max_rows) {
+  const Grid& g = G->g;
+  NRay w_ray(v3(o[0], o[1], o[2]), v3(d[0], d[1], d[2]));
+  w_ray.t1 = 10000.0f;  // setMaxTime
+  NRay ray = w_ray.worldToIndexF(g);
+  if (!ray.clip(g.bbox_min, g.bbox_max)) return -1;
+  ray.t0 = ray.t0 - 16.0f;  // setMinTime / setMaxTime
+  ray.t1 = ray.t1 + 16.0f;
+  // DDA::init
+  float t0 = ray.t0;
+  const V3 pos = ray.at(t0);
+  const float P[3] = {pos.x, pos.y, pos.z}, D[3] = {ray.dir.x, ray.dir.y, ray.dir.z}, I[3] = {ray.inv.x, ray.inv.y, ray.inv.z};
+  int32_t voxel[3], stp[3];
+  float next[3], delta[3] = {0.0f, 0.0f, 0.0f};
+  for (int a = 0; a < 3; ++a) {
+    voxel[a] = nvdb_floor(P[a]);  // RoundDown<Coord>(pos) & ~(Dim - 1), Dim = 1
+    if (D[a] == 0.0f) {
+      next[a] = std::numeric_limits<float>::max();
+      stp[a] = 0;
+    } else if (I[a] > 0) {
+      stp[a] = 1;
+      next[a] = t0 + ((float)(voxel[a] + 1) - P[a]) * I[a];
+      delta[a] = I[a];
+    } else {
+      stp[a] = -1;
+      next[a] = t0 + ((float)voxel[a] - P[a]) * I[a];
+      delta[a] = -I[a];
+    }
+  }
+  int n = 0;
+  do {
+    if (n < max_rows) {
+      vpt_dda_row& r = rows[n];
+      const Grid::Hit h = g.query(voxel[0], voxel[1], voxel[2]);
+      for (int a = 0; a < 3; ++a) r.ijk[a] = voxel[a];
+      r.t = t0;
+      r.value = h.value;                // getValue
+      r.dim_getdim = h.dim;             // getDim(ijk, ray)
+      g.node_info(voxel[0], voxel[1], voxel[2], r.dim_nodeinfo, r.maximum);
+      r.active = h.active ? 1 : 0;      // isActive
+    }
+    ++n;
+    // DDA::step
+    const int axis = (next[0] < next[1] && next[0] < next[2]) ? 0 : (next[1] < next[2] ? 1 : 2);
+    t0 = next[axis];
+    next[axis] += delta[axis];
+    voxel[axis] += stp[axis];
+  } while (t0 <= ray.t1);
   return n;
 }
 

@@ -75,6 +75,9 @@ int vpto_render_jobs_events(const vpt_configuration* cfg, const vpto_grid* densi
                             float y_integral, uint64_t jid_begin, uint64_t jid_count, float* film,
                             vpt_event* events, uint64_t capacity, uint64_t* count);
 /* Volume::log_majorant_trace (volume.cpp:176-192): [max_rows][9] rows; returns the segment count. */
+/* Volume::log_dda_trace (src/volume.cpp:194-225): rows as vpt_dda_row; returns the voxel count or
+ * -1 when the ray misses the index bbox. */
+int vpto_dda_trace(const vpto_grid* density, const float* origin3, const float* dir3, vpt_dda_row* rows, int max_rows);
 int vpto_majorant_trace(const vpto_grid* density, const float* origin3, const float* dir3, float* rows,
                         int max_rows);
 

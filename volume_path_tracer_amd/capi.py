@@ -91,6 +91,10 @@ class Counters(C.Structure):
 # vpt_event (include/vpt_gpu.h): one Logger line (src/worker.cpp:16-48)
 EVENT_DTYPE = np.dtype([("jid", "<u8"), ("pixel", "<u4"), ("seq", "<u4"), ("type", "<u4"), ("v", "<f4", (7,))])
 assert EVENT_DTYPE.itemsize == 48
+# vpt_dda_row (Volume::log_dda_trace, one dda_trace.csv line)
+DDA_ROW_DTYPE = np.dtype([("ijk", "<i4", (3,)), ("t", "<f4"), ("value", "<f4"), ("dim_getdim", "<u4"),
+                          ("dim_nodeinfo", "<u4"), ("active", "<i4"), ("maximum", "<f4")])
+assert DDA_ROW_DTYPE.itemsize == 36
 VPT_RNG_REFERENCE, VPT_RNG_PIXEL = 0, 1
 VPT_ORDER_JID, VPT_ORDER_COST_WAVE_MAJOR, VPT_ORDER_COST_TILE_MAJOR, VPT_ORDER_COST_TAIL = 0, 1, 2, 3
 EVENT_NAMES = ("new_ray", "sampled_point", "null", "scatter_terminated", "scatter", "absorbed")
@@ -227,6 +231,7 @@ def lib() -> C.CDLL:
     L.vpt_film_to_srgb8.argtypes = [fp, C.c_int64, C.c_int64, C.POINTER(C.c_uint8)]
     L.vpt_gpu_trace_jobs.argtypes = [vp, C.c_uint64, C.c_uint64, vp, vp, C.c_uint64, C.POINTER(C.c_uint64), vp]
     L.vpt_gpu_majorant_trace.argtypes = [vp, fp, fp, fp, C.c_int, C.POINTER(C.c_int)]
+    L.vpt_dda_trace.argtypes = [C.POINTER(GridDesc), fp, fp, vp, C.c_int, C.POINTER(C.c_int)]
     L.vpt_gpu_set_rng_mode.argtypes = [vp, C.c_int]
     L.vpt_gpu_set_job_order.argtypes = [vp, C.c_int]
     L.vpt_gpu_set_job_order_tail.argtypes = [vp, C.c_int]
