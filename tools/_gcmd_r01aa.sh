@@ -1,0 +1,12 @@
+# run-radius HDDA skipping: full GPU tests, then A/B vs HEAD base on C3 (and C2)
+export TMPDIR=/tmp; O=gpurun_out/r01aa; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -2 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
+for R in 1 2; do for L in libvpt_amd_base libvpt_amd; do
+  VPT_LIB=$PWD/volume_path_tracer_amd/lib/$L.so timeout -k 10 200 python tools/tune.py --spp 256 --gates 8:12:32:4 --reps 2 > $O/$L.$R.log 2>&1 || exit $?
+  echo "$L $(grep Msps $O/$L.$R.log | tail -1 | cut -c90-200)"
+done; done
+for L in libvpt_amd_base libvpt_amd; do
+  VPT_LIB=$PWD/volume_path_tracer_amd/lib/$L.so timeout -k 10 200 python tools/tune.py --config c2 --spp 64 --gates 8:12:32:4 --reps 2 > $O/$L.c2.log 2>&1 || exit $?
+  echo "c2 $L $(grep Msps $O/$L.c2.log | tail -1 | cut -c90-200)"
+done
