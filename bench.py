@@ -201,7 +201,9 @@ def main():
             "scaling": args.mode,
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (512^3 procedural cloud stand-in for wdas_cloud.nvdb, SURVEY §8d)",
+            "data": (f"synthetic ({wl.grid_n}^3 procedural cloud stand-in for "
+                     f"{'fire.nvdb + 40*base temperature grid' if wl.temperature else 'wdas_cloud.nvdb'}, SURVEY §8d)"
+                     if wl.density_kind == 1 else f"synthetic constant-density {wl.grid_n}^3 grid (SURVEY §8d C2)"),
             "config": {"workload": f"{args.config}: {'fire' if wl.temperature else 'wdas_cloud'}.json "
                                    f"{wl.cfg.width}x{wl.cfg.height}, {spp} spp "
                                    f"{'per GPU' if args.mode == 'weak' else 'per image'}, 8x8 tiles, seed {wl.cfg.seed}",
@@ -214,7 +216,9 @@ def main():
                          "kernel": "vpt_integrate_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                          "algorithmic_bytes_per_launch": int(bytes_per_launch),
                          "bytes_per_sample": round(algorithmic_bytes(counters) / samples_rank, 2)},
-            "counters_per_sample": {k: round(v / samples_rank, 3) for k, v in counters.items() if k != "samples"},
+            # the production kernel counts the events that price algorithmic bytes
+            "counters_per_sample": {k: round(counters[k] / samples_rank, 3)
+                                    for k in ("dda_steps", "stencils", "temp_stencils")},
         }
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(wl, dens, temp, args.cpu_budget)
