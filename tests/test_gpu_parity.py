@@ -71,6 +71,43 @@ def test_gpu_c3_fullres_job_sample_bit_exact():
     assert total > 0 and diff == 0, f"{diff}/{total}"
 
 
+def test_gpu_c4_fullres_job_sample_bit_exact():
+    """C4 (fire 1920x1080, 512^3 density + temperature): jobs sampled across the jid space, with the
+    blackbody emission at every tentative collision."""
+    wl = workload("c4")
+    it, dens, temp = _integrator(wl)
+    T = it.jobs_per_wave
+    rng = np.random.default_rng(4)
+    begins = sorted(set(int(x) for x in rng.integers(0, 256 * T - 64, size=5))) + [T * 200 + T // 2 + 7]
+    od = O.OracleGrid(dens, fix_majorants=True)
+    ot = O.OracleGrid(temp, fix_majorants=False)
+    diff = total = emitting = 0
+    for b in begins:
+        _, r_g = _gpu_records(it, b, 48)
+        _, r_o, _ = O.render_jobs(wl.cfg, od, ot, b, 48, records=True)
+        ok = ~np.isnan(r_o[:, 0])
+        diff += int((r_g[ok].view(np.uint32) != r_o[ok].view(np.uint32)).any(axis=1).sum())
+        total += int(ok.sum())
+        emitting += int((r_o[ok, 1] > 0).sum())
+    assert total > 0 and emitting > 0 and diff == 0, f"{diff}/{total}"
+
+
+def test_gpu_fire_lowscattering_scene_bit_exact():
+    """The reference's third scene (scenes/fire_lowscattering.json) on the fire stand-in."""
+    from volume_path_tracer_amd.scenes import Workload, _standin_camera, scene
+    cfg = scene("fire_lowscattering")
+    cfg.output_size[0], cfg.output_size[1], cfg.num_waves = 40, 24, 2
+    _standin_camera(cfg, 800.0 * 64 / 512)
+    wl = Workload("fire_lowscattering", cfg, 1, 64, True)
+    it, dens, temp = _integrator(wl)
+    jobs = cfg.jobs_per_wave() * 2
+    f_g, r_g = _gpu_records(it, 0, jobs)
+    f_o, r_o, _ = _oracle(wl, dens, temp, 0, jobs)
+    same = (r_g.view(np.uint32) == r_o.view(np.uint32)).all(axis=1)
+    assert same.all(), f"{(~same).sum()} of {same.size} samples differ"
+    np.testing.assert_array_equal(f_g[..., 3], f_o[..., 3])
+
+
 def test_gpu_sharded_waves_sum_to_full():
     """Wave-sharded rendering (the multi-GPU partition) reproduces the one-launch film."""
     wl = workload("c3", width=96, height=64, spp=8, grid_n=128)
