@@ -26,6 +26,8 @@ struct HostEnv {
   uint32_t order_tail_k0 = 0;
   uint32_t order_tail_n = 0;
   int32_t count(bool pred) { return pred ? 1 : 0; }  // one lane
+  vpt::LaneCold cold_{};
+  vpt::LaneCold& cold() { return cold_; }
   uint64_t cnt[vpt::CNT_COUNT] = {};
   void tally(int32_t k, int32_t w) { cnt[k] += (uint64_t)w; }
   void prof(int32_t) {}
@@ -40,15 +42,16 @@ struct HostEnv {
   void film_add(const vpt::DevScene& S, const vpt::Lane& ln, int32_t px, int32_t py, int32_t rw) {
     float* f = film + ((int64_t)py * S.W + px) * 4;
     f[3] += 1.0f;
-    f[0] += S.imaging_ratio * ln.L[0];
-    f[1] += S.imaging_ratio * ln.L[1];
-    f[2] += S.imaging_ratio * ln.L[2];
+    const vpt::LaneCold& lc = cold_;
+    f[0] += S.imaging_ratio * lc.L[0];
+    f[1] += S.imaging_ratio * lc.L[1];
+    f[2] += S.imaging_ratio * lc.L[2];
     if (records) {
-      int32_t xl = px - ln.x0, yl = py - ln.y0;
+      int32_t xl = px - lc.x0, yl = py - lc.y0;
       float* r = records + (ln.jid_local * (uint64_t)tile_area + (uint64_t)(yl * rw + xl)) * 3;
-      r[0] = ln.L[0];
-      r[1] = ln.L[1];
-      r[2] = ln.L[2];
+      r[0] = lc.L[0];
+      r[1] = lc.L[1];
+      r[2] = lc.L[2];
     }
   }
 };
@@ -94,12 +97,13 @@ extern "C" int vpths_render_jobs_order(const vpt_configuration* cfg, const vpt_g
   vpt::Lane ln;
   std::memset(&ln, 0, sizeof ln);
   vpt::lane_init(ln);
+  vpt::cold_init(env.cold());
   if (temperature)
     while (ln.state != vpt::ST_DONE) vpt::lane_iteration<true, true>(&S, ln, env);
   else
     while (ln.state != vpt::ST_DONE) vpt::lane_iteration<false, true>(&S, ln, env);
   env.cnt[vpt::CNT_DDA_STEPS] += ln.n_dda;
-  env.cnt[vpt::CNT_STENCILS] += ln.n_stencil;
+  env.cnt[vpt::CNT_STENCILS] += env.cold().n_stencil;
   if (counters) {
     uint64_t* o = reinterpret_cast<uint64_t*>(counters);
     for (int k = 0; k < vpt::CNT_COUNT; ++k) o[k] += env.cnt[k];

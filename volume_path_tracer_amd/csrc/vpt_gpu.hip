@@ -35,14 +35,19 @@ int set_error(int code, const std::string& msg) {
 
 constexpr int kCounterCount = CNT_COUNT;
 constexpr int kBlockThreads = 256;
-// Minimum waves per SIMD (launch bounds): 5 for the production density-only kernel (97 -> 96
-// VGPRs, no spills); 4 for the temperature and per-sample-record variants, which would spill.
+// Minimum waves per SIMD (launch bounds): 6 for the production density-only kernel (80 VGPRs; the
+// cold lane state lives in LDS, see LaneCold); 4 for the temperature and per-sample-record
+// variants.  The kernel is latency-bound enough that occupancy pays: persistent grids of 3/4/5
+// blocks per CU measured 802/956/1067 Msps on C3 with one binary, and 6 waves 1115.
 #ifndef VPT_WAVES_FAST
-#define VPT_WAVES_FAST 5
+#define VPT_WAVES_FAST 6
 #endif
 #ifndef VPT_WAVES_SLOW
 #define VPT_WAVES_SLOW 4
 #endif
+
+// The lanes' cold state (vpt_integrator.h LaneCold), one slot per thread of the integrator's block.
+__shared__ LaneCold g_lane_cold[kBlockThreads];
 
 struct KernelEnv {
   uint64_t jid_begin;
@@ -115,7 +120,7 @@ struct KernelEnv {
     if (slot >= event_cap) return;
     vpt_event* e = events + slot;
     e->jid = jid_begin + ln.jid_local;
-    e->pixel = (uint32_t)((ln.pix & kPixelMask) - 1);
+    e->pixel = (uint32_t)((cold().pix & kPixelMask) - 1);
     e->seq = seq;
     e->type = type;
     for (int i = 0; i < 3; ++i) {
@@ -124,6 +129,7 @@ struct KernelEnv {
     }
     e->v[6] = 0.0f;
   }
+  __device__ __forceinline__ LaneCold& cold() { return g_lane_cold[threadIdx.x]; }
   // lanes of this wavefront for which pred holds
   // (ballot_w64 on the bool itself: the compare folds into the mask, no materialised 0/1 VGPR)
   __device__ __forceinline__ int32_t count(bool pred) { return (int32_t)__popcll(__builtin_amdgcn_ballot_w64(pred)); }
@@ -136,16 +142,17 @@ struct KernelEnv {
   __device__ __forceinline__ void film_add(const DevScene& S, const Lane& ln, int32_t px, int32_t py, int32_t rw) {
     float* f = film + ((int64_t)py * S.W + px) * 4;
     const float r = S.imaging_ratio;
+    const LaneCold& lc = cold();
     atomicAdd(f + 3, 1.0f);
-    atomicAdd(f + 0, r * ln.L[0]);
-    atomicAdd(f + 1, r * ln.L[1]);
-    atomicAdd(f + 2, r * ln.L[2]);
+    atomicAdd(f + 0, r * lc.L[0]);
+    atomicAdd(f + 1, r * lc.L[1]);
+    atomicAdd(f + 2, r * lc.L[2]);
     if (records) {
-      const int32_t xl = px - ln.x0, yl = py - ln.y0;
+      const int32_t xl = px - lc.x0, yl = py - lc.y0;
       float* rec = records + (ln.jid_local * (uint64_t)tile_area + (uint64_t)(yl * rw + xl)) * 3;
-      rec[0] = ln.L[0];
-      rec[1] = ln.L[1];
-      rec[2] = ln.L[2];
+      rec[0] = lc.L[0];
+      rec[1] = lc.L[1];
+      rec[2] = lc.L[2];
     }
   }
 };
@@ -167,10 +174,11 @@ __global__ __launch_bounds__(kBlockThreads, (HasTemp || Debug) ? VPT_WAVES_SLOW 
 #endif
   Lane ln;
   lane_init(ln);
+  cold_init(env.cold());
   const ScenePtr sp = (ScenePtr)scene;
   while (ln.state != ST_DONE) lane_iteration<HasTemp, Debug>(sp, ln, env);
   atomicAdd(wg_counters + CNT_DDA_STEPS, (unsigned long long)ln.n_dda);
-  atomicAdd(wg_counters + CNT_STENCILS, (unsigned long long)ln.n_stencil);
+  atomicAdd(wg_counters + CNT_STENCILS, (unsigned long long)env.cold().n_stencil);
   __syncthreads();
   if (threadIdx.x < kCounterCount && wg_counters[threadIdx.x])
     atomicAdd(counters + threadIdx.x, wg_counters[threadIdx.x]);

@@ -363,15 +363,23 @@ enum : int32_t {
   CNT_SCATTERS, CNT_SHADOW_RAYS, CNT_RNG_DRAWS, CNT_COUNT
 };
 
-struct Lane {
-  int32_t state, sm, shadow, terminated;
-  uint64_t rng;
-  uint64_t jid_local;  // job index relative to jid_begin (records / events only)
-  uint32_t n_events;   // events logged so far in this job (event traces only)
+// The lane's cold state: touched only by the per-pixel, per-bounce and film blocks, never by the
+// walk.  The kernel keeps it in LDS (Env::cold(), one 15-word slot per lane: an odd stride, so a
+// wavefront's accesses hit distinct banks) instead of VGPRs, which leaves the walk its registers.
+struct LaneCold {
   int32_t x0, y0, pix;
   uint32_t depth;
   float L[3];
   float ro[3], rd[3];  // current primary world ray; ro is also the scatter point during NEE
+  int32_t terminated;
+  uint32_t n_stencil;  // stencil refreshes (flushed by the kernel at exit)
+};
+
+struct Lane {
+  int32_t state, sm, shadow;
+  uint64_t rng;
+  uint64_t jid_local;  // job index relative to jid_begin (records / events only)
+  uint32_t n_events;   // events logged so far in this job (event traces only)
   float Tr;            // shadow-ray transmittance (< 0: sample_Ld returns zero)
   // RayMajorantIterator: index-space ray, scale, majorant, HDDA (NanoVDB math::HDDA state)
   float e[3], d[3], inv[3];
@@ -387,7 +395,7 @@ struct Lane {
   float s_t0, s_t1, s_dmaj;
   float y_draw;  // 1 - u of a free-flight draw whose exact distance is pending (SM_EVAL)
   StencilCell dens_cell, temp_cell;
-  uint32_t n_dda, n_stencil;  // hot counters, per lane (flushed by the kernel at exit)
+  uint32_t n_dda;  // hot counter, per lane (flushed by the kernel at exit)
 };
 
 // HDDA step direction and per-cell increment from the (normalised, index-space) direction:
@@ -635,6 +643,7 @@ __host__ __device__ inline void scene_finalize(DevScene& S) {
 // (worker.cpp:145-188) or the shadow ray's ratio-tracking update (worker.cpp:66-85).
 template <bool HasTemp, bool Debug, class Env>
 __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const DevGrid& G, Lane& ln, Env& env) {
+  LaneCold& lc = env.cold();
   const float sigma_maj = ln.s_dmaj * S.sigma_t;
   {
     // The draw's exact free-flight distance, deferred from SM_DRAW (majorant_transmittance_sampler.cpp:44-45):
@@ -652,7 +661,7 @@ __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const
   float pi_x = ln.e[0] + ln.d[0] * t, pi_y = ln.e[1] + ln.d[1] * t, pi_z = ln.e[2] + ln.d[2] * t;
   float dens;
   if (Debug) env.tally(CNT_DENSITY_EVALS, 1);
-  if (trilinear(G, ln.dens_cell, pi_x, pi_y, pi_z, dens)) ++ln.n_stencil;
+  if (trilinear(G, ln.dens_cell, pi_x, pi_y, pi_z, dens)) ++lc.n_stencil;
   ln.sm = SM_DRAW;  // density <= 0, a null event or an unkilled shadow ray: keep drawing
   if (dens > 0.0f) {
     float cp[3];
@@ -671,9 +680,9 @@ __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const
         float tK = tadim * S.temp_scale + S.temp_offset;
         blackbody_xyz(S, tK, X, Y, Z);
         float sc = p_a * S.le_scale;
-        ln.L[0] = ln.L[0] + sc * X;
-        ln.L[1] = ln.L[1] + sc * Y;
-        ln.L[2] = ln.L[2] + sc * Z;
+        lc.L[0] = lc.L[0] + sc * X;
+        lc.L[1] = lc.L[1] + sc * Y;
+        lc.L[2] = lc.L[2] + sc * Z;
       }
       float ue = rng_uniform(ln.rng);
       if (Debug) env.tally(CNT_RNG_DRAWS, 1);
@@ -690,17 +699,17 @@ __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const
       }
       if (ev == 1) {
         if (Debug) env.event(ln, VPT_EV_ABSORBED, nullptr, nullptr, 0.0f);
-        ln.terminated = 1;
+        lc.terminated = 1;
         ln.state = ST_FINISH;
       } else if (ev == 2) {
-        if (ln.depth++ >= S.max_depth) {
+        if (lc.depth++ >= S.max_depth) {
           if (Debug) env.event(ln, VPT_EV_SCATTER_TERMINATED, nullptr, nullptr, 0.0f);
-          ln.terminated = 1;
+          lc.terminated = 1;
           ln.state = ST_FINISH;
         } else {
           if (Debug) env.tally(CNT_SCATTERS, 1);
           // The next primary ray starts at the scatter point (worker.cpp:179): keep it in ro.
-          for (int i = 0; i < 3; ++i) ln.ro[i] = cp[i];
+          for (int i = 0; i < 3; ++i) lc.ro[i] = cp[i];
           // sample_Ld (worker.cpp:52-90)
           if (S.li_zero) {
             ln.Tr = -1.0f;  // returns Li == 0 without draws
@@ -789,6 +798,7 @@ __host__ __device__ __forceinline__ ScenePtr opaque(ScenePtr p) {
 template <bool HasTemp, bool Debug, class Env>
 __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, Env& env) {
   env.prof(PB_ITER);
+  LaneCold& lc = env.cold();
   // Every block reads the scene constants it needs afresh (scalar loads behind opaque(), see
   // ScenePtr): nothing stays live in SGPRs across the whole loop, so the walk keeps its own.
   int32_t gate_min;
@@ -821,25 +831,25 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       env.prof(PB_NEE_DONE);
       if (ln.Tr >= 0.0f) {
         // p * T_ray * Li with p = HG(w . wi)
-        float c = ln.rd[0] * S.wi[0] + (ln.rd[1] * S.wi[1] + ln.rd[2] * S.wi[2]);
+        float c = lc.rd[0] * S.wi[0] + (lc.rd[1] * S.wi[1] + lc.rd[2] * S.wi[2]);
         float p = hg_eval(S, c);
         float pt = p * ln.Tr;
-        ln.L[0] = ln.L[0] + pt * S.Li[0];
-        ln.L[1] = ln.L[1] + pt * S.Li[1];
-        ln.L[2] = ln.L[2] + pt * S.Li[2];
+        lc.L[0] = lc.L[0] + pt * S.Li[0];
+        lc.L[1] = lc.L[1] + pt * S.Li[1];
+        lc.L[2] = lc.L[2] + pt * S.Li[2];
       } else {
-        ln.L[0] = ln.L[0] + 0.0f;
-        ln.L[1] = ln.L[1] + 0.0f;
-        ln.L[2] = ln.L[2] + 0.0f;
+        lc.L[0] = lc.L[0] + 0.0f;
+        lc.L[1] = lc.L[1] + 0.0f;
+        lc.L[2] = lc.L[2] + 0.0f;
       }
       float u0 = rng_uniform(ln.rng);
       float u1 = rng_uniform(ln.rng);
       if (Debug) env.tally(CNT_RNG_DRAWS, 2);
       float nd[3];
-      sample_hg(S, ln.rd, u0, u1, nd);
-      for (int i = 0; i < 3; ++i) ln.rd[i] = nd[i];
-      if (Debug) env.event(ln, VPT_EV_SCATTER, ln.ro, ln.rd, 0.0f);
-      ++ln.depth;  // the for-loop increment (worker.cpp:130)
+      sample_hg(S, lc.rd, u0, u1, nd);
+      for (int i = 0; i < 3; ++i) lc.rd[i] = nd[i];
+      if (Debug) env.event(ln, VPT_EV_SCATTER, lc.ro, lc.rd, 0.0f);
+      ++lc.depth;  // the for-loop increment (worker.cpp:130)
       ln.shadow = 0;
       ln.state = ST_RAY;
     }
@@ -851,15 +861,15 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
     (void)G;
     if (go(ST_FINISH)) {
       env.prof(PB_FINISH);
-      if (!ln.terminated) {
-        ln.L[0] = ln.L[0] + S.le_inf[0];
-        ln.L[1] = ln.L[1] + S.le_inf[1];
-        ln.L[2] = ln.L[2] + S.le_inf[2];
+      if (!lc.terminated) {
+        lc.L[0] = lc.L[0] + S.le_inf[0];
+        lc.L[1] = lc.L[1] + S.le_inf[1];
+        lc.L[2] = lc.L[2] + S.le_inf[2];
       }
       // the pixel just traced is pix - 1 of the tile
-      const int32_t rw = min(S.W - ln.x0, S.tw);
-      const int32_t q = (ln.pix & kPixelMask) - 1, y = div_pix(q, rw);
-      env.film_add(S, ln, ln.x0 + (q - y * rw), ln.y0 + y, rw);
+      const int32_t rw = min(S.W - lc.x0, S.tw);
+      const int32_t q = (lc.pix & kPixelMask) - 1, y = div_pix(q, rw);
+      env.film_add(S, ln, lc.x0 + (q - y * rw), lc.y0 + y, rw);
       env.tally(CNT_SAMPLES, 1);
       ln.state = ST_PIXEL;
     }
@@ -889,9 +899,9 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       uint64_t jid = env.jid_begin + j;
       ln.rng = job_seed(S.seed, S.pixel_mode ? jid * S.tile_area + p : jid);
       uint64_t tile = jid % S.T;
-      ln.x0 = (int32_t)(tile % S.ntx) * S.tw;  // TileProvider::compute_tile_rect
-      ln.y0 = (int32_t)(tile / S.ntx) * S.th;
-      ln.pix = S.pixel_mode ? (int32_t)p | kOnePixel : 0;
+      lc.x0 = (int32_t)(tile % S.ntx) * S.tw;  // TileProvider::compute_tile_rect
+      lc.y0 = (int32_t)(tile / S.ntx) * S.th;
+      lc.pix = S.pixel_mode ? (int32_t)p | kOnePixel : 0;
       if (HasTemp) {
         ln.temp_cell.i = kNoCell;
         ln.temp_cell.code = -1;
@@ -907,23 +917,23 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
     if (go(ST_PIXEL)) {
       env.prof(PB_PIXEL);
       // Clipped tile extent (tile_provider.cpp:102): recomputed, not stored.
-      const int32_t rw = min(S.W - ln.x0, S.tw);
-      const int32_t rh = min(S.H - ln.y0, S.th);
+      const int32_t rw = min(S.W - lc.x0, S.tw);
+      const int32_t rh = min(S.H - lc.y0, S.th);
       // Skip pixels filtered by single_pixel mode without any draw (worker.cpp:113-116).
       int32_t px, py;
-      const int32_t one = ln.pix & kOnePixel;
-      int32_t q = ln.pix & kPixelMask;
-      const int32_t end = one ? ((ln.pix & kPixelTaken) ? 0 : min(q + 1, rw * rh)) : rw * rh;
+      const int32_t one = lc.pix & kOnePixel;
+      int32_t q = lc.pix & kPixelMask;
+      const int32_t end = one ? ((lc.pix & kPixelTaken) ? 0 : min(q + 1, rw * rh)) : rw * rh;
       while (true) {
         if (q >= end) {
           ln.state = ST_FETCH;
           return;
         }
         int32_t y = div_pix(q, rw);
-        px = ln.x0 + (q - y * rw);
-        py = ln.y0 + y;
+        px = lc.x0 + (q - y * rw);
+        py = lc.y0 + y;
         ++q;
-        ln.pix = q | (one ? (kOnePixel | kPixelTaken) : 0);
+        lc.pix = q | (one ? (kOnePixel | kPixelTaken) : 0);
         if (!S.single_pixel_enabled || (px == S.sp_x && py == S.sp_y)) break;
       }
       float jx = rng_uniform(ln.rng);
@@ -943,15 +953,15 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         dv[2] = math::div_by_recip(dv[2], s, rs);
       }
       for (int i = 0; i < 3; ++i) {
-        ln.ro[i] = S.cam_pos[i];
-        ln.rd[i] = dv[i];
-        ln.L[i] = 0.0f;
+        lc.ro[i] = S.cam_pos[i];
+        lc.rd[i] = dv[i];
+        lc.L[i] = 0.0f;
       }
-      ln.terminated = 0;
-      ln.depth = 0;
+      lc.terminated = 0;
+      lc.depth = 0;
       ln.shadow = 0;
       ln.state = ST_RAY;
-      if (Debug) env.event(ln, VPT_EV_NEW_RAY, ln.ro, ln.rd, 0.0f);
+      if (Debug) env.event(ln, VPT_EV_NEW_RAY, lc.ro, lc.rd, 0.0f);
     }
   }
   env.tick(PT_PIXEL);
@@ -964,12 +974,12 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
     if (go2(ST_RAY, ST_SHADOW)) {
       env.prof(PB_RAY);
       const bool primary = ln.state == ST_RAY;
-      if (primary && !(ln.depth < S.max_depth)) {
+      if (primary && !(lc.depth < S.max_depth)) {
         ln.state = ST_FINISH;  // for (depth < max_depth) exhausted
       } else {
         RayDir rd;
         if (primary) {
-          rd = ray_dir_setup(G, ln.rd);
+          rd = ray_dir_setup(G, lc.rd);
         } else {
           for (int i = 0; i < 3; ++i) {
             rd.d[i] = S.sh_d[i];
@@ -979,7 +989,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
           rd.scale = S.sh_scale;
           rd.rscale = S.sh_rscale;
         }
-        if (begin_ray(G, ln, ln.ro, rd)) {
+        if (begin_ray(G, ln, lc.ro, rd)) {
           if (Debug && !primary) env.tally(CNT_SHADOW_RAYS, 1);
           ln.state = ST_SAMPLE;
         } else {
@@ -1086,13 +1096,15 @@ __host__ __device__ __forceinline__ void lane_init(Lane& ln) {
   ln.state = ST_FETCH;
   ln.sm = SM_NEED_SEG;
   ln.shadow = 0;
-  ln.terminated = 0;
   ln.dens_cell.i = kNoCell;
   ln.dens_cell.code = -1;
   ln.temp_cell.i = kNoCell;
   ln.temp_cell.code = -1;
   ln.n_dda = 0;
-  ln.n_stencil = 0;
+}
+__host__ __device__ __forceinline__ void cold_init(LaneCold& lc) {
+  lc.terminated = 0;
+  lc.n_stencil = 0;
 }
 
 }  // namespace vpt
