@@ -35,12 +35,12 @@ int set_error(int code, const std::string& msg) {
 
 constexpr int kCounterCount = CNT_COUNT;
 constexpr int kBlockThreads = 256;
-// Minimum waves per SIMD (launch bounds): 6 for the production density-only kernel (80 VGPRs; the
+// Minimum waves per SIMD (launch bounds): 7 for the production density-only kernel (72 VGPRs; the
 // cold lane state lives in LDS, see LaneCold); 4 for the temperature and per-sample-record
 // variants.  The kernel is latency-bound enough that occupancy pays: persistent grids of 3/4/5
-// blocks per CU measured 802/956/1067 Msps on C3 with one binary, and 6 waves 1115.
+// blocks per CU measured 802/956/1067 Msps on C3 with one binary; 6 waves 1155, 7 waves 1194.
 #ifndef VPT_WAVES_FAST
-#define VPT_WAVES_FAST 6
+#define VPT_WAVES_FAST 7
 #endif
 #ifndef VPT_WAVES_SLOW
 #define VPT_WAVES_SLOW 4

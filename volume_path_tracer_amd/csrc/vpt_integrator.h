@@ -373,6 +373,9 @@ struct LaneCold {
   float ro[3], rd[3];  // current primary world ray; ro is also the scatter point during NEE
   int32_t terminated;
   uint32_t n_stencil;  // stencil refreshes (flushed by the kernel at exit)
+  StencilCell dens_cell;  // the density sampler's last stencil cell (collision evaluation only)
+  float Tr;               // shadow-ray transmittance (< 0: sample_Ld returns zero)
+  float y_draw;           // 1 - u of a free-flight draw whose exact distance is pending (SM_EVAL)
 };
 
 struct Lane {
@@ -380,9 +383,8 @@ struct Lane {
   uint64_t rng;
   uint64_t jid_local;  // job index relative to jid_begin (records / events only)
   uint32_t n_events;   // events logged so far in this job (event traces only)
-  float Tr;            // shadow-ray transmittance (< 0: sample_Ld returns zero)
   // RayMajorantIterator: index-space ray, scale, majorant, HDDA (NanoVDB math::HDDA state)
-  float e[3], d[3], inv[3];
+  float e[3], d[3];  // (invDir = rcp_rn(d) is recomputed where HDDA::update needs it)
   float scale, rscale;  // m_scale and recip_for_div(m_scale)
   float maj;
   int32_t dim;
@@ -393,8 +395,7 @@ struct Lane {
   int32_t vinc[3];  // HDDA: dim * step[axis]
   // current majorant segment
   float s_t0, s_t1, s_dmaj;
-  float y_draw;  // 1 - u of a free-flight draw whose exact distance is pending (SM_EVAL)
-  StencilCell dens_cell, temp_cell;
+  StencilCell temp_cell;
   uint32_t n_dda;  // hot counter, per lane (flushed by the kernel at exit)
 };
 
@@ -459,9 +460,6 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
   ln.d[0] = dx;
   ln.d[1] = dy;
   ln.d[2] = dz;
-  ln.inv[0] = ix;
-  ln.inv[1] = iy;
-  ln.inv[2] = iz;
   ln.scale = rd.scale;
   ln.rscale = rd.rscale;
   // HDDA(ray, max(8, getDim(floor(ray.start())))) -> init(ray, t0, t1, dim)
@@ -488,8 +486,6 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
       ln.nxt[a] = t0 + ((float)v - P[a]) * I[a];
   }
   ln.sm = SM_NEED_SEG;
-  ln.dens_cell.i = kNoCell;
-  ln.dens_cell.code = -1;
   return true;
 }
 
@@ -555,12 +551,13 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
     const float P[3] = {ln.e[0] + ln.d[0] * ln.T0, ln.e[1] + ln.d[1] * ln.T0, ln.e[2] + ln.d[2] * ln.T0};
     for (int b = 0; b < 3; ++b) ln.vox[b] = ((int32_t)floorf(P[b])) & (~(nd - 1));
     for (int b = 0; b < 3; ++b) {
-      const int32_t st = hdda_stp(ln.d[b], ln.inv[b]);
-      ln.finc[b] = (float)nd * fabsf(ln.inv[b]);
+      const float inv = math::rcp_rn(ln.d[b]);  // == the ray's invDir (begin_ray / scene_finalize)
+      const int32_t st = hdda_stp(ln.d[b], inv);
+      ln.finc[b] = (float)nd * fabsf(inv);
       ln.vinc[b] = nd * st;
       if (st == 0) continue;
-      float n = ln.T0 + ((float)ln.vox[b] - P[b]) * ln.inv[b];
-      if (st > 0) n += (float)nd * ln.inv[b];
+      float n = ln.T0 + ((float)ln.vox[b] - P[b]) * inv;
+      if (st > 0) n += (float)nd * inv;
       ln.nxt[b] = n;
     }
   }
@@ -648,7 +645,7 @@ __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const
   {
     // The draw's exact free-flight distance, deferred from SM_DRAW (majorant_transmittance_sampler.cpp:44-45):
     // dt = -log(1 - u) / sigma_maj (random.hpp:20-22), t = t0 + dt / m_scale.
-    const float dt_m = -math::logf_glibc_unit(ln.y_draw) / sigma_maj;
+    const float dt_m = -math::logf_glibc_unit(lc.y_draw) / sigma_maj;
     const float tc = ln.s_t0 + math::div_by_recip(dt_m, ln.scale, ln.rscale);  // == dt_m / m_scale
     if (!(tc < ln.s_t1)) {  // overshoot after all: drop the segment
       ln.sm = SM_NEED_SEG;
@@ -661,7 +658,7 @@ __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const
   float pi_x = ln.e[0] + ln.d[0] * t, pi_y = ln.e[1] + ln.d[1] * t, pi_z = ln.e[2] + ln.d[2] * t;
   float dens;
   if (Debug) env.tally(CNT_DENSITY_EVALS, 1);
-  if (trilinear(G, ln.dens_cell, pi_x, pi_y, pi_z, dens)) ++lc.n_stencil;
+  if (trilinear(G, lc.dens_cell, pi_x, pi_y, pi_z, dens)) ++lc.n_stencil;
   ln.sm = SM_DRAW;  // density <= 0, a null event or an unkilled shadow ray: keep drawing
   if (dens > 0.0f) {
     float cp[3];
@@ -712,10 +709,10 @@ __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const
           for (int i = 0; i < 3; ++i) lc.ro[i] = cp[i];
           // sample_Ld (worker.cpp:52-90)
           if (S.li_zero) {
-            ln.Tr = -1.0f;  // returns Li == 0 without draws
+            lc.Tr = -1.0f;  // returns Li == 0 without draws
             ln.state = ST_NEE_DONE;
           } else {
-            ln.Tr = 1.0f;
+            lc.Tr = 1.0f;
             ln.shadow = 1;
             ln.state = ST_SHADOW;
           }
@@ -727,17 +724,17 @@ __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const
       env.prof(PB_SHADOW_HIT);
       // Ratio tracking with Russian roulette (worker.cpp:68-85)
       float sigma_n = fmaxf(0.0f, sigma_maj - S.sigma_t * dens);
-      ln.Tr *= sigma_n / sigma_maj;
-      if (ln.Tr <= 0.05f) {
+      lc.Tr *= sigma_n / sigma_maj;
+      if (lc.Tr <= 0.05f) {
         float q = 0.75f;
         if (Debug) env.tally(CNT_RNG_DRAWS, 1);
         if (rng_uniform(ln.rng) < q)
-          ln.Tr = 0.0f;
+          lc.Tr = 0.0f;
         else
-          ln.Tr /= 1 - q;
+          lc.Tr /= 1 - q;
       }
-      if (ln.Tr <= 0.0f) {
-        ln.Tr = -1.0f;  // returns Zero()
+      if (lc.Tr <= 0.0f) {
+        lc.Tr = -1.0f;  // returns Zero()
         ln.state = ST_NEE_DONE;
       }
     }
@@ -829,11 +826,11 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
     (void)G;
     if (go(ST_NEE_DONE)) {
       env.prof(PB_NEE_DONE);
-      if (ln.Tr >= 0.0f) {
+      if (lc.Tr >= 0.0f) {
         // p * T_ray * Li with p = HG(w . wi)
         float c = lc.rd[0] * S.wi[0] + (lc.rd[1] * S.wi[1] + lc.rd[2] * S.wi[2]);
         float p = hg_eval(S, c);
-        float pt = p * ln.Tr;
+        float pt = p * lc.Tr;
         lc.L[0] = lc.L[0] + pt * S.Li[0];
         lc.L[1] = lc.L[1] + pt * S.Li[1];
         lc.L[2] = lc.L[2] + pt * S.Li[2];
@@ -989,6 +986,8 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
           rd.scale = S.sh_scale;
           rd.rscale = S.sh_rscale;
         }
+        lc.dens_cell.i = kNoCell;  // a new sampler (and its stencil cache) per ray
+        lc.dens_cell.code = -1;
         if (begin_ray(G, ln, lc.ro, rd)) {
           if (Debug && !primary) env.tally(CNT_SHADOW_RAYS, 1);
           ln.state = ST_SAMPLE;
@@ -1069,7 +1068,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         if (math::neg_log2_hw(y) > thr && D >= 0x1p-96f && ln.rscale == ln.rscale) {
           ln.sm = SM_NEED_SEG;
         } else {
-          ln.y_draw = y;
+          lc.y_draw = y;
           ln.sm = SM_EVAL;
         }
       }
@@ -1096,8 +1095,6 @@ __host__ __device__ __forceinline__ void lane_init(Lane& ln) {
   ln.state = ST_FETCH;
   ln.sm = SM_NEED_SEG;
   ln.shadow = 0;
-  ln.dens_cell.i = kNoCell;
-  ln.dens_cell.code = -1;
   ln.temp_cell.i = kNoCell;
   ln.temp_cell.code = -1;
   ln.n_dda = 0;
@@ -1105,6 +1102,8 @@ __host__ __device__ __forceinline__ void lane_init(Lane& ln) {
 __host__ __device__ __forceinline__ void cold_init(LaneCold& lc) {
   lc.terminated = 0;
   lc.n_stencil = 0;
+  lc.dens_cell.i = kNoCell;
+  lc.dens_cell.code = -1;
 }
 
 }  // namespace vpt
