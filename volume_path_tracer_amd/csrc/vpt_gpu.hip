@@ -36,14 +36,17 @@ int set_error(int code, const std::string& msg) {
 constexpr int kCounterCount = CNT_COUNT;
 constexpr int kBlockThreads = 256;
 // Minimum waves per SIMD (launch bounds): 7 for the production density-only kernel (72 VGPRs; the
-// cold lane state lives in LDS, see LaneCold); 4 for the temperature and per-sample-record
-// variants.  The kernel is latency-bound enough that occupancy pays: persistent grids of 3/4/5
+// cold lane state lives in LDS, see LaneCold), 6 for the temperature kernel (C4: 3748 Msps at its
+// natural 5, 3809 at 6, 3684 at 7), 4 for the per-sample-record / event variants.  The kernel is latency-bound enough that occupancy pays: persistent grids of 3/4/5
 // blocks per CU measured 802/956/1067 Msps on C3 with one binary; 6 waves 1155, 7 waves 1194.
 #ifndef VPT_WAVES_FAST
 #define VPT_WAVES_FAST 7
 #endif
 #ifndef VPT_WAVES_SLOW
 #define VPT_WAVES_SLOW 4
+#endif
+#ifndef VPT_WAVES_TEMP
+#define VPT_WAVES_TEMP 6
 #endif
 
 // The lanes' cold state (vpt_integrator.h LaneCold), one slot per thread of the integrator's block.
@@ -159,7 +162,7 @@ struct KernelEnv {
 
 // counters[] order = vpt_counters field order
 template <bool HasTemp, bool Debug>
-__global__ __launch_bounds__(kBlockThreads, (HasTemp || Debug) ? VPT_WAVES_SLOW : VPT_WAVES_FAST) void vpt_integrate_kernel(const DevScene* scene, KernelEnv env,
+__global__ __launch_bounds__(kBlockThreads, Debug ? VPT_WAVES_SLOW : (HasTemp ? VPT_WAVES_TEMP : VPT_WAVES_FAST)) void vpt_integrate_kernel(const DevScene* scene, KernelEnv env,
                                                                        unsigned long long* counters) {
   __shared__ unsigned long long wg_counters[kCounterCount];
   if (threadIdx.x < kCounterCount) wg_counters[threadIdx.x] = 0;
