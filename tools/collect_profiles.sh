@@ -4,6 +4,6 @@ set -e
 TAG=${1:-r01}; O=gpurun_out/$TAG
 cp $O/${TAG}_pmc.json profiles/${TAG}_pmc.json
 cp $(find $O/prof -name "*kernel_stats.csv" | head -1) profiles/${TAG}_c3_kernel_stats.csv
-tail -1 $O/rocprof.log > profiles/${TAG}_c3_rocprof_bench.json
+grep "\"metric\"" $O/rocprof.log | tail -1 > profiles/${TAG}_c3_rocprof_bench.json
 cp $O/bench.log profiles/${TAG}_c3_bench.log
 ls -la profiles/
