@@ -1,0 +1,10 @@
+# exact short sequences in HG sampling / evaluation (VPT_HGX): parity, A/B on C3 and C4
+export TMPDIR=/tmp; O=gpurun_out/r01ao; mkdir -p $O
+VPT_LIB=$PWD/volume_path_tracer_amd/lib/libvpt_amd_hgx.so timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest_rsm.log 2>&1; rc=$?
+echo "pytest rsm rc=$rc"; tail -1 $O/pytest_rsm.log; [ $rc -ne 0 ] && exit $rc
+for R in 1 2; do for L in libvpt_amd libvpt_amd_hgx; do
+  VPT_LIB=$PWD/volume_path_tracer_amd/lib/$L.so timeout -k 10 200 python tools/tune.py --spp 256 --gates 8:12:32:4 --reps 2 > $O/$L.$R.log 2>&1 || exit $?
+  echo "c3 $L $(grep Msps $O/$L.$R.log | tail -1 | cut -c100-200)"
+  VPT_LIB=$PWD/volume_path_tracer_amd/lib/$L.so timeout -k 10 200 python tools/tune.py --config c4 --spp 256 --gates 8:12:32:4 --reps 2 > $O/$L.c4.$R.log 2>&1 || exit $?
+  echo "c4 $L $(grep Msps $O/$L.c4.$R.log | tail -1 | cut -c100-200)"
+done; done
