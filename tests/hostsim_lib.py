@@ -27,6 +27,8 @@ def lib():
         L.vpths_render_jobs_order.argtypes = [cfgp, gp, gp, fp, C.c_uint64, C.c_uint64, fp, fp,
                                               C.POINTER(Counters), C.c_int, C.POINTER(C.c_uint32), C.c_int]
         L.vpths_probe.argtypes = [gp, C.POINTER(C.c_int32), C.c_int, fp, C.POINTER(C.c_int32), fp]
+        L.vpths_check_runs.argtypes = [gp, C.POINTER(C.c_int64), C.POINTER(C.c_double)]
+        L.vpths_check_runs.restype = C.c_int64
         L.vpths_math_mismatches.argtypes = [C.c_int]
         L.vpths_math_mismatches.restype = C.c_int64
         L.vpths_pow2_mismatches.restype = C.c_int64

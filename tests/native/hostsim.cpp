@@ -68,6 +68,7 @@ extern "C" int vpths_render_jobs_order(const vpt_configuration* cfg, const vpt_g
   if (rc) return rc;
   vpt::HostGrid hd, ht;
   if ((rc = vpt::build_host_grid(*density, true, 0, hd))) return rc;
+  vpt::compute_runs(hd, 0);  // the density-only path runs the Runs variant (run skipping) here
   S.density = hd.dev;
   vpt::scene_finalize(S);
   if (temperature) {
@@ -99,9 +100,9 @@ extern "C" int vpths_render_jobs_order(const vpt_configuration* cfg, const vpt_g
   vpt::lane_init(ln);
   vpt::cold_init(env.cold());
   if (temperature)
-    while (ln.state != vpt::ST_DONE) vpt::lane_iteration<true, true>(&S, ln, env);
+    while (ln.state != vpt::ST_DONE) vpt::lane_iteration<true, true, false>(&S, ln, env);
   else
-    while (ln.state != vpt::ST_DONE) vpt::lane_iteration<false, true>(&S, ln, env);
+    while (ln.state != vpt::ST_DONE) vpt::lane_iteration<false, true, true>(&S, ln, env);
   env.cnt[vpt::CNT_DDA_STEPS] += ln.n_dda;
   env.cnt[vpt::CNT_STENCILS] += env.cold().n_stencil;
   if (counters) {
@@ -147,6 +148,49 @@ extern "C" int vpths_probe(const vpt_grid_desc* d, const int32_t* ijk, int n, fl
     maj[q] = vpt::majorant_of(c);
   }
   return 0;
+}
+
+// Run radii (vpt::compute_runs) checked by brute force: every cell within Chebyshev distance r of a
+// cell with radius r is in the table, interior, and has the same majorant bits.  hist[r] = cells
+// with radius r (r = 0..15); *fraction = HostGrid::run_fraction; returns the violations.
+extern "C" int64_t vpths_check_runs(const vpt_grid_desc* d, int64_t* hist, double* fraction) {
+  vpt::HostGrid h;
+  if (vpt::build_host_grid(*d, true, 0, h)) return -1;
+  vpt::compute_runs(h, 0);
+  *fraction = h.run_fraction;
+  const vpt::DevGrid& G = h.dev;
+  const int64_t nx = G.r8_n[0], ny = G.r8_n[1], nz = G.r8_n[2];
+  auto at = [&](int64_t a, int64_t b, int64_t c) { return ((size_t)a * ny + b) * nz + c; };
+  auto maj_bits = [&](size_t q) {
+    float v;
+    std::memcpy(&v, &h.cells8[q].y, 4);
+    const float m = vpt::majorant_of(vpt::Cell{vpt::cell8_code(h.cells8[q].x), v});
+    uint32_t u;
+    std::memcpy(&u, &m, 4);
+    return u;
+  };
+  int64_t bad = 0;
+  for (int r = 0; r <= 15; ++r) hist[r] = 0;
+  if (h.runs8.size() != h.cells8.size()) return -2;
+  for (int64_t a = 0; a < nx; ++a)
+    for (int64_t b = 0; b < ny; ++b)
+      for (int64_t c = 0; c < nz; ++c) {
+        const size_t q = at(a, b, c);
+        const int r = h.runs8[q];
+        if (r > 15) return -3;
+        ++hist[r];
+        for (int64_t x = a - r; x <= a + r && r > 0; ++x)
+          for (int64_t y = b - r; y <= b + r; ++y)
+            for (int64_t z = c - r; z <= c + r; ++z) {
+              if (x < 0 || y < 0 || z < 0 || x >= nx || y >= ny || z >= nz) {
+                ++bad;
+                continue;
+              }
+              const size_t f = at(x, y, z);
+              if (!vpt::cell8_interior(h.cells8[f].x) || maj_bits(f) != maj_bits(q)) ++bad;
+            }
+      }
+  return bad;
 }
 
 // The math clones vs glibc, over every input the integrator can produce.

@@ -76,3 +76,24 @@ def test_trilinear_matches_oracle():
     for p in rng.uniform(-2, 66, size=(500, 3)).astype(np.float32):
         v = og.sample(*[float(x) for x in p])
         assert np.isfinite(v)
+
+
+@pytest.mark.parametrize("which", ["cloud128", "cloud256", "constant", "sparse", "tiles_only"])
+def test_run_radii_hold(which):
+    """Run radii (compute_runs) let the Runs kernel variant take r HDDA steps without cell loads:
+    every cell within Chebyshev distance r must be interior with the same majorant (brute force).
+    The variant is chosen for grids where >= 1/4 of the interior cells have r >= 2 (C2's constant
+    cube), not for the cloud."""
+    import ctypes as C
+    import grids
+    g = {"cloud128": lambda: SynthGrid(1, 128).grid(), "cloud256": lambda: SynthGrid(1, 256).grid(),
+         "constant": lambda: SynthGrid(0, 128).grid(), "sparse": grids.sparse_grid,
+         "tiles_only": grids.tiles_only_grid}[which]()
+    hist = np.zeros(16, np.int64)
+    frac = C.c_double(0.0)
+    bad = HS.lib().vpths_check_runs(C.byref(g.desc), hist.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(frac))
+    assert bad == 0
+    if which == "constant":
+        assert frac.value >= 0.25 and hist[2:].sum() > 0
+    if which.startswith("cloud"):
+        assert frac.value < 0.25 and hist[1:].sum() > 0

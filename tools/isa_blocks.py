@@ -3,7 +3,7 @@ accesses with their line numbers, and the loop labels, for the production kernel
     python tools/isa_blocks.py [Lb0ELb0E]"""
 import re, sys
 t = open("/tmp/isa/vpt.s").read()
-tag = sys.argv[1] if len(sys.argv) > 1 else "Lb0ELb0E"
+tag = sys.argv[1] if len(sys.argv) > 1 else "Lb0ELb0ELb0E"
 m = re.search(r"^_ZN3vpt20vpt_integrate_kernelI%sEEvPKNS_8DevScene\w*:" % tag, t, re.M)
 seg = t[m.end():]
 seg = seg[:seg.index(".Lfunc_end")]

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -161,7 +162,7 @@ struct KernelEnv {
 };
 
 // counters[] order = vpt_counters field order
-template <bool HasTemp, bool Debug>
+template <bool HasTemp, bool Debug, bool Runs>
 __global__ __launch_bounds__(kBlockThreads, Debug ? VPT_WAVES_SLOW : (HasTemp ? VPT_WAVES_TEMP : VPT_WAVES_FAST)) void vpt_integrate_kernel(const DevScene* scene, KernelEnv env,
                                                                        unsigned long long* counters) {
   __shared__ unsigned long long wg_counters[kCounterCount];
@@ -179,7 +180,7 @@ __global__ __launch_bounds__(kBlockThreads, Debug ? VPT_WAVES_SLOW : (HasTemp ? 
   lane_init(ln);
   cold_init(env.cold());
   const ScenePtr sp = (ScenePtr)scene;
-  while (ln.state != ST_DONE) lane_iteration<HasTemp, Debug>(sp, ln, env);
+  while (ln.state != ST_DONE) lane_iteration<HasTemp, Debug, Runs>(sp, ln, env);
   atomicAdd(wg_counters + CNT_DDA_STEPS, (unsigned long long)ln.n_dda);
   atomicAdd(wg_counters + CNT_STENCILS, (unsigned long long)env.cold().n_stencil);
   __syncthreads();
@@ -272,6 +273,8 @@ __global__ void vpt_tile_cost_kernel(const DevScene* scene, float* cost) {
 // ------------------------------------------------------------------------------------------------
 struct DeviceGrid {
   void* cells8 = nullptr;
+  void* runs8 = nullptr;
+  double run_fraction = 0.0;
   void* cells128 = nullptr;
   void* root = nullptr;
   void* bricks = nullptr;
@@ -292,10 +295,13 @@ static int upload_grid(const HostGrid& h, DeviceGrid& d) {
   d.dev = h.dev;
   int rc;
   if ((rc = upload(h.cells8.data(), h.cells8.size() * sizeof(int2), &d.cells8, d.bytes))) return rc;
+  if ((rc = upload(h.runs8.data(), h.runs8.size(), &d.runs8, d.bytes))) return rc;
+  d.run_fraction = h.run_fraction;
   if ((rc = upload(h.cells128.data(), h.cells128.size() * sizeof(int2), &d.cells128, d.bytes))) return rc;
   if ((rc = upload(h.root.data(), h.root.size() * sizeof(RootTileDev), &d.root, d.bytes))) return rc;
   if ((rc = upload(h.bricks.data(), h.bricks.size() * sizeof(float), &d.bricks, d.bytes))) return rc;
   d.dev.cells8 = (const int2*)d.cells8;
+  d.dev.runs8 = (const uint8_t*)d.runs8;
   d.dev.cells128 = (const int2*)d.cells128;
   d.dev.root = (const RootTileDev*)d.root;
   d.dev.bricks = (const float*)d.bricks;
@@ -304,6 +310,7 @@ static int upload_grid(const HostGrid& h, DeviceGrid& d) {
 
 static void free_grid(DeviceGrid& d) {
   (void)hipFree(d.cells8);
+  (void)hipFree(d.runs8);
   (void)hipFree(d.cells128);
   (void)hipFree(d.root);
   (void)hipFree(d.bricks);
@@ -326,6 +333,7 @@ struct vpt_gpu_ctx {
   unsigned long long* prof = nullptr;
   vpt::DevScene* scene_dev = nullptr;  // the kernel's copy of scene (read through ScenePtr)
   hipStream_t stream = nullptr;
+  bool use_runs = false;             // density-only kernel variant with run skipping (see create)
   int grid_blocks = 0;               // resident capacity (or the set_tuning override)
   int cus = 1;                       // compute units of the device
   bool grid_user = false;            // grid_blocks set by vpt_gpu_set_tuning: use it as is
@@ -456,8 +464,10 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.event_cap = event_cap;
   VPT_HIP(hipMemsetAsync(ctx->job_counter, 0, 2 * sizeof(unsigned long long), s));
   const bool temp = ctx->scene.has_temperature != 0, dbg = records != nullptr || events != nullptr;
-  auto kernel = temp ? (dbg ? vpt::vpt_integrate_kernel<true, true> : vpt::vpt_integrate_kernel<true, false>)
-                     : (dbg ? vpt::vpt_integrate_kernel<false, true> : vpt::vpt_integrate_kernel<false, false>);
+  auto kernel = temp ? (dbg ? vpt::vpt_integrate_kernel<true, true, false> : vpt::vpt_integrate_kernel<true, false, false>)
+                     : ctx->use_runs
+                         ? (dbg ? vpt::vpt_integrate_kernel<false, true, true> : vpt::vpt_integrate_kernel<false, false, true>)
+                         : (dbg ? vpt::vpt_integrate_kernel<false, true, false> : vpt::vpt_integrate_kernel<false, false, false>);
   hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, ctx->scene_dev, env, ctx->counters);
   VPT_HIP(hipGetLastError());
   return VPT_OK;
@@ -490,6 +500,7 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   {
     vpt::HostGrid h;
     if ((rc = vpt::build_host_grid(*density, true, 0, h))) return rc;
+    vpt::compute_runs(h, 0);
     if ((rc = vpt::upload_grid(h, ctx->density))) return rc;
   }
   if (temperature) {
@@ -497,6 +508,11 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
     if ((rc = vpt::build_host_grid(*temperature, false, 0, h))) return rc;
     if ((rc = vpt::upload_grid(h, ctx->temperature))) return rc;
   }
+  // The run-skipping kernel variant is for grids with large equal-majorant regions (C2's constant
+  // cube: 36 % of the interior cells have run radius >= 2; the 512^3 cloud: 4 %, where the variant
+  // would cost more than it skips).  VPT_RUNS=0/1 overrides the choice (A/B).
+  ctx->use_runs = !temperature && ctx->density.run_fraction >= 0.25;
+  if (const char* e = getenv("VPT_RUNS")) ctx->use_runs = !temperature && atoi(e) != 0;
   ctx->scene.density = ctx->density.dev;
   vpt::scene_finalize(ctx->scene);  // uses only the density map (host copy of the values)
   ctx->scene.temperature = ctx->temperature.dev;
@@ -527,7 +543,8 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   int per_cu = 0, cus = 0;
   // sized for the production kernel of this scene; the debug variant is launched with the same grid
   VPT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu, temperature ? vpt::vpt_integrate_kernel<true, false> : vpt::vpt_integrate_kernel<false, false>,
+      &per_cu, temperature ? vpt::vpt_integrate_kernel<true, false, false>
+                           : (ctx->use_runs ? vpt::vpt_integrate_kernel<false, false, true> : vpt::vpt_integrate_kernel<false, false, false>),
       vpt::kBlockThreads, 0));
   VPT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
   if (per_cu < 1) per_cu = 1;

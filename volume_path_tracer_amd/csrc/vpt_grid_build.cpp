@@ -69,6 +69,76 @@ inline int2 enc(int32_t code, float v) {
 
 float host_value_at(const HostGrid& g, int32_t i, int32_t j, int32_t k) { return value_at(g.dev, i, j, k); }
 
+void compute_runs(HostGrid& h, int threads) {
+  if (threads <= 0) threads = default_threads();
+  const DevGrid& G = h.dev;
+  const std::vector<int2>& cells8 = h.cells8;
+  const int32_t nx = G.r8_n[0], ny = G.r8_n[1], nz = G.r8_n[2];
+  const size_t n = cells8.size();
+  h.runs8.assign(n, 0);
+  h.run_fraction = 0.0;
+  h.dev.runs8 = h.runs8.data();
+  if (n == 0 || nx < 3 || ny < 3 || nz < 3) return;
+  auto idx = [&](int64_t a, int32_t b, int32_t c) { return ((size_t)a * ny + b) * nz + c; };
+  std::vector<int8_t> r(n);
+  std::vector<uint32_t> lab(n);
+  parallel_for(nx, threads, [&](int64_t b0, int64_t e0) {
+    for (size_t q = idx(b0, 0, 0); q < idx(e0, 0, 0); ++q) {
+      const int32_t x = cells8[q].x;
+      const float m = majorant_of(Cell{cell8_code(x), math::as_f32((uint32_t)cells8[q].y)});
+      r[q] = (cell8_interior(x) && m == m) ? 0 : -1;
+      lab[q] = math::as_u32(m);
+    }
+  });
+  // erosion pass k: a cell reaches radius k when its 3x3x3 block has radius >= k-1 and one label
+  // (separable over z, y, x, as mark_interior)
+  std::vector<uint8_t> ez(n), ey(n), grow(n);
+  for (int32_t k = 1; k <= 15; ++k) {
+    auto ok = [&](size_t q) { return r[q] >= k - 1; };
+    parallel_for(nx, threads, [&](int64_t b0, int64_t e0) {
+      for (int64_t a = b0; a < e0; ++a)
+        for (int32_t b = 0; b < ny; ++b)
+          for (int32_t c = 0; c < nz; ++c) {
+            const size_t q = idx(a, b, c);
+            ez[q] = c > 0 && c + 1 < nz && ok(q - 1) && ok(q) && ok(q + 1) && lab[q - 1] == lab[q] && lab[q + 1] == lab[q];
+          }
+    });
+    parallel_for(nx, threads, [&](int64_t b0, int64_t e0) {
+      for (int64_t a = b0; a < e0; ++a)
+        for (int32_t b = 0; b < ny; ++b)
+          for (int32_t c = 0; c < nz; ++c) {
+            const size_t q = idx(a, b, c), s = (size_t)nz;
+            ey[q] = b > 0 && b + 1 < ny && ez[q - s] && ez[q] && ez[q + s] && lab[q - s] == lab[q] && lab[q + s] == lab[q];
+          }
+    });
+    std::vector<int64_t> grown_by(nx, 0);
+    parallel_for(nx, threads, [&](int64_t b0, int64_t e0) {
+      for (int64_t a = b0; a < e0; ++a)
+        for (int32_t b = 0; b < ny; ++b)
+          for (int32_t c = 0; c < nz; ++c) {
+            const size_t q = idx(a, b, c), s = (size_t)ny * nz;
+            const bool g = a > 0 && a + 1 < nx && ey[q - s] && ey[q] && ey[q + s] && lab[q - s] == lab[q] && lab[q + s] == lab[q];
+            grow[q] = g;
+            grown_by[a] += g;
+          }
+    });
+    int64_t grown = 0;
+    for (int64_t v : grown_by) grown += v;
+    if (!grown) break;
+    parallel_for(nx, threads, [&](int64_t b0, int64_t e0) {
+      for (size_t q = idx(b0, 0, 0); q < idx(e0, 0, 0); ++q)
+        if (grow[q]) r[q] = (int8_t)k;
+    });
+  }
+  int64_t interior = 0, long_runs = 0;
+  for (size_t q = 0; q < n; ++q) {
+    if (r[q] > 0) h.runs8[q] = (uint8_t)r[q];
+    interior += r[q] >= 0;
+    long_runs += r[q] >= 2;
+  }
+  h.run_fraction = interior ? (double)long_runs / (double)interior : 0.0;
+}
+
 namespace {
 // Sets the interior bit (see cell8_interior) of every cells8 entry whose 3x3x3 neighbourhood lies
 // in the table and holds only dim-8 cells (leaves: code >= 0; lower-node tiles: -16 / -17).

@@ -42,6 +42,7 @@ struct DevGrid {
   int32_t r128_org[3], r128_n[3];    // dense 128^3-cell table over all upper nodes
   int32_t root_count, pad0;
   const int2* cells8;
+  const uint8_t* runs8;  // per cells8 entry: run radius (see mark_runs), for the Runs kernel variant
   const int2* cells128;
   const RootTileDev* root;
   const float* bricks;  // [leaf][9][9][9]: voxel (origin + (x,y,z)) for x,y,z in 0..8 (apron +1)
@@ -489,18 +490,16 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
   return true;
 }
 
-// One iteration of the do-while in RayMajorantIterator::next (volume.cpp:53-71).
-// Returns true when the segment [s_t0, s_t1) with majorant s_dmaj is complete.
-__host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
-  ln.s_dmaj = ln.maj;
-  // HDDA::step(): axis = MinIndex(next).  Written as selects over all three axes: branches (or an
-  // axis index) make the compiler move the HDDA state into an indexed scratch array.
+// HDDA::step() without the time test: axis = MinIndex(next), mNext[axis] += mDim * mDelta[axis],
+// mVoxel[axis] += mDim * mStep[axis]; returns the new time (also stored in T0).  Written as selects
+// over all three axes: branches (or an axis index) make the compiler move the HDDA state into an
+// indexed scratch array.
+__host__ __device__ __forceinline__ float hdda_advance(Lane& ln) {
   const float n0 = ln.nxt[0], n1 = ln.nxt[1], n2 = ln.nxt[2];
   const bool a0 = n0 < n1 && n0 < n2;
   const bool a1 = !a0 && n1 < n2;
   const bool a2 = !a0 && !a1;
   const float tn = a0 ? n0 : (a1 ? n1 : n2);
-  // mNext[axis] += mDim * mDelta[axis]; mVoxel[axis] += mDim * mStep[axis]
   ln.nxt[0] = a0 ? tn + ln.finc[0] : n0;
   ln.nxt[1] = a1 ? tn + ln.finc[1] : n1;
   ln.nxt[2] = a2 ? tn + ln.finc[2] : n2;
@@ -508,6 +507,17 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
   ln.vox[1] += a1 ? ln.vinc[1] : 0;
   ln.vox[2] += a2 ? ln.vinc[2] : 0;
   ln.T0 = tn;
+  return tn;
+}
+
+// One iteration of the do-while in RayMajorantIterator::next (volume.cpp:53-71).
+// Returns true when the segment [s_t0, s_t1) with majorant s_dmaj is complete.
+// Runs: the grid's run radii (runs8) let an interior step that keeps the majorant take the next r
+// HDDA steps without loading their cells (grids with large equal-majorant regions, e.g. C2).
+template <bool Runs = false>
+__host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
+  ln.s_dmaj = ln.maj;
+  const float tn = hdda_advance(ln);
   if (!(tn <= ln.T1)) {
     ln.s_t1 = ln.T1;
     return true;
@@ -526,13 +536,28 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
                   c = (ln.vox[2] - g.r8_org[2]) >> 3;
     if ((uint32_t)a < (uint32_t)g.r8_n[0] && (uint32_t)b < (uint32_t)g.r8_n[1] && (uint32_t)c < (uint32_t)g.r8_n[2]) {
       // one 8-byte load (code + value together)
-      const uint64_t raw = reinterpret_cast<const uint64_t*>(
-          g.cells8)[((uint32_t)a * (uint32_t)g.r8_n[1] + (uint32_t)b) * (uint32_t)g.r8_n[2] + (uint32_t)c];
+      const uint32_t idx = ((uint32_t)a * (uint32_t)g.r8_n[1] + (uint32_t)b) * (uint32_t)g.r8_n[2] + (uint32_t)c;
+      const uint64_t raw = reinterpret_cast<const uint64_t*>(g.cells8)[idx];
+      const int32_t run = Runs ? (int32_t)g.runs8[idx] : 0;
       const int32_t x = (int32_t)(uint32_t)raw;
       const float m = majorant_of(Cell{cell8_code(x), math::as_f32((uint32_t)(raw >> 32))});
       if (cell8_interior(x)) {
         ln.maj = m;
-        if (m == ln.s_dmaj) return false;
+        if (m == ln.s_dmaj) {
+          if (Runs) {
+            // Every cell within Chebyshev distance `run` is interior with this majorant, so the
+            // next `run` iterations would each load a cell, take the fast path and keep going:
+            // take their HDDA steps here (same float operations, same order) without the loads.
+            for (int32_t r = run; r > 0; --r) {
+              ++ln.n_dda;
+              if (!(hdda_advance(ln) <= ln.T1)) {
+                ln.s_t1 = ln.T1;
+                return true;
+              }
+            }
+          }
+          return false;
+        }
         ln.s_t1 = ln.T0;
         return true;
       }
@@ -792,7 +817,7 @@ __host__ __device__ __forceinline__ ScenePtr opaque(ScenePtr p) {
   return p;
 }
 
-template <bool HasTemp, bool Debug, class Env>
+template <bool HasTemp, bool Debug, bool Runs, class Env>
 __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, Env& env) {
   env.prof(PB_ITER);
   LaneCold& lc = env.cold();
@@ -1039,7 +1064,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       if (ln.state == ST_SAMPLE && ln.sm == SM_STEP) {
         env.prof(PB_STEP);
         ++ln.n_dda;
-        if (hdda_step(G, ln)) {
+        if (hdda_step<Runs>(G, ln)) {
           if (Debug) env.tally(CNT_SEGMENTS, 1);
           ln.sm = (ln.s_dmaj <= 0.0f) ? SM_NEED_SEG : SM_DRAW;  // empty segment: no draw (:32-35)
         }

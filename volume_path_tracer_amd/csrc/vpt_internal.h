@@ -20,7 +20,14 @@ struct HostGrid {
   std::vector<RootTileDev> root;
   std::vector<float> bricks;     // [leaf][729]
   std::vector<float> leaf_max;   // fixed majorants
+  std::vector<uint8_t> runs8;    // run radius per cells8 entry (compute_runs; empty until then)
+  double run_fraction = 0.0;     // share of interior cells with a run radius >= 2
 };
+
+// Run radii of the cells8 table (DevGrid::runs8): r(c) = the largest r <= 15 such that every cell
+// within Chebyshev distance r of c is in the table, interior, and has c's majorant (same bits,
+// not NaN).  Sets h.runs8, h.dev.runs8 and h.run_fraction.
+void compute_runs(HostGrid& h, int threads);
 
 // Builds the leaf-slot tables and the 9^3 apron brick pool; fixes the majorants
 // (fix_majorants_for_interpolation, volume.cpp:104-160) when fix == true.
