@@ -212,6 +212,12 @@ extern "C" int64_t vpths_math_mismatches(int which) {
       float phi = 2.0f * 3.14159274f * u;
       if (which == 1 && vpt::math::as_u32(vpt::math::sinf_glibc(phi)) != vpt::math::as_u32(std::sin(phi))) ++bad;
       if (which == 2 && vpt::math::as_u32(vpt::math::cosf_glibc(phi)) != vpt::math::as_u32(std::cos(phi))) ++bad;
+      if (which == 3) {  // the fused clone the HG sampler calls
+        float sn, cs;
+        vpt::math::sincosf_glibc(phi, sn, cs);
+        if (vpt::math::as_u32(sn) != vpt::math::as_u32(std::sin(phi))) ++bad;
+        if (vpt::math::as_u32(cs) != vpt::math::as_u32(std::cos(phi))) ++bad;
+      }
     }
   }
   return bad;

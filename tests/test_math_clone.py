@@ -5,7 +5,8 @@ import pytest
 import hostsim_lib as HS
 
 
-@pytest.mark.parametrize("which,name", [(0, "logf(1-u)"), (1, "sinf(2*pi*u)"), (2, "cosf(2*pi*u)")])
+@pytest.mark.parametrize("which,name", [(0, "logf(1-u)"), (1, "sinf(2*pi*u)"), (2, "cosf(2*pi*u)"),
+                                       (3, "sincosf(2*pi*u) fused")])
 def test_clone_equals_glibc_exhaustive(which, name):
     assert HS.lib().vpths_math_mismatches(which) == 0, name
 

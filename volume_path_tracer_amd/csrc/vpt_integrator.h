@@ -615,7 +615,13 @@ __host__ __device__ __forceinline__ void sample_hg(const DevScene& S, const floa
   float phi = 2.0f * 3.14159274f * u1;
   float sc = sin_theta < -1.0f ? -1.0f : (sin_theta > 1.0f ? 1.0f : sin_theta);
   float cc = cos_theta < -1.0f ? -1.0f : (cos_theta > 1.0f ? 1.0f : cos_theta);
+#ifdef VPT_SEPARATE_SINCOS
   float lx = sc * math::cosf_glibc(phi), ly = sc * math::sinf_glibc(phi), lz = cc;
+#else
+  float sphi, cphi;
+  math::sincosf_glibc(phi, sphi, cphi);
+  float lx = sc * cphi, ly = sc * sphi, lz = cc;
+#endif
   float n2 = lx * lx + (ly * ly + lz * lz);  // local.normalize()
   if (n2 > 0.0f) {
     float s = sqrtf(n2);

@@ -156,6 +156,26 @@ __host__ __device__ __forceinline__ float cosf_glibc(float y) {
   double s = quadrant_sign(n);
   return sinf_poly(x * s, x * x, (n & 2) != 0, n ^ 1);
 }
+// sinf and cosf of one argument with one range reduction and each polynomial evaluated once:
+// sinf uses the sine polynomial for even quadrants and the cosine one for odd, cosf the reverse,
+// on the same reduced argument, so selecting between the two gives both functions' exact values.
+__host__ __device__ __forceinline__ void sincosf_glibc(float y, float& sn, float& cs) {
+  double x = y, xs = y;
+  int n = 0;
+  if (abstop12(y) >= 0x3f4u) {
+    x = reduce_fast(x, &n);
+    xs = x * quadrant_sign(n);
+  }
+  const double x2 = x * x;
+  const float ps = sinf_poly(xs, x2, false, 0);
+  const float pc = sinf_poly(xs, x2, (n & 2) != 0, 1);
+  sn = (n & 1) ? pc : ps;
+  cs = (n & 1) ? ps : pc;
+  if (abstop12(y) < 0x398u) {
+    sn = y;
+    cs = 1.0f;
+  }
+}
 
 // ---- exact short sequences for 1/x, sqrt(x) and a/b ------------------------------------------
 // The IEEE-correct f32 division and square root macros cost ~19 and ~22 v_add_f32 issue slots on
