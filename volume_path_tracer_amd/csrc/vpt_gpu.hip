@@ -550,10 +550,10 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   if (per_cu < 1) per_cu = 1;
   ctx->grid_blocks = per_cu * cus;
   ctx->cus = cus > 0 ? cus : 1;
-  // Scheduling defaults from tools/tune.py sweeps on MI355X (C3, 256 spp): rare states run for >= 8
+  // Scheduling defaults from tools/tune.py sweeps on MI355X (C3, 256 spp): rare states run for >= 6
   // waiting lanes, density evaluations (with the deferred exact draw) for >= 32, everything runs when
   // < 12 lanes are walking; the walk loops while >= 4 lanes walk.
-  ctx->scene.gate_min = 8;
+  ctx->scene.gate_min = 6;
   ctx->scene.gate_idle = 12;
   ctx->scene.gate_eval = 32;
   ctx->scene.gate_walk = 4;
