@@ -595,6 +595,13 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
   return true;
 }
 
+// Walk-loop iterations between two checks of its exit condition (the ballots).  The extra
+// iterations only delay the loop's exit, never a lane's own order of operations.  C3 at 7 waves:
+// 433.5 ms (1) / 427.2 (2) / 423.2 (3) / 424.1 (4); C4 139.8 / 136.5 / 137.3 / 136.5.
+#ifndef VPT_WALK_UNROLL
+#define VPT_WALK_UNROLL 3
+#endif
+
 // Free-flight overshoot pre-test margin (SM_DRAW): RN(log2(e) * (1 + 2^-16)).
 constexpr float kOvershootC = 0x1.7155e8p+0f;
 
@@ -1087,6 +1094,10 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       // wavefront are walking and too few wait on a density evaluation; the other states wait
       // (their gating counts them next outer iteration).  Each lane's own op order is unchanged.
       do {
+#if VPT_WALK_UNROLL > 1
+#pragma unroll
+      for (int rep = 0; rep < VPT_WALK_UNROLL; ++rep) {
+#endif
 #ifdef VPT_PROFILE
       env.prof_add(PB_W_WALK, env.count(ln.state == ST_SAMPLE && ln.sm != SM_EVAL));
       env.prof_add(PB_W_EVAL, env.count(ln.state == ST_SAMPLE && ln.sm == SM_EVAL));
@@ -1146,6 +1157,9 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         }
       }
       env.tick(PT_DRAW);
+#if VPT_WALK_UNROLL > 1
+      }
+#endif
       } while (S.gate_walk > 0 && env.count(ln.state == ST_SAMPLE && ln.sm != SM_EVAL) >= S.gate_walk &&
                env.count(ln.state == ST_SAMPLE && ln.sm == SM_EVAL) < S.gate_eval);
     }
