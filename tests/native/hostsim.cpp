@@ -104,7 +104,6 @@ extern "C" int vpths_render_jobs_order(const vpt_configuration* cfg, const vpt_g
   else
     while (ln.state != vpt::ST_DONE) vpt::lane_iteration<false, true, true>(&S, ln, env);
   env.cnt[vpt::CNT_DDA_STEPS] += ln.n_dda;
-  env.cnt[vpt::CNT_STENCILS] += env.cold().n_stencil;
   if (counters) {
     uint64_t* o = reinterpret_cast<uint64_t*>(counters);
     for (int k = 0; k < vpt::CNT_COUNT; ++k) o[k] += env.cnt[k];

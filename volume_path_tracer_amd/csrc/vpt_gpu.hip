@@ -182,7 +182,6 @@ __global__ __launch_bounds__(kBlockThreads, Debug ? VPT_WAVES_SLOW : (HasTemp ? 
   const ScenePtr sp = (ScenePtr)scene;
   while (ln.state != ST_DONE) lane_iteration<HasTemp, Debug, Runs>(sp, ln, env);
   atomicAdd(wg_counters + CNT_DDA_STEPS, (unsigned long long)ln.n_dda);
-  atomicAdd(wg_counters + CNT_STENCILS, (unsigned long long)env.cold().n_stencil);
   __syncthreads();
   if (threadIdx.x < kCounterCount && wg_counters[threadIdx.x])
     atomicAdd(counters + threadIdx.x, wg_counters[threadIdx.x]);

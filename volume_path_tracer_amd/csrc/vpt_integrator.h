@@ -342,7 +342,8 @@ enum : int32_t {
   ST_NEE_DONE = 4,
   ST_FINISH = 5,  // pixel done: environment light, film
   ST_DONE = 6,
-  ST_SHADOW = 7   // sample_Ld's Volume::intersect + iterator setup (direction wi: constants)
+  ST_SHADOW = 7,  // sample_Ld's Volume::intersect + iterator setup (direction wi: constants)
+  ST_FINISH_T = 8 // pixel done after absorption / scatter past max_depth ("terminated": no env light)
 };
 enum : int32_t { SM_NEED_SEG = 0, SM_STEP = 1, SM_DRAW = 2, SM_EVAL = 3 };  // SM_EVAL: density at s_t0 pending
 // Block ids for the optional SIMT-utilisation profile (env.prof; a no-op unless VPT_PROFILE).
@@ -372,8 +373,6 @@ struct LaneCold {
   uint32_t depth;
   float L[3];
   float ro[3], rd[3];  // current primary world ray; ro is also the scatter point during NEE
-  int32_t terminated;
-  uint32_t n_stencil;  // stencil refreshes (flushed by the kernel at exit)
   StencilCell dens_cell;  // the density sampler's last stencil cell (collision evaluation only)
   float Tr;               // shadow-ray transmittance (< 0: sample_Ld returns zero)
   float y_draw;           // 1 - u of a free-flight draw whose exact distance is pending (SM_EVAL)
@@ -715,13 +714,11 @@ __host__ __device__ __forceinline__ void primary_event(const DevScene& S, const 
   }
   if (ev == 1) {
     if (Debug) env.event(ln, VPT_EV_ABSORBED, nullptr, nullptr, 0.0f);
-    lc.terminated = 1;
-    ln.state = ST_FINISH;
+    ln.state = ST_FINISH_T;
   } else if (ev == 2) {
     if (lc.depth++ >= S.max_depth) {
       if (Debug) env.event(ln, VPT_EV_SCATTER_TERMINATED, nullptr, nullptr, 0.0f);
-      lc.terminated = 1;
-      ln.state = ST_FINISH;
+      ln.state = ST_FINISH_T;
     } else {
       if (Debug) env.tally(CNT_SCATTERS, 1);
       // The next primary ray starts at the scatter point (worker.cpp:179): keep it in ro.
@@ -763,7 +760,7 @@ __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const
   float pi_x = ln.e[0] + ln.d[0] * t, pi_y = ln.e[1] + ln.d[1] * t, pi_z = ln.e[2] + ln.d[2] * t;
   float dens;
   if (Debug) env.tally(CNT_DENSITY_EVALS, 1);
-  if (trilinear(G, lc.dens_cell, pi_x, pi_y, pi_z, dens)) ++lc.n_stencil;
+  env.tally(CNT_STENCILS, trilinear(G, lc.dens_cell, pi_x, pi_y, pi_z, dens) ? 1 : 0);
   ln.sm = SM_DRAW;  // density <= 0, a null event or an unkilled shadow ray: keep drawing
   if (dens > 0.0f) {
     if (!HasTemp) {
@@ -936,9 +933,9 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
     const DevScene S = *opaque(sp);
     const DevGrid& G = S.density;
     (void)G;
-    if (go(ST_FINISH)) {
+    if (go2(ST_FINISH, ST_FINISH_T)) {
       env.prof(PB_FINISH);
-      if (!lc.terminated) {
+      if (ln.state == ST_FINISH) {  // not terminated (worker.cpp:198-200)
         lc.L[0] = lc.L[0] + S.le_inf[0];
         lc.L[1] = lc.L[1] + S.le_inf[1];
         lc.L[2] = lc.L[2] + S.le_inf[2];
@@ -1034,7 +1031,6 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         lc.rd[i] = dv[i];
         lc.L[i] = 0.0f;
       }
-      lc.terminated = 0;
       lc.depth = 0;
       ln.shadow = 0;
       ln.state = ST_RAY;
@@ -1084,7 +1080,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
     const DevGrid& G = S.density;
     (void)G;
 #ifdef VPT_PROFILE
-    const int32_t c_nee = env.count(ln.state == ST_NEE_DONE), c_fin = env.count(ln.state == ST_FINISH),
+    const int32_t c_nee = env.count(ln.state == ST_NEE_DONE), c_fin = env.count(ln.state == ST_FINISH || ln.state == ST_FINISH_T),
                   c_ray = env.count(ln.state == ST_RAY || ln.state == ST_SHADOW),
                   c_pix = env.count(ln.state == ST_PIXEL || ln.state == ST_FETCH), c_done = 64 - env.count(true);
 #endif
@@ -1187,8 +1183,6 @@ __host__ __device__ __forceinline__ void lane_init(Lane& ln) {
   ln.n_dda = 0;
 }
 __host__ __device__ __forceinline__ void cold_init(LaneCold& lc) {
-  lc.terminated = 0;
-  lc.n_stencil = 0;
   lc.dens_cell.i = kNoCell;
   lc.dens_cell.code = -1;
 }
