@@ -6,9 +6,15 @@ cloud stand-in (the reference's wdas_cloud.nvdb is not available).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
 
 One step = one full frame (every wave of the configuration) rendered into a zeroed film on every
-rank, plus — for N > 1 — the RCCL sum of the films over xGMI.  Multi-GPU is weak scaling: rank r
-renders waves r*spp+1 .. (r+1)*spp of the same job space (independent RNG streams per job id), so
-the per-GPU work is fixed and the reduced film is an N*spp-sample image.
+rank, plus — for N > 1 — the RCCL sum of the films over xGMI.
+
+Multi-GPU.  `--gpus N` runs N ranks, one per GPU: under torchrun (WORLD_SIZE must equal N), or, when
+WORLD_SIZE is unset, by starting torch.distributed.run itself before anything touches the GPU.
+  * default `--mode weak` (the driver's SCALE runs): every rank renders its own block of the C3
+    frame's 256 waves (rank r: waves r*256+1 .. (r+1)*256), so N = 1 is exactly BENCH's C3 line and
+    the per-GPU work is fixed;
+  * the 8-GPU configuration of BASELINE.json (configs[4], C5: one 3840x2160 frame at 1024 spp dealt
+    across the GPUs) is `--config c5 --mode strong --gpus 8`.
 
 The JSON line also carries:
   roofline      the integrator kernel's algorithmic bytes per launch (SURVEY §8d:
@@ -50,34 +56,76 @@ def algorithmic_bytes(c: dict) -> int:
     return 32 * c["stencils"] + 8 * c["dda_steps"] + 32 * c["temp_stencils"] + 32 * c["samples"]
 
 
-def cpu_baseline(wl, dens, temp, budget_s: float = 12.0):
-    """Oracle worker pool on this host: whole waves of the workload's frame until ~budget_s."""
+def host_cpu_info() -> dict:
+    """The host's CPUs as this process sees them: nproc, the affinity mask, the cgroup CPU quota
+    (cpu.max, when limited) and the model name."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except Exception:
+        info["affinity"] = os.cpu_count()
+    info["cgroup_cpus"] = None
+    try:
+        quota, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if quota != "max":
+            info["cgroup_cpus"] = round(int(quota) / int(period), 2)
+    except Exception:
+        pass
+    info["cpu_model"] = None
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                info["cpu_model"] = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return info
+
+
+def cpu_baseline(wl, dens, temp, budget_s: float = 15.0, runs: int = 3):
+    """The reference worker pool (main.cpp:62-87, restated headless in the oracle: one std::thread per
+    core calling run() over a TileProvider) on every core of this process's affinity mask, over the
+    DISTINCT waves 1..k of the workload's frame (k sized so that `runs` runs take ~budget_s);
+    the value is the median of the runs' Msamples/s."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib as O
 
-    try:
-        aff = len(os.sched_getaffinity(0))
-    except Exception:
-        aff = os.cpu_count() or 1
-    threads = max(1, min(16, aff, os.cpu_count() or 1))
+    info = host_cpu_info()
+    threads = max(1, info["affinity"] or 1)
     od = O.OracleGrid(dens, fix_majorants=True)
     ot = O.OracleGrid(temp, fix_majorants=False) if temp is not None else None
     cfg = wl.cfg.copy()
-    waves, total_ms = 0, 0.0
-    samples = cfg.width * cfg.height
-    while waves < 16:
-        film, ms, _ = O.render_pool(cfg, od, ot, 1, threads)
-        waves += 1
-        total_ms += ms
-        if total_ms / 1e3 >= budget_s:
-            break
-        # each call renders wave 1 again (same jobs): a fixed, repeatable sample of the frame
-        if total_ms / waves * (waves + 1) / 1e3 > 2.5 * budget_s:
-            break
-    rate = waves * samples / (total_ms / 1e3) / 1e6
-    return {"value": round(rate, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{waves} x wave 1 of {cfg.width}x{cfg.height} ({waves * samples} samples), "
-                      f"oracle worker pool, {threads} threads, {total_ms / 1e3:.1f} s"}
+    per_wave = cfg.width * cfg.height
+    _, ms1, _ = O.render_pool(cfg, od, ot, 1, threads)  # calibration: wave 1
+    k = int(max(1, min(wl.spp, budget_s / runs / max(ms1 / 1e3, 1e-3))))
+    rates, secs = [], []
+    for _ in range(runs):
+        _, ms, _ = O.render_pool(cfg, od, ot, k, threads)
+        rates.append(k * per_wave / (ms / 1e3) / 1e6)
+        secs.append(ms / 1e3)
+    rates.sort()
+    med = rates[len(rates) // 2]
+    return {"value": round(med, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"waves 1..{k} of {cfg.width}x{cfg.height} ({k * per_wave} samples) per run, median of {runs} "
+                      f"runs ({', '.join(f'{r:.3f}' for r in rates)} Msamples/s, {sum(secs):.1f} s), oracle worker "
+                      f"pool (main.cpp:62-87 restated), {threads} threads",
+            "spread": round((rates[-1] - rates[0]) / med, 4), "host": info}
+
+
+def spawn_ranks(args) -> int:
+    """--gpus N without torchrun's environment: start N fresh ranks (this process has not touched the
+    GPU) through torch.distributed.run on 127.0.0.1, and return their exit code."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve()), *sys.argv[1:]]
+    log(f"bench: starting {args.gpus} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd).returncode
 
 
 def main():
@@ -92,22 +140,34 @@ def main():
     ap.add_argument("--rng-mode", choices=["reference", "pixel"], default="reference",
                     help="pixel = throughput mode (per-pixel streams; not the reference's samples)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work (3 runs)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="every rank on device 0 (multi-process tests on a one-GPU box)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}: launch with --nproc-per-node equal to --gpus")
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev_index = 0 if (world == 1 or args.one_device) else local
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from volume_path_tracer_amd import distributed as D
     from volume_path_tracer_amd.render import Integrator
@@ -133,14 +193,13 @@ def main():
 
     def step(timed: bool):
         it.film.zero_()
-        for b, n in ranges:
-            ev0 = torch.cuda.Event(enable_timing=True)
-            ev1 = torch.cuda.Event(enable_timing=True)
-            ev0.record(stream)
-            it.render_jobs(b, n, stream=stream)
-            ev1.record(stream)
-            if timed:
-                launch_ms.append((ev0, ev1))
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)  # the kernel runs on this stream: the events bracket exactly its launches
+        D.render_rank(it, rank, world, spp, args.mode, stream=stream)
+        ev1.record(stream)
+        if timed:
+            launch_ms.append((ev0, ev1))
         D.reduce_film(it.film)
 
     for _ in range(args.warmup):
@@ -157,8 +216,10 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    # scalars travel on the device with RCCL, through the host with gloo
+    sdev = dev if args.backend == "nccl" else torch.device("cpu")
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=sdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -167,15 +228,15 @@ def main():
     area = int(wl.cfg.tile_size[0] * wl.cfg.tile_size[1])
     samples_rank = counters["samples"]
     assert samples_rank == (wl.cfg.width * wl.cfg.height * jobs_rank // it.jobs_per_wave) * args.steps, samples_rank
-    t = torch.tensor([samples_rank], dtype=torch.float64, device=dev)
+    t = torch.tensor([samples_rank], dtype=torch.float64, device=sdev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     total_samples = int(t.item())
     value = total_samples / elapsed / 1e6
-    launches_per_step = len(ranges)
+    launches_per_step = max(1, len(ranges))
 
     if rank == 0:
-        avg_launch_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+        avg_launch_s = sum(kernel_ms) / len(kernel_ms) / 1e3 / launches_per_step
         bytes_per_launch = algorithmic_bytes(counters) / (args.steps * launches_per_step)
         achieved = bytes_per_launch / avg_launch_s / 1e9
         traffic = None

@@ -183,7 +183,15 @@ int vpt_gpu_job_space(const vpt_gpu_ctx* ctx, uint64_t* jobs_per_wave, uint64_t*
  * (a hipStream_t; NULL = the null stream, as everywhere in HIP), accumulating into `film_device`:
  * a device float[H][W][4] (X, Y, Z, sample count; image.hpp:40-60) — NULL = the context's own
  * film.  Film adds are fp32 atomics, so the per-pixel sum order may differ from the
- * reference's wave order (≈1e-7 relative). */
+ * reference's wave order (≈1e-7 relative).
+ *
+ * Concurrency: launches of one context may be in flight on several streams at once.  Each launch
+ * takes its own job counter from a ring of 64 per context; a ring slot is reused only after the
+ * launch that last held it has completed (the new launch's stream waits on an event), so any number
+ * of launches is safe.  Launches that share a film add into it atomically.  The calls that change
+ * context state read by running kernels (vpt_gpu_set_tuning, vpt_gpu_set_rng_mode) and
+ * vpt_gpu_film_clear first wait for all work on the device.  One context is driven by one host
+ * thread at a time (as the reference's `run` owns its RandomNumberGenerator). */
 int vpt_gpu_render_jobs(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count,
                         float* film_device, void* hip_stream);
 
@@ -247,6 +255,15 @@ int vpt_gpu_majorant_trace(vpt_gpu_ctx* ctx, const float origin[3], const float 
  * the reference only in expectation and is never used for parity. */
 enum { VPT_RNG_REFERENCE = 0, VPT_RNG_PIXEL = 1 };
 int vpt_gpu_set_rng_mode(vpt_gpu_ctx* ctx, int mode);
+
+/* Kernel variant of density-only scenes.  The run-skipping variant takes, from an interior cell whose
+ * majorant equals the segment's, the next r HDDA steps without loading their cells (r = the cell's
+ * precomputed run radius); samples are identical.  mode -1 (default): chosen at creation (on when
+ * >= 1/4 of the interior cells have r >= 2, e.g. C2's constant cube); 0: off; 1: on (VPT_E_INVALID
+ * with a temperature grid).  Takes effect at the next launch. */
+int vpt_gpu_set_run_skipping(vpt_gpu_ctx* ctx, int mode);
+/* The production kernel the context launches: temperature grid present, run skipping on. */
+int vpt_gpu_kernel_variant(const vpt_gpu_ctx* ctx, int* has_temperature, int* run_skipping);
 
 /* Scheduling order of a whole-wave job range (jid_begin and jid_count multiples of T).  Results
  * never depend on it: every job keeps its jid and RNG stream, only the fp32 atomic film-add order

@@ -1,0 +1,137 @@
+"""Analytic anchor for the homogeneous medium, independent of the oracle.
+
+C2's constant cube (density 1 on index [0,127]^3, world = index - 64) with sigma_s = 0,
+sigma_a = 0.02 and the distant light off (Li == 0: no NEE, worker.cpp:57-58).  A path is then either
+absorbed (L = 0, `terminated`) or leaves the volume and collects the environment light
+(worker.cpp:198-200), so a pixel's film value / sample count is
+
+    imaging_ratio * Le_inf * E_jitter[ exp(-sigma_a * integral of density along the clipped chord) ]
+
+where the density is NanoVDB's trilinear interpolation of the voxel lattice (1 inside, background 0
+outside): along each index axis f(x) = 1 for x <= 127 and 128 - x on the half-voxel ramp
+(127, 128] up to the clip box's max + 1 face (volume.cpp:83).  The chord integral is exact
+(3-point Gauss-Legendre between the ramp breakpoints; the integrand is a cubic there), and the jitter
+expectation (jitter in [0, 0.5)^2, worker.cpp:121-122) a 12x12 midpoint rule over pixels whose
+transmittance is smooth across the pixel (silhouette pixels are skipped).
+
+This tests the restated NanoVDB/Eigen semantics (HDDA, clip, Map, trilinear, delta tracking) that no
+reference fixture pins: a systematic error there shifts the expectation.  Bar: every pixel within
+5 sigma of its Monte-Carlo error, and the mean z-score within 4 / sqrt(pixels).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from volume_path_tracer_amd.scenes import SynthGrid, workload
+
+SIGMA_A = 0.02
+GL_X = np.array([-np.sqrt(0.6), 0.0, np.sqrt(0.6)])
+GL_W = np.array([5.0, 8.0, 5.0]) / 9.0
+
+
+def analytic_config(w, h, spp):
+    wl = workload("c2", width=w, height=h, spp=spp)
+    v = wl.cfg.volume_parameters
+    v.sigma_s, v.sigma_a = 0.0, SIGMA_A
+    wl.cfg.worker_parameters.distant_light_multiplier = 0.0
+    return wl
+
+
+def chord_optical_depth(o, d):
+    """sigma_a * integral of the trilinear density of the constant 128^3 cube along rays o + t d
+    (index space, |d| = 1: voxel size 1) clipped to [0, 128]^3.  o: [3], d: [n, 3]."""
+    n = d.shape[0]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        inv = 1.0 / d
+        t_a = (0.0 - o) * inv
+        t_b = (128.0 - o) * inv
+    t0 = np.max(np.minimum(t_a, t_b), axis=1).clip(min=0.0)
+    t1 = np.min(np.maximum(t_a, t_b), axis=1)
+    hit = t1 > t0
+    with np.errstate(divide="ignore", invalid="ignore"):
+        br = (127.0 - o) * inv  # where an axis enters its ramp
+    br = np.where(np.isfinite(br), br, t0[:, None])
+    pts = np.sort(np.concatenate([t0[:, None], np.clip(br, t0[:, None], t1[:, None]), t1[:, None]], axis=1), axis=1)
+    tau = np.zeros(n)
+    for k in range(pts.shape[1] - 1):
+        a, b = pts[:, k], pts[:, k + 1]
+        half, mid = 0.5 * (b - a), 0.5 * (a + b)
+        for x, wgt in zip(GL_X, GL_W):
+            t = mid + half * x
+            p = o[None, :] + t[:, None] * d
+            f = np.clip(128.0 - p, 0.0, 1.0).prod(axis=1)
+            tau += wgt * half * f
+    return np.where(hit, SIGMA_A * tau, 0.0)
+
+
+def expected_transmittance(cfg, jit=12):
+    """Per pixel: E over jitter of exp(-tau) and its spread over the jitter points (edge detector)."""
+    lin, trans = np.zeros(9, np.float32), np.zeros(3, np.float32)
+    O.lib().vpto_camera_matrix(C.byref(cfg), O.fptr(lin), O.fptr(trans))
+    L = lin.astype(np.float64).reshape(3, 3)
+    W, H = cfg.width, cfg.height
+    j = (np.arange(jit) + 0.5) / jit * 0.5
+    jx, jy = np.meshgrid(j, j)
+    ys, xs = np.mgrid[0:H, 0:W]
+    rx = (xs[..., None] + 0.5 + jx.reshape(-1)).reshape(-1)
+    ry = (ys[..., None] + 0.5 + jy.reshape(-1)).reshape(-1)
+    dirs = (np.stack([rx, ry, np.zeros_like(rx)], 1) @ L.T) + trans.astype(np.float64)
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    origin = np.asarray(cfg.camera_parameters.position, np.float64) + 64.0  # world -> index
+    tr = np.exp(-chord_optical_depth(origin, dirs)).reshape(H, W, jit * jit)
+    return tr.mean(axis=2), tr.max(axis=2) - tr.min(axis=2)
+
+
+def check_film(cfg, film, spp):
+    le = np.asarray(cfg.worker_parameters.infinite_light_xyz, np.float64) * cfg.worker_parameters.infinite_light_multiplier
+    r = cfg.camera_parameters.imaging_ratio
+    np.testing.assert_array_equal(film[..., 3], spp)
+    est = film[..., 1].astype(np.float64) / film[..., 3] / (r * le[1])
+    t, spread = expected_transmittance(cfg)
+    smooth = spread < 0.02
+    inside = smooth & (t < 0.999)
+    outside = smooth & (t >= 1.0)
+    assert inside.sum() >= 100, inside.sum()
+    np.testing.assert_allclose(est[outside], 1.0, rtol=2e-5)  # fp32 sums of spp equal terms
+    sd = np.sqrt(t * (1 - t) / spp)
+    z = (est - t)[inside] / sd[inside]
+    assert np.abs(z).max() < 5.0, (np.abs(z).max(), z.mean())
+    assert abs(z.mean()) < 4.0 / np.sqrt(z.size), (z.mean(), z.size)
+    return z
+
+
+def test_analytic_expectation_self_check():
+    """The chord integral against brute-force midpoint integration on a few rays."""
+    rng = np.random.default_rng(0)
+    o = np.array([64.3, 61.7, -236.0])
+    d = rng.normal(size=(6, 3)) * [0.15, 0.15, 0.0] + [0, 0, 1]
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    tau = chord_optical_depth(o, d)
+    t = np.linspace(0, 600, 600001)[:-1] + 0.0005
+    for i in range(6):
+        p = o + t[:, None] * d[i]
+        inb = np.all((p >= 0) & (p <= 128), axis=1)
+        f = np.clip(128.0 - p, 0.0, 1.0).prod(axis=1) * inb
+        assert abs(SIGMA_A * f.sum() * 0.001 - tau[i]) < 1e-5
+
+
+def test_oracle_homogeneous_absorption_matches_analytic():
+    """The CPU oracle against the closed form (24x24 pixels, 256 spp)."""
+    wl = analytic_config(24, 24, 256)
+    od = O.OracleGrid(SynthGrid(0, 128).grid(), fix_majorants=True)
+    film, _, _ = O.render_jobs(wl.cfg, od, None, 0, wl.cfg.jobs_per_wave() * 256)
+    check_film(wl.cfg, film, 256)
+
+
+@pytest.mark.gpu
+def test_gpu_homogeneous_absorption_matches_analytic():
+    """The HIP integrator (production kernel, run-skipping variant as C2 selects it) against the
+    closed form: 96x96 pixels at 1024 spp."""
+    from volume_path_tracer_amd.render import Integrator
+
+    wl = analytic_config(96, 96, 1024)
+    it = Integrator(wl.cfg, SynthGrid(0, 128).grid(), None, device=0)
+    it.render_waves(1, 1024)
+    check_film(wl.cfg, it.film_host(), 1024)

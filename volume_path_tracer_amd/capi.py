@@ -233,6 +233,8 @@ def lib() -> C.CDLL:
     L.vpt_gpu_majorant_trace.argtypes = [vp, fp, fp, fp, C.c_int, C.POINTER(C.c_int)]
     L.vpt_dda_trace.argtypes = [C.POINTER(GridDesc), fp, fp, vp, C.c_int, C.POINTER(C.c_int)]
     L.vpt_gpu_set_rng_mode.argtypes = [vp, C.c_int]
+    L.vpt_gpu_set_run_skipping.argtypes = [vp, C.c_int]
+    L.vpt_gpu_kernel_variant.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.vpt_gpu_set_job_order.argtypes = [vp, C.c_int]
     L.vpt_gpu_set_job_order_tail.argtypes = [vp, C.c_int]
     L.vpt_gpu_tile_costs.argtypes = [vp, fp, C.POINTER(C.c_uint32)]

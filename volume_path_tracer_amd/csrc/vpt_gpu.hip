@@ -327,7 +327,14 @@ struct vpt_gpu_ctx {
   float* cie = nullptr;
   float* film = nullptr;
   uint64_t film_count = 0;
-  unsigned long long* job_counter = nullptr;
+  // Per-launch job / event counters: a ring of kLaunchSlots pairs, so launches on different streams
+  // of one context never share a counter.  slot_done[i] is recorded on the stream of the launch
+  // that last used slot i; the next launch to take slot i waits for it on its own stream first.
+  unsigned long long* job_counter = nullptr;  // [kLaunchSlots][2]: jobs, events
+  hipEvent_t slot_done[64] = {};
+  bool slot_used[64] = {};
+  uint32_t next_slot = 0;
+  std::mutex slot_mu;
   unsigned long long* counters = nullptr;
   unsigned long long* prof = nullptr;
   vpt::DevScene* scene_dev = nullptr;  // the kernel's copy of scene (read through ScenePtr)
@@ -346,14 +353,35 @@ struct vpt_gpu_ctx {
 namespace {
 
 constexpr int kProfWords = 2 * vpt::PB_COUNT + vpt::PT_COUNT;
+constexpr uint32_t kLaunchSlots = 64;
 
 int ctx_device(vpt_gpu_ctx* ctx);
 
-// Device copy of the scene constants (between renders: a running kernel reads it).  A pageable
-// hipMemcpy may return before its DMA lands, and the next render may run on another stream: wait.
+// Device copy of the scene constants, which every in-flight launch reads: wait for all work on the
+// device (launches may sit on any stream, including non-blocking ones), copy, and wait again (a
+// pageable hipMemcpy may return before its DMA lands, and the next render may use another stream).
 int push_scene(vpt_gpu_ctx* ctx) {
+  VPT_HIP(hipDeviceSynchronize());
   VPT_HIP(hipMemcpy(ctx->scene_dev, &ctx->scene, sizeof(vpt::DevScene), hipMemcpyHostToDevice));
   VPT_HIP(hipDeviceSynchronize());
+  return VPT_OK;
+}
+
+// The counter pair of the next launch on stream s: ordered after the previous launch that used the
+// same ring slot (whatever stream it ran on), then zeroed on s.
+int take_slot(vpt_gpu_ctx* ctx, hipStream_t s, uint32_t& slot) {
+  std::lock_guard<std::mutex> lock(ctx->slot_mu);
+  slot = ctx->next_slot;
+  ctx->next_slot = (ctx->next_slot + 1) % kLaunchSlots;
+  if (ctx->slot_used[slot]) VPT_HIP(hipStreamWaitEvent(s, ctx->slot_done[slot], 0));
+  VPT_HIP(hipMemsetAsync(ctx->job_counter + 2 * slot, 0, 2 * sizeof(unsigned long long), s));
+  return VPT_OK;
+}
+
+int release_slot(vpt_gpu_ctx* ctx, hipStream_t s, uint32_t slot) {
+  std::lock_guard<std::mutex> lock(ctx->slot_mu);
+  VPT_HIP(hipEventRecord(ctx->slot_done[slot], s));
+  ctx->slot_used[slot] = true;
   return VPT_OK;
 }
 
@@ -376,6 +404,8 @@ void destroy(vpt_gpu_ctx* ctx) {
   (void)hipFree(ctx->prof);
   (void)hipFree(ctx->scene_dev);
   (void)hipFree(ctx->order);
+  for (uint32_t i = 0; i < kLaunchSlots; ++i)
+    if (ctx->slot_done[i]) (void)hipEventDestroy(ctx->slot_done[i]);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -409,7 +439,7 @@ int ensure_order(vpt_gpu_ctx* ctx) {
 }
 
 int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film, float* records, void* stream_ptr,
-           vpt_event* events = nullptr, uint64_t event_cap = 0) {
+           vpt_event* events = nullptr, uint64_t event_cap = 0, uint32_t* slot_out = nullptr) {
   if (!ctx) return vpt::set_error(VPT_E_INVALID, "render: null context");
   int rc = ctx_device(ctx);
   if (rc) return rc;
@@ -424,7 +454,6 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
     if (jid_count > UINT64_MAX / ctx->scene.tile_area) return vpt::set_error(VPT_E_INVALID, "render: job range too large");
     env.jid_count = jid_count * ctx->scene.tile_area;
   }
-  env.job_counter = ctx->job_counter;
   env.film = film ? film : ctx->film;
   env.records = records;
   env.tile_area = ctx->scene.tw * ctx->scene.th;
@@ -458,10 +487,13 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
     env.order_tail_n = tail;
     env.order_tail_k0 = (n - tail) * (uint32_t)T;
   }
+  uint32_t slot = 0;
+  if ((rc = take_slot(ctx, s, slot))) return rc;
+  env.job_counter = ctx->job_counter + 2 * slot;
   env.events = events;
-  env.event_count = ctx->job_counter + 1;
+  env.event_count = ctx->job_counter + 2 * slot + 1;
   env.event_cap = event_cap;
-  VPT_HIP(hipMemsetAsync(ctx->job_counter, 0, 2 * sizeof(unsigned long long), s));
+  if (slot_out) *slot_out = slot;
   const bool temp = ctx->scene.has_temperature != 0, dbg = records != nullptr || events != nullptr;
   auto kernel = temp ? (dbg ? vpt::vpt_integrate_kernel<true, true, false> : vpt::vpt_integrate_kernel<true, false, false>)
                      : ctx->use_runs
@@ -469,7 +501,7 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
                          : (dbg ? vpt::vpt_integrate_kernel<false, true, false> : vpt::vpt_integrate_kernel<false, false, false>);
   hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, ctx->scene_dev, env, ctx->counters);
   VPT_HIP(hipGetLastError());
-  return VPT_OK;
+  return release_slot(ctx, s, slot);
 }
 
 }  // namespace
@@ -509,9 +541,8 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   }
   // The run-skipping kernel variant is for grids with large equal-majorant regions (C2's constant
   // cube: 36 % of the interior cells have run radius >= 2; the 512^3 cloud: 4 %, where the variant
-  // would cost more than it skips).  VPT_RUNS=0/1 overrides the choice (A/B).
+  // would cost more than it skips).  vpt_gpu_set_run_skipping overrides the choice.
   ctx->use_runs = !temperature && ctx->density.run_fraction >= 0.25;
-  if (const char* e = getenv("VPT_RUNS")) ctx->use_runs = !temperature && atoi(e) != 0;
   ctx->scene.density = ctx->density.dev;
   vpt::scene_finalize(ctx->scene);  // uses only the density map (host copy of the values)
   ctx->scene.temperature = ctx->temperature.dev;
@@ -531,7 +562,9 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   ctx->film_count = (uint64_t)cfg->output_size[0] * (uint64_t)cfg->output_size[1] * 4;
   VPT_HIP(hipMalloc((void**)&ctx->film, ctx->film_count * sizeof(float)));
   VPT_HIP(hipMemset(ctx->film, 0, ctx->film_count * sizeof(float)));
-  VPT_HIP(hipMalloc((void**)&ctx->job_counter, 2 * sizeof(unsigned long long)));  // jobs, events
+  VPT_HIP(hipMalloc((void**)&ctx->job_counter, kLaunchSlots * 2 * sizeof(unsigned long long)));  // jobs, events
+  for (uint32_t i = 0; i < kLaunchSlots; ++i)
+    VPT_HIP(hipEventCreateWithFlags(&ctx->slot_done[i], hipEventDisableTiming));
   VPT_HIP(hipMalloc((void**)&ctx->counters, vpt::kCounterCount * sizeof(unsigned long long)));
   VPT_HIP(hipMemset(ctx->counters, 0, vpt::kCounterCount * sizeof(unsigned long long)));
   VPT_HIP(hipMalloc((void**)&ctx->prof, kProfWords * sizeof(unsigned long long)));
@@ -590,11 +623,12 @@ int vpt_gpu_trace_jobs(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count,
                        vpt_event* events_device, uint64_t capacity, uint64_t* count, void* hip_stream) {
   if (!ctx || !events_device || !count) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_trace_jobs: null argument");
   *count = 0;
-  int rc = render(ctx, jid_begin, jid_count, film_device, nullptr, hip_stream, events_device, capacity);
+  uint32_t slot = 0;
+  int rc = render(ctx, jid_begin, jid_count, film_device, nullptr, hip_stream, events_device, capacity, &slot);
   if (rc) return rc;
   if (jid_count == 0) return VPT_OK;
   unsigned long long n = 0;
-  VPT_HIP(hipMemcpyAsync(&n, ctx->job_counter + 1, sizeof n, hipMemcpyDeviceToHost, (hipStream_t)hip_stream));
+  VPT_HIP(hipMemcpyAsync(&n, ctx->job_counter + 2 * slot + 1, sizeof n, hipMemcpyDeviceToHost, (hipStream_t)hip_stream));
   VPT_HIP(hipStreamSynchronize((hipStream_t)hip_stream));
   *count = n;
   return VPT_OK;
@@ -639,6 +673,21 @@ int vpt_gpu_set_rng_mode(vpt_gpu_ctx* ctx, int mode) {
   return push_scene(ctx);
 }
 
+int vpt_gpu_set_run_skipping(vpt_gpu_ctx* ctx, int mode) {
+  if (!ctx || mode < -1 || mode > 1) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_run_skipping: bad argument");
+  if (mode == 1 && ctx->scene.has_temperature)
+    return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_run_skipping: no run-skipping variant with a temperature grid");
+  ctx->use_runs = mode < 0 ? (!ctx->scene.has_temperature && ctx->density.run_fraction >= 0.25) : mode == 1;
+  return VPT_OK;
+}
+
+int vpt_gpu_kernel_variant(const vpt_gpu_ctx* ctx, int* has_temperature, int* run_skipping) {
+  if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
+  if (has_temperature) *has_temperature = ctx->scene.has_temperature ? 1 : 0;
+  if (run_skipping) *run_skipping = ctx->use_runs ? 1 : 0;
+  return VPT_OK;
+}
+
 int vpt_gpu_set_job_order(vpt_gpu_ctx* ctx, int mode) {
   if (!ctx || mode < VPT_ORDER_JID || mode > VPT_ORDER_COST_TAIL)
     return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_job_order: bad argument");
@@ -674,6 +723,7 @@ int vpt_gpu_film_clear(vpt_gpu_ctx* ctx) {
   if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
   int rc = ctx_device(ctx);
   if (rc) return rc;
+  VPT_HIP(hipDeviceSynchronize());  // renders into the film may be in flight on any stream
   VPT_HIP(hipMemsetAsync(ctx->film, 0, ctx->film_count * sizeof(float), ctx->stream));
   VPT_HIP(hipStreamSynchronize(ctx->stream));
   return VPT_OK;

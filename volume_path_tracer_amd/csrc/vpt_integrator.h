@@ -521,12 +521,6 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
     ln.s_t1 = ln.T1;
     return true;
   }
-#ifdef VPT_ABL_NOLOOK  // timing ablation only (wrong at dim changes): no lookahead
-  ln.maj = majorant_of(cell_at(g, ln.vox[0], ln.vox[1], ln.vox[2]));
-  if (ln.maj == ln.s_dmaj) return false;
-  ln.s_t1 = ln.T0;
-  return true;
-#endif
 #ifndef VPT_NO_INTERIOR
   // Fast path: at dim 8 in an interior cell the lookahead point (within ~1 voxel of the cell)
   // lies in a dim-8 cell, so getDim answers 8 == dim and HDDA::update is a no-op.

@@ -40,10 +40,26 @@ def total_samples_per_pixel(world: int, spp: int, mode: str = "weak") -> int:
     return spp * world if mode == "weak" else spp
 
 
+def render_rank(integrator, rank: int, world: int, spp: int, mode: str = "weak", film=None, stream=None):
+    """Launch this rank's share of the job space on its integrator (asynchronously, on `stream`) into
+    `film` (default: the integrator's own).  Returns the (jid_begin, count) ranges launched."""
+    ranges = rank_job_ranges(rank, world, spp, integrator.jobs_per_wave, mode)
+    for b, n in ranges:
+        integrator.render_jobs(b, n, film=film, stream=stream)
+    return ranges
+
+
 def reduce_film(film, group=None):
-    """Sum the per-rank films in place (every rank ends with the whole image)."""
+    """Sum the per-rank films in place (every rank ends with the whole image): RCCL over xGMI for a
+    device film with the "nccl" backend; with gloo (CPU tests, several ranks sharing one GPU) a
+    device film is summed through a host copy."""
     import torch.distributed as dist
 
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(film, op=dist.ReduceOp.SUM, group=group)
+        if film.is_cuda and dist.get_backend(group) == "gloo":
+            host = film.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+            film.copy_(host)
+        else:
+            dist.all_reduce(film, op=dist.ReduceOp.SUM, group=group)
     return film

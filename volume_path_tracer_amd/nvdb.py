@@ -20,7 +20,7 @@ restates its published on-disk layout (NanoVDB 32.x, float grids, ``NANOVDB_USE_
                64 B at 16, min/max/avg/std at 80, values at 96)
 
 Parity unpinned: no .nvdb file ships with the reference (volumes/ is absent), so the reader is
-checked only against ``write_nvdb`` round trips and the grids' own semantics (tests/test_nvdb.py).
+checked only against ``write_nvdb`` round trips and the grids' own semantics (tests/test_image_io.py: test_nvdb_roundtrip, test_nvdb_rejects_garbage).
 """
 from __future__ import annotations
 

@@ -183,6 +183,16 @@ class Integrator:
         (throughput mode: one stream per pixel; matches the reference only in expectation)."""
         capi.check(capi.lib().vpt_gpu_set_rng_mode(self.h, int(mode)), "vpt_gpu_set_rng_mode")
 
+    def set_run_skipping(self, mode: int) -> None:
+        """-1: the creation-time choice; 0 / 1: force the run-skipping kernel variant off / on."""
+        capi.check(capi.lib().vpt_gpu_set_run_skipping(self.h, int(mode)), "vpt_gpu_set_run_skipping")
+
+    def kernel_variant(self) -> dict:
+        """The production kernel this context launches."""
+        t, r = C.c_int(), C.c_int()
+        capi.check(capi.lib().vpt_gpu_kernel_variant(self.h, C.byref(t), C.byref(r)), "vpt_gpu_kernel_variant")
+        return {"has_temperature": bool(t.value), "run_skipping": bool(r.value)}
+
     def set_job_order(self, mode: int) -> None:
         """Scheduling order of whole-wave launches: capi.VPT_ORDER_JID (TileProvider order),
         VPT_ORDER_COST_WAVE_MAJOR, VPT_ORDER_COST_TILE_MAJOR or VPT_ORDER_COST_TAIL (default).
