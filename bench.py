@@ -84,14 +84,18 @@ def host_cpu_info() -> dict:
 
 def cpu_baseline(wl, dens, temp, budget_s: float = 15.0, runs: int = 3):
     """The reference worker pool (main.cpp:62-87, restated headless in the oracle: one std::thread per
-    core calling run() over a TileProvider) on every core of this process's affinity mask, over the
+    core calling run() over a TileProvider) on every CPU this process may use, over the
     DISTINCT waves 1..k of the workload's frame (k sized so that `runs` runs take ~budget_s);
     the value is the median of the runs' Msamples/s."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib as O
 
     info = host_cpu_info()
+    # every CPU this process may run on: the affinity mask, capped by the cgroup CPU quota (threads
+    # beyond the quota only time-slice; the GPU box grants a 1-GPU job 16 of its 256 CPUs)
     threads = max(1, info["affinity"] or 1)
+    if info["cgroup_cpus"]:
+        threads = max(1, min(threads, int(info["cgroup_cpus"] + 0.5)))
     od = O.OracleGrid(dens, fix_majorants=True)
     ot = O.OracleGrid(temp, fix_majorants=False) if temp is not None else None
     cfg = wl.cfg.copy()
@@ -109,7 +113,8 @@ def cpu_baseline(wl, dens, temp, budget_s: float = 15.0, runs: int = 3):
             "sample": f"waves 1..{k} of {cfg.width}x{cfg.height} ({k * per_wave} samples) per run, median of {runs} "
                       f"runs ({', '.join(f'{r:.3f}' for r in rates)} Msamples/s, {sum(secs):.1f} s), oracle worker "
                       f"pool (main.cpp:62-87 restated), {threads} threads",
-            "spread": round((rates[-1] - rates[0]) / med, 4), "host": info}
+            "spread": round((rates[-1] - rates[0]) / med, 4),
+            "per_thread": round(med / threads, 5), "host": info}
 
 
 def spawn_ranks(args) -> int:

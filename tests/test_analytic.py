@@ -15,8 +15,9 @@ expectation (jitter in [0, 0.5)^2, worker.cpp:121-122) a 12x12 midpoint rule ove
 transmittance is smooth across the pixel (silhouette pixels are skipped).
 
 This tests the restated NanoVDB/Eigen semantics (HDDA, clip, Map, trilinear, delta tracking) that no
-reference fixture pins: a systematic error there shifts the expectation.  Bar: every pixel within
-5 sigma of its Monte-Carlo error, and the mean z-score within 4 / sqrt(pixels).
+reference fixture pins: a systematic error there shifts the expectation.  Bar: every pixel's surviving
+sample count inside its exact binomial tails (two-sided p > 1e-3 / pixels), and the mean z-score of
+the pixels in the normal regime within 4 / sqrt(pixels).
 """
 import ctypes as C
 
@@ -95,9 +96,20 @@ def check_film(cfg, film, spp):
     outside = smooth & (t >= 1.0)
     assert inside.sum() >= 100, inside.sum()
     np.testing.assert_allclose(est[outside], 1.0, rtol=2e-5)  # fp32 sums of spp equal terms
-    sd = np.sqrt(t * (1 - t) / spp)
-    z = (est - t)[inside] / sd[inside]
-    assert np.abs(z).max() < 5.0, (np.abs(z).max(), z.mean())
+    # Each sample survives with probability t: the surviving count k is Binomial(spp, t) per pixel.
+    # Exact two-sided binomial tails (pixels that barely clip the volume have spp * (1 - t) << 1, where
+    # a normal approximation is wrong), Bonferroni over the pixels; plus the mean z-score over the
+    # pixels in the normal regime, which a small systematic shift of the expectation moves.
+    from scipy.stats import binom
+
+    k = np.rint(est[inside] * spp)
+    assert np.abs(est[inside] * spp - k).max() < 0.05
+    ti = t[inside]
+    p_two = 2 * np.minimum(binom.cdf(k, spp, ti), binom.sf(k - 1, spp, ti))
+    assert p_two.min() > 1e-3 / inside.sum(), (p_two.min(), int(k[p_two.argmin()]), ti[p_two.argmin()])
+    normal = spp * ti * (1 - ti) >= 10
+    z = (est[inside] - ti)[normal] / np.sqrt(ti * (1 - ti) / spp)[normal]
+    assert z.size >= 50
     assert abs(z.mean()) < 4.0 / np.sqrt(z.size), (z.mean(), z.size)
     return z
 
