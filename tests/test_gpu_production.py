@@ -256,7 +256,7 @@ def test_c5_strong_partitions_sum_to_one_launch_film():
         np.testing.assert_array_equal(f[..., 3], spp)
         xn = f[..., :3] / f[..., 3:]
         rmse = float(np.sqrt(np.mean((xn.astype(np.float64) - x1) ** 2)))
-        assert rmse < 1e-6 and np.allclose(xn, x1, rtol=1e-4, atol=1e-7), (N, rmse)
+        assert rmse < 1e-5 and np.allclose(xn, x1, rtol=1e-4, atol=1e-6), (N, rmse)
 
 
 def test_concurrent_launches_on_three_streams():
