@@ -273,6 +273,7 @@ __global__ void vpt_tile_cost_kernel(const DevScene* scene, float* cost) {
 struct DeviceGrid {
   void* cells8 = nullptr;
   void* runs8 = nullptr;
+  void* walk8 = nullptr;
   double run_fraction = 0.0;
   void* cells128 = nullptr;
   void* root = nullptr;
@@ -295,12 +296,14 @@ static int upload_grid(const HostGrid& h, DeviceGrid& d) {
   int rc;
   if ((rc = upload(h.cells8.data(), h.cells8.size() * sizeof(int2), &d.cells8, d.bytes))) return rc;
   if ((rc = upload(h.runs8.data(), h.runs8.size(), &d.runs8, d.bytes))) return rc;
+  if ((rc = upload(h.walk8.data(), h.walk8.size() * sizeof(uint32_t), &d.walk8, d.bytes))) return rc;
   d.run_fraction = h.run_fraction;
   if ((rc = upload(h.cells128.data(), h.cells128.size() * sizeof(int2), &d.cells128, d.bytes))) return rc;
   if ((rc = upload(h.root.data(), h.root.size() * sizeof(RootTileDev), &d.root, d.bytes))) return rc;
   if ((rc = upload(h.bricks.data(), h.bricks.size() * sizeof(float), &d.bricks, d.bytes))) return rc;
   d.dev.cells8 = (const int2*)d.cells8;
   d.dev.runs8 = (const uint8_t*)d.runs8;
+  d.dev.walk8 = (const uint32_t*)d.walk8;
   d.dev.cells128 = (const int2*)d.cells128;
   d.dev.root = (const RootTileDev*)d.root;
   d.dev.bricks = (const float*)d.bricks;
@@ -310,6 +313,7 @@ static int upload_grid(const HostGrid& h, DeviceGrid& d) {
 static void free_grid(DeviceGrid& d) {
   (void)hipFree(d.cells8);
   (void)hipFree(d.runs8);
+  (void)hipFree(d.walk8);
   (void)hipFree(d.cells128);
   (void)hipFree(d.root);
   (void)hipFree(d.bricks);

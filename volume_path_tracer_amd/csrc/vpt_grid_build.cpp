@@ -5,9 +5,11 @@
 //            (x = leaf index or -(2*dim+active), y = leaf majorant or tile value bits)
 //   cells128 int2[...]                     one entry per 128^3 cell over every upper node
 //   root     RootTileDev[]                 value tiles at the root (outside every upper node)
-//   bricks   float[leaf][9][9][9]          each leaf's 8^3 voxels plus a +1 apron, so that a
-//                                          trilinear stencil whose corner cell is in the leaf
-//                                          reads one brick (NanoVDB SampleFromVoxels semantics)
+//   walk8    uint32[r8_n.x][r8_n.y][r8_n.z] the HDDA fast path's word per cells8 entry: the majorant's
+//                                          bits for an interior cell, kWalkSlow otherwise
+//   bricks   float[leaf][8][8][8][8]       per leaf voxel its whole 2x2x2 trilinear stencil (built
+//                                          from 9^3 apron bricks: the leaf's voxels plus the +1
+//                                          neighbours), NanoVDB SampleFromVoxels semantics
 // One 8-byte cells8 load answers getDim, probeLeaf, probeValue and the majorant of
 // RayMajorantIterator::update_current_majorant (volume.cpp:18-36) for any voxel of the cell.
 //
@@ -137,6 +139,20 @@ void compute_runs(HostGrid& h, int threads) {
     long_runs += r[q] >= 2;
   }
   h.run_fraction = interior ? (double)long_runs / (double)interior : 0.0;
+}
+
+void build_walk_table(HostGrid& h, int threads) {
+  const size_t n = h.cells8.size();
+  h.walk8.assign(n, kWalkSlow);
+  parallel_for((int64_t)n, threads, [&](int64_t b0, int64_t e0) {
+    for (int64_t q = b0; q < e0; ++q) {
+      const int32_t x = h.cells8[q].x;
+      if (!cell8_interior(x)) continue;
+      const float m = majorant_of(Cell{cell8_code(x), math::as_f32((uint32_t)h.cells8[q].y)});
+      h.walk8[q] = math::as_u32(m);
+    }
+  });
+  h.dev.walk8 = h.walk8.data();
 }
 
 namespace {
@@ -332,29 +348,53 @@ int build_host_grid(const vpt_grid_desc& d, bool fix, int threads, HostGrid& out
   G.root = out.root.data();
 
   // --- bricks: 8^3 leaf voxels + the +1 apron ------------------------------------------------
-  out.bricks.assign((size_t)nleaf * kBrickVox, 0.0f);
+  out.bricks.assign((size_t)nleaf * 729, 0.0f);  // 9^3 apron bricks first (expanded into stencils below)
   G.bricks = out.bricks.data();
   // interior first (the apron reads neighbours' interiors through value_at)
   parallel_for((int64_t)nleaf, threads, [&](int64_t b, int64_t e) {
     for (int64_t n = b; n < e; ++n) {
       const float* src = d.leaf_values + (size_t)n * 512;
-      float* dst = out.bricks.data() + (size_t)n * kBrickVox;
+      float* dst = out.bricks.data() + (size_t)n * 729;
       for (int x = 0; x < 8; ++x)
         for (int y = 0; y < 8; ++y)
           for (int z = 0; z < 8; ++z) dst[x * 81 + y * 9 + z] = src[(x << 6) | (y << 3) | z];
     }
   });
+  // getValue over the interiors written so far (apron layout)
+  auto apron_value_at = [&](int32_t i, int32_t j, int32_t k) -> float {
+    const Cell c = cell_at(G, i, j, k);
+    if (c.code < 0) return c.value;
+    return out.bricks[(size_t)c.code * 729 + (i & 7) * 81 + (j & 7) * 9 + (k & 7)];
+  };
   parallel_for((int64_t)nleaf, threads, [&](int64_t b, int64_t e) {
     for (int64_t n = b; n < e; ++n) {
       const int32_t* o = d.leaf_origin + 3 * n;
-      float* dst = out.bricks.data() + (size_t)n * kBrickVox;
+      float* dst = out.bricks.data() + (size_t)n * 729;
       for (int x = 0; x < 9; ++x)
         for (int y = 0; y < 9; ++y)
           for (int z = 0; z < 9; ++z)
-            if (x == 8 || y == 8 || z == 8) dst[x * 81 + y * 9 + z] = value_at(G, o[0] + x, o[1] + y, o[2] + z);
+            if (x == 8 || y == 8 || z == 8) dst[x * 81 + y * 9 + z] = apron_value_at(o[0] + x, o[1] + y, o[2] + z);
     }
   });
 
+  {
+    // expand the apron bricks into per-voxel stencils (corner q = dx<<2 | dy<<1 | dz)
+    std::vector<float> apron;
+    apron.swap(out.bricks);
+    out.bricks.assign((size_t)nleaf * kBrickVox, 0.0f);
+    parallel_for((int64_t)nleaf, threads, [&](int64_t b, int64_t e) {
+      for (int64_t n = b; n < e; ++n) {
+        const float* src = apron.data() + (size_t)n * 729;
+        float* dst = out.bricks.data() + (size_t)n * kBrickVox;
+        for (int x = 0; x < 8; ++x)
+          for (int y = 0; y < 8; ++y)
+            for (int z = 0; z < 8; ++z)
+              for (int q = 0; q < 8; ++q)
+                dst[(((x << 6) | (y << 3) | z) << 3) | q] = src[(x + (q >> 2)) * 81 + (y + ((q >> 1) & 1)) * 9 + z + (q & 1)];
+      }
+    });
+    G.bricks = out.bricks.data();
+  }
   // --- majorants -------------------------------------------------------------------------------
   out.leaf_max.assign(d.leaf_max, d.leaf_max + nleaf);
   if (fix) {
@@ -383,6 +423,7 @@ int build_host_grid(const vpt_grid_desc& d, bool fix, int threads, HostGrid& out
     }
   }
   mark_interior(G, out.cells8, threads);
+  build_walk_table(out, threads);
   return VPT_OK;
 }
 

@@ -43,13 +43,22 @@ struct DevGrid {
   int32_t root_count, pad0;
   const int2* cells8;
   const uint8_t* runs8;  // per cells8 entry: run radius (see mark_runs), for the Runs kernel variant
+  const uint32_t* walk8; // per cells8 entry: the majorant's bits if the cell is interior, else kWalkSlow
   const int2* cells128;
   const RootTileDev* root;
-  const float* bricks;  // [leaf][9][9][9]: voxel (origin + (x,y,z)) for x,y,z in 0..8 (apron +1)
+  const float* bricks;  // [leaf][8][8][8][8]: per leaf voxel its 2x2x2 trilinear stencil (see brick_index)
 };
 
-constexpr int kBrick = 9;
-constexpr int kBrickVox = kBrick * kBrick * kBrick;  // 729
+// Stencil-major brick pool: per leaf voxel (x, y, z) in 0..7 its whole 2x2x2 trilinear stencil
+// (the voxel and its +x/+y/+z neighbours, crossing into the neighbour leaves at the faces), 8 floats =
+// 32 B, one aligned piece of a 128-B line; corner q = dx<<2 | dy<<1 | dz.  A stencil refresh is two
+// 16-byte loads from one line, where the 9^3 apron brick of round 1 spread it over up to 4 lines
+// (8 loads); the pool is 8x the 8^3 voxels (16 KiB per leaf: 1.5 GB for the 512^3 stand-in; HBM has
+// 288 GB).  Measured (r02, same box): C3 423.3/421.3 -> 417.4/417.7 ms, C4 137.1 -> 134.9 ms.
+constexpr int kBrickVox = 512 * 8;
+__host__ __device__ __forceinline__ int64_t brick_index(int32_t code, int32_t i, int32_t j, int32_t k) {
+  return ((int64_t)code * 512 + (((i & 7) << 6) | ((j & 7) << 3) | (k & 7))) * 8;
+}
 
 struct Cell {
   int32_t code;
@@ -60,6 +69,9 @@ struct Cell {
 // HDDA dim 8 (leaf or lower-node tile) and lie inside the table.  It is stored as bit 30 differing
 // from the sign bit (codes are leaf indices < 2^30 or small negatives, where bit 30 == bit 31).
 constexpr int32_t kInteriorBit = 1 << 30;
+// walk8 entry of a cell the HDDA fast path cannot take (not interior; or an interior cell whose
+// majorant has exactly these NaN bits, which then takes the general path -- same result).
+constexpr uint32_t kWalkSlow = 0xFFFFFFFFu;
 __host__ __device__ __forceinline__ int32_t cell8_code(int32_t x) {
   return (x & ~kInteriorBit) | ((x >> 1) & kInteriorBit);
 }
@@ -97,7 +109,7 @@ __host__ __device__ __forceinline__ float majorant_of(Cell c) {
 __host__ __device__ __forceinline__ float value_at(const DevGrid& g, int32_t i, int32_t j, int32_t k) {
   Cell c = cell_at(g, i, j, k);
   if (c.code < 0) return c.value;
-  return g.bricks[(int64_t)c.code * kBrickVox + (i & 7) * 81 + (j & 7) * 9 + (k & 7)];
+  return g.bricks[brick_index(c.code, i, j, k)];
 }
 
 // nanovdb::math::SampleFromVoxels<Acc,1,true> caches the 2x2x2 stencil of the last cell; the cache
@@ -111,16 +123,17 @@ struct StencilCell {
 __host__ __device__ __forceinline__ void fetch_stencil(const DevGrid& g, Cell c, int32_t i, int32_t j, int32_t k,
                                                        float v[8]) {
   if (c.code >= 0) {
-    // Corner cell inside a leaf: the 9^3 apron brick holds the whole 2^3 stencil.
-    const float* b = g.bricks + (int64_t)c.code * kBrickVox + (i & 7) * 81 + (j & 7) * 9 + (k & 7);
-    v[0] = b[0];
-    v[1] = b[1];
-    v[2] = b[9];
-    v[3] = b[10];
-    v[4] = b[81];
-    v[5] = b[82];
-    v[6] = b[90];
-    v[7] = b[91];
+    // Corner cell inside a leaf: its stencil is one 32-byte piece of the pool.
+    const float4* p = reinterpret_cast<const float4*>(g.bricks + brick_index(c.code, i, j, k));
+    const float4 lo = p[0], hi = p[1];
+    v[0] = lo.x;
+    v[1] = lo.y;
+    v[2] = lo.z;
+    v[3] = lo.w;
+    v[4] = hi.x;
+    v[5] = hi.y;
+    v[6] = hi.z;
+    v[7] = hi.w;
   } else {
     // Corner cell without a leaf (tile / background cell, rare): eight getValue calls, one at a
     // time — a compact loop whose lookups are not all in flight at once (register pressure), the
@@ -521,26 +534,22 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
     ln.s_t1 = ln.T1;
     return true;
   }
-#ifndef VPT_NO_INTERIOR
   // Fast path: at dim 8 in an interior cell the lookahead point (within ~1 voxel of the cell)
-  // lies in a dim-8 cell, so getDim answers 8 == dim and HDDA::update is a no-op.
+  // lies in a dim-8 cell, so getDim answers 8 == dim and HDDA::update is a no-op.  One 4-byte load
+  // of the walk table answers both "interior?" and the majorant; 24-bit index arithmetic (the table
+  // has < 2^24 cells per axis product) and a 32-bit byte offset from the table base.
   if (ln.dim == 8) {
     const int32_t a = (ln.vox[0] - g.r8_org[0]) >> 3, b = (ln.vox[1] - g.r8_org[1]) >> 3,
                   c = (ln.vox[2] - g.r8_org[2]) >> 3;
     if ((uint32_t)a < (uint32_t)g.r8_n[0] && (uint32_t)b < (uint32_t)g.r8_n[1] && (uint32_t)c < (uint32_t)g.r8_n[2]) {
-      // one 8-byte load (code + value together)
-      const uint32_t idx = ((uint32_t)a * (uint32_t)g.r8_n[1] + (uint32_t)b) * (uint32_t)g.r8_n[2] + (uint32_t)c;
-      const uint64_t raw = reinterpret_cast<const uint64_t*>(g.cells8)[idx];
+      const uint32_t idx = math::mul24(math::mul24((uint32_t)a, (uint32_t)g.r8_n[1]) + (uint32_t)b, (uint32_t)g.r8_n[2]) + (uint32_t)c;
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(g.walk8) + idx * 4u);
       const int32_t run = Runs ? (int32_t)g.runs8[idx] : 0;
-      const int32_t x = (int32_t)(uint32_t)raw;
-      const float m = majorant_of(Cell{cell8_code(x), math::as_f32((uint32_t)(raw >> 32))});
-      if (cell8_interior(x)) {
+      if (w != kWalkSlow) {
+        const float m = math::as_f32(w);
         ln.maj = m;
         if (m == ln.s_dmaj) {
           if (Runs) {
-            // Every cell within Chebyshev distance `run` is interior with this majorant, so the
-            // next `run` iterations would each load a cell, take the fast path and keep going:
-            // take their HDDA steps here (same float operations, same order) without the loads.
             for (int32_t r = run; r > 0; --r) {
               ++ln.n_dda;
               if (!(hdda_advance(ln) <= ln.T1)) {
@@ -556,7 +565,6 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
       }
     }
   }
-#endif
   // new_dim = max(8, getDim(floor(ray(time + 1.0001f))))
   float tl = ln.T0 + 1.0001f;
   const int32_t lx = (int32_t)floorf(ln.e[0] + ln.d[0] * tl), ly = (int32_t)floorf(ln.e[1] + ln.d[1] * tl),

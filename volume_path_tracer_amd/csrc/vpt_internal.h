@@ -21,6 +21,7 @@ struct HostGrid {
   std::vector<float> bricks;     // [leaf][729]
   std::vector<float> leaf_max;   // fixed majorants
   std::vector<uint8_t> runs8;    // run radius per cells8 entry (compute_runs; empty until then)
+  std::vector<uint32_t> walk8;   // HDDA fast-path table (build_walk_table)
   double run_fraction = 0.0;     // share of interior cells with a run radius >= 2
 };
 
@@ -29,7 +30,11 @@ struct HostGrid {
 // not NaN).  Sets h.runs8, h.dev.runs8 and h.run_fraction.
 void compute_runs(HostGrid& h, int threads);
 
-// Builds the leaf-slot tables and the 9^3 apron brick pool; fixes the majorants
+// The HDDA fast-path table of the cells8 entries (DevGrid::walk8): the majorant's bits for interior
+// cells, kWalkSlow for the others.  Sets h.walk8 and h.dev.walk8 (build_host_grid calls it).
+void build_walk_table(HostGrid& h, int threads);
+
+// Builds the leaf-slot tables, the walk table and the stencil brick pool; fixes the majorants
 // (fix_majorants_for_interpolation, volume.cpp:104-160) when fix == true.
 int build_host_grid(const vpt_grid_desc& d, bool fix, int threads, HostGrid& out);
 

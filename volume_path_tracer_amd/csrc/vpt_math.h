@@ -28,6 +28,14 @@ __host__ __device__ __forceinline__ float as_f32(uint32_t u) {
   __builtin_memcpy(&f, &u, 4);
   return f;
 }
+// a * b for a, b < 2^24 (v_mul_u32_u24: full rate, where a 32-bit multiply is quarter rate)
+__host__ __device__ __forceinline__ uint32_t mul24(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul24(a, b);
+#else
+  return a * b;
+#endif
+}
 
 // logf: LOGF_TABLE_BITS = 4, polynomial order 4 (glibc sysdeps/ieee754/flt-32/e_logf.c).
 // Table entries: 1/c and log(c) for the 16 sub-intervals of [0x3f330000, 2*0x3f330000).
