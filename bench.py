@@ -245,14 +245,15 @@ def main():
         bytes_per_launch = algorithmic_bytes(counters) / (args.steps * launches_per_step)
         achieved = bytes_per_launch / avg_launch_s / 1e9
         traffic = None
-        pmc = sorted((ROOT / "profiles").glob("*_pmc.json"))
-        if pmc:
+        # the newest round's PMC measurement of this workload (tools/profile_round.sh), if any
+        for pf in sorted((ROOT / "profiles").glob("*_pmc.json"), reverse=True):
             try:
-                pj = json.loads(pmc[-1].read_text())
-                if pj.get("config") == args.config and pj.get("spp") == spp:
-                    traffic = pj.get("hbm_bytes_per_launch")
+                pj = json.loads(pf.read_text())
             except Exception:
-                traffic = None
+                continue
+            if pj.get("config") == args.config and pj.get("spp") == spp:
+                traffic = pj.get("hbm_bytes_per_launch")
+                break
         film = it.film_host()
         assert (film[..., 3] == D.total_samples_per_pixel(world, spp, args.mode)).all(), "sample-count channel mismatch"
         out = {
