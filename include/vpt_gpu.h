@@ -281,6 +281,9 @@ int vpt_gpu_set_job_order_tail(vpt_gpu_ctx* ctx, int waves);
 /* The per-tile cost estimates (float[T], may be NULL) and the tile ranks by descending cost
  * (uint32[T], may be NULL): HDDA steps + 4 x majorant optical depth of 5 primary rays per tile. */
 int vpt_gpu_tile_costs(vpt_gpu_ctx* ctx, float* cost_T, uint32_t* rank_T);
+/* Replaces the cost estimates with caller-supplied per-tile costs (float[T], e.g. measured job times
+ * of an earlier launch) and re-ranks the tiles; waits for all work on the device first. */
+int vpt_gpu_set_tile_costs(vpt_gpu_ctx* ctx, const float* cost_T);
 
 int vpt_gpu_sync(vpt_gpu_ctx* ctx);
 /* Zero the context's own film. */

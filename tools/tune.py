@@ -13,6 +13,7 @@ ap.add_argument("--profile", action="store_true")
 ap.add_argument("--rng-mode", default="reference")
 ap.add_argument("--order", type=int, default=-1, help="job order mode (-1: library default)")
 ap.add_argument("--tail", type=int, default=0, help="VPT_ORDER_COST_TAIL tile-major waves (0: auto)")
+ap.add_argument("--tile-costs", default=None, help=".npy of per-tile costs for the job order (vpt_gpu_set_tile_costs)")
 a = ap.parse_args()
 import torch
 from volume_path_tracer_amd.render import Integrator
@@ -27,6 +28,9 @@ if a.rng_mode == "pixel":
 if a.order >= 0:
     it.set_job_order(a.order)
 it.set_job_order_tail(a.tail)
+if a.tile_costs:
+    import numpy as np
+    it.set_tile_costs(np.load(a.tile_costs))
 it.render_waves(1, 1); torch.cuda.synchronize()
 if a.profile:
     it.profile(reset=True)

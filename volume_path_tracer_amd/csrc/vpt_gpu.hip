@@ -134,6 +134,16 @@ struct KernelEnv {
     e->v[6] = 0.0f;
   }
   __device__ __forceinline__ LaneCold& cold() { return g_lane_cold[threadIdx.x]; }
+#ifdef VPT_JOB_LOG
+  // diagnostic build: per job (tile, fetch time, end time, hardware id) into the records buffer
+  __device__ __forceinline__ void job_done(uint32_t job, uint32_t tile, uint32_t t0) {
+    uint32_t* e = reinterpret_cast<uint32_t*>(records) + 4 * (uint64_t)job;
+    e[0] = tile;
+    e[1] = t0;
+    e[2] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    e[3] = (blockIdx.x << 8) | threadIdx.x;
+  }
+#endif
   // lanes of this wavefront for which pred holds
   // (ballot_w64 on the bool itself: the compare folds into the mask, no materialised 0/1 VGPR)
   __device__ __forceinline__ int32_t count(bool pred) { return (int32_t)__popcll(__builtin_amdgcn_ballot_w64(pred)); }
@@ -151,7 +161,11 @@ struct KernelEnv {
     atomicAdd(f + 0, r * lc.L[0]);
     atomicAdd(f + 1, r * lc.L[1]);
     atomicAdd(f + 2, r * lc.L[2]);
+#ifdef VPT_JOB_LOG
+    if (false) {
+#else
     if (records) {
+#endif
       const int32_t xl = px - lc.x0, yl = py - lc.y0;
       float* rec = records + (ln.jid_local * (uint64_t)tile_area + (uint64_t)(yl * rw + xl)) * 3;
       rec[0] = lc.L[0];
@@ -414,6 +428,25 @@ void destroy(vpt_gpu_ctx* ctx) {
   delete ctx;
 }
 
+// The descending-cost tile ranks of ctx->tile_cost, uploaded as the job order.
+int rank_tiles(vpt_gpu_ctx* ctx) {
+  const uint64_t T = ctx->scene.T;
+  ctx->tile_rank.resize(T);
+  for (uint64_t i = 0; i < T; ++i) ctx->tile_rank[i] = (uint32_t)i;
+  std::stable_sort(ctx->tile_rank.begin(), ctx->tile_rank.end(),
+                   [&](uint32_t a, uint32_t b) { return ctx->tile_cost[a] > ctx->tile_cost[b]; });
+  uint32_t* d = nullptr;
+  VPT_HIP(hipMalloc((void**)&d, T * sizeof(uint32_t)));
+  const hipError_t e = hipMemcpy(d, ctx->tile_rank.data(), T * sizeof(uint32_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(d);
+    return vpt::set_error(VPT_E_HIP, std::string("tile order upload: ") + hipGetErrorString(e));
+  }
+  (void)hipFree(ctx->order);
+  ctx->order = d;
+  return VPT_OK;
+}
+
 // Tile costs (vpt_tile_cost_kernel) and the descending-cost tile ranks, once per context.
 int ensure_order(vpt_gpu_ctx* ctx) {
   if (ctx->order) return VPT_OK;
@@ -427,19 +460,7 @@ int ensure_order(vpt_gpu_ctx* ctx) {
   if (e == hipSuccess) e = hipMemcpy(ctx->tile_cost.data(), cost, T * sizeof(float), hipMemcpyDeviceToHost);
   (void)hipFree(cost);
   if (e != hipSuccess) return vpt::set_error(VPT_E_HIP, std::string("tile cost pass: ") + hipGetErrorString(e));
-  ctx->tile_rank.resize(T);
-  for (uint64_t i = 0; i < T; ++i) ctx->tile_rank[i] = (uint32_t)i;
-  std::stable_sort(ctx->tile_rank.begin(), ctx->tile_rank.end(),
-                   [&](uint32_t a, uint32_t b) { return ctx->tile_cost[a] > ctx->tile_cost[b]; });
-  uint32_t* d = nullptr;
-  VPT_HIP(hipMalloc((void**)&d, T * sizeof(uint32_t)));
-  e = hipMemcpy(d, ctx->tile_rank.data(), T * sizeof(uint32_t), hipMemcpyHostToDevice);
-  if (e != hipSuccess) {
-    (void)hipFree(d);
-    return vpt::set_error(VPT_E_HIP, std::string("tile order upload: ") + hipGetErrorString(e));
-  }
-  ctx->order = d;
-  return VPT_OK;
+  return rank_tiles(ctx);
 }
 
 int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film, float* records, void* stream_ptr,
@@ -498,7 +519,11 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.event_count = ctx->job_counter + 2 * slot + 1;
   env.event_cap = event_cap;
   if (slot_out) *slot_out = slot;
+#ifdef VPT_JOB_LOG
+  const bool temp = ctx->scene.has_temperature != 0, dbg = events != nullptr;  // records = the job log
+#else
   const bool temp = ctx->scene.has_temperature != 0, dbg = records != nullptr || events != nullptr;
+#endif
   auto kernel = temp ? (dbg ? vpt::vpt_integrate_kernel<true, true, false> : vpt::vpt_integrate_kernel<true, false, false>)
                      : ctx->use_runs
                          ? (dbg ? vpt::vpt_integrate_kernel<false, true, true> : vpt::vpt_integrate_kernel<false, false, true>)
@@ -713,6 +738,15 @@ int vpt_gpu_tile_costs(vpt_gpu_ctx* ctx, float* cost, uint32_t* rank) {
   if (cost) std::memcpy(cost, ctx->tile_cost.data(), ctx->tile_cost.size() * sizeof(float));
   if (rank) std::memcpy(rank, ctx->tile_rank.data(), ctx->tile_rank.size() * sizeof(uint32_t));
   return VPT_OK;
+}
+
+int vpt_gpu_set_tile_costs(vpt_gpu_ctx* ctx, const float* cost) {
+  if (!ctx || !cost) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_tile_costs: null argument");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  VPT_HIP(hipDeviceSynchronize());  // in-flight launches read the current order
+  ctx->tile_cost.assign(cost, cost + ctx->scene.T);
+  return rank_tiles(ctx);
 }
 
 int vpt_gpu_sync(vpt_gpu_ctx* ctx) {

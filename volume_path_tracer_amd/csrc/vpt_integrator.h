@@ -389,6 +389,10 @@ struct LaneCold {
   StencilCell dens_cell;  // the density sampler's last stencil cell (collision evaluation only)
   float Tr;               // shadow-ray transmittance (< 0: sample_Ld returns zero)
   float y_draw;           // 1 - u of a free-flight draw whose exact distance is pending (SM_EVAL)
+#ifdef VPT_JOB_LOG
+  uint32_t t_start;       // diagnostic build: s_memrealtime at the job's fetch
+  uint32_t job;           // and the job's index in the launch
+#endif
 };
 
 struct Lane {
@@ -972,6 +976,10 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         ln.jid_local = j;
         ln.n_events = 0;
       }
+#ifdef VPT_JOB_LOG
+      lc.job = (uint32_t)j;
+      lc.t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
       uint64_t jid = env.jid_begin + j;
       ln.rng = job_seed(S.seed, S.pixel_mode ? jid * S.tile_area + p : jid);
       uint64_t tile = jid % S.T;
@@ -1002,6 +1010,9 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       const int32_t end = one ? ((lc.pix & kPixelTaken) ? 0 : min(q + 1, rw * rh)) : rw * rh;
       while (true) {
         if (q >= end) {
+#ifdef VPT_JOB_LOG
+          env.job_done(lc.job, (uint32_t)((lc.x0 / S.tw) + (lc.y0 / S.th) * S.ntx), lc.t_start);
+#endif
           ln.state = ST_FETCH;
           return;
         }

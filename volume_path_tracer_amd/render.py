@@ -211,6 +211,13 @@ class Integrator:
                                                   rank.ctypes.data_as(C.POINTER(C.c_uint32))), "vpt_gpu_tile_costs")
         return cost, rank
 
+    def set_tile_costs(self, cost) -> None:
+        """Replace the job-order cost estimates with per-tile costs (float32[T], e.g. measured)."""
+        c = np.ascontiguousarray(cost, np.float32)
+        assert c.shape == (self.cfg.jobs_per_wave(),)
+        capi.check(capi.lib().vpt_gpu_set_tile_costs(self.h, c.ctypes.data_as(C.POINTER(C.c_float))),
+                   "vpt_gpu_set_tile_costs")
+
     def counters(self, reset: bool = False) -> dict:
         c = capi.Counters()
         capi.check(capi.lib().vpt_gpu_counters(self.h, C.byref(c), 1 if reset else 0), "vpt_gpu_counters")
