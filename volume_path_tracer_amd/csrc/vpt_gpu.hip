@@ -157,7 +157,8 @@ struct KernelEnv {
     float* f = film + ((int64_t)py * S.W + px) * 4;
     const float r = S.imaging_ratio;
     const LaneCold& lc = cold();
-    atomicAdd(f + 3, 1.0f);
+    // The sample-count channel (w += 1 per sample) is added per launch by vpt_count_kernel: each fp32
+    // atomic here costs ~2 % of the C3 frame (it stays in vmcnt until the memory side acks it).
     atomicAdd(f + 0, r * lc.L[0]);
     atomicAdd(f + 1, r * lc.L[1]);
     atomicAdd(f + 2, r * lc.L[2]);
@@ -202,6 +203,24 @@ __global__ __launch_bounds__(kBlockThreads, Debug ? VPT_WAVES_SLOW : (HasTemp ? 
 #if defined(VPT_PROFILE) || defined(VPT_PROFILE_TIME)
   if (threadIdx.x < PT_COUNT) atomicAdd(env.prof_buf + 2 * PB_COUNT + threadIdx.x, wg_prof[threadIdx.x]);
 #endif
+}
+
+// The film's sample-count channel for the job range [jid_begin, jid_begin + jid_count): a pixel of
+// tile t gains one sample per job t + k*T in the range (only the single_pixel pixel when that mode is
+// on, worker.cpp:113-116).  Counts are integers, so adding them at once equals the reference's
+// per-sample += 1.0f (exact below 2^24).
+__global__ void vpt_count_kernel(const DevScene* scene, float* film, uint64_t jid_begin, uint64_t jid_count) {
+  const DevScene& S = *scene;
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= (uint64_t)S.W * (uint64_t)S.H) return;
+  const int32_t px = (int32_t)(p % (uint64_t)S.W), py = (int32_t)(p / (uint64_t)S.W);
+  if (S.single_pixel_enabled && (px != S.sp_x || py != S.sp_y)) return;
+  const uint64_t t = (uint64_t)(py / S.th) * S.ntx + (uint64_t)(px / S.tw), T = S.T, end = jid_begin + jid_count;
+  // k from ceil((jid_begin - t) / T) (or 0) to the last k with t + k*T < end
+  const uint64_t k0 = jid_begin > t ? (jid_begin - t + T - 1) / T : 0;
+  if (t >= end || t + k0 * T >= end) return;
+  const uint64_t n = (end - 1 - t) / T - k0 + 1;
+  atomicAdd(film + p * 4 + 3, (float)n);
 }
 
 // Volume::log_majorant_trace (src/volume.cpp:176-192) of one world ray, on one lane: every
@@ -529,6 +548,10 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
                          ? (dbg ? vpt::vpt_integrate_kernel<false, true, true> : vpt::vpt_integrate_kernel<false, false, true>)
                          : (dbg ? vpt::vpt_integrate_kernel<false, true, false> : vpt::vpt_integrate_kernel<false, false, false>);
   hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, ctx->scene_dev, env, ctx->counters);
+  VPT_HIP(hipGetLastError());
+  const uint64_t npix = (uint64_t)ctx->scene.W * (uint64_t)ctx->scene.H;
+  hipLaunchKernelGGL(vpt::vpt_count_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, ctx->scene_dev,
+                     env.film, jid_begin, jid_count);
   VPT_HIP(hipGetLastError());
   return release_slot(ctx, s, slot);
 }
