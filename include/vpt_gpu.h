@@ -284,6 +284,10 @@ int vpt_gpu_tile_costs(vpt_gpu_ctx* ctx, float* cost_T, uint32_t* rank_T);
 /* Replaces the cost estimates with caller-supplied per-tile costs (float[T], e.g. measured job times
  * of an earlier launch) and re-ranks the tiles; waits for all work on the device first. */
 int vpt_gpu_set_tile_costs(vpt_gpu_ctx* ctx, const float* cost_T);
+/* An explicit job order for launches of exactly n jobs (any jid_begin): work item k renders job
+ * jid_begin + perm[k].  perm must be a permutation of 0..n-1; n = 0 clears it.  Samples never depend
+ * on the order.  Not used in the pixel RNG mode. */
+int vpt_gpu_set_job_permutation(vpt_gpu_ctx* ctx, const uint32_t* perm, uint64_t n);
 
 int vpt_gpu_sync(vpt_gpu_ctx* ctx);
 /* Zero the context's own film. */

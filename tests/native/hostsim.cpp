@@ -23,6 +23,7 @@ struct HostEnv {
   float* records;
   int32_t tile_area;
   const uint32_t* order = nullptr;  // job order (see vpt_integrator.h ST_FETCH)
+  const uint32_t* perm = nullptr;   // explicit job order (vpt_gpu_set_job_permutation)
   uint32_t order_tail_k0 = 0;
   uint32_t order_tail_n = 0;
   int32_t count(bool pred) { return pred ? 1 : 0; }  // one lane

@@ -1,0 +1,66 @@
+"""Job-order experiments on the full C3 frame through vpt_gpu_set_job_permutation (samples never depend
+on the order, only the launch's drain does).  Costs: measured per-tile job times (tools/job_log.py) or
+the built-in estimates.
+    python tools/order_lab.py [--costs gpurun_out/joblog/tile_cost_c3.npy] [--reps 2]"""
+import argparse, json, sys, time
+from pathlib import Path
+import numpy as np
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="c3")
+ap.add_argument("--costs", default=None)
+ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--only", default=None)
+a = ap.parse_args()
+import torch
+from volume_path_tracer_amd.render import Integrator
+from volume_path_tracer_amd.scenes import SynthGrid, workload
+wl = workload(a.config)
+dg = SynthGrid(wl.density_kind, wl.grid_n); tg = SynthGrid(2, wl.grid_n) if wl.temperature else None
+it = Integrator(wl.cfg, dg.grid(copy=False), tg.grid(copy=False) if tg else None)
+T, W = it.jobs_per_wave, wl.spp
+lanes = it.launch_info()[0] * it.launch_info()[1]
+est, _ = it.tile_costs()
+cost = np.load(a.costs).astype(np.float64) if a.costs else est.astype(np.float64)
+rank = np.argsort(-cost, kind="stable").astype(np.int64)
+
+
+def cost_tail(rank, n_waves, tail, waves0=0):
+    """vpt_integrator.h ordered_job: wave-major costliest-first, then `tail` waves tile-major in groups of 64."""
+    head = (np.arange(waves0, n_waves - tail)[:, None] * T + rank[None, :]).ravel()
+    full = len(rank) // 64
+    g = rank[: full * 64].reshape(full, 64)
+    tw = np.arange(n_waves - tail, n_waves)
+    body = (tw[None, :, None] * T + g[:, None, :]).reshape(-1)
+    rest = (tw[:, None] * T + rank[full * 64:][None, :]).ravel()
+    return np.concatenate([head, body, rest])
+
+
+auto_tail = min(W, (6 * lanes + T - 1) // T)
+orders = {"builtin": None, "perm_current": cost_tail(rank, W, auto_tail)}
+for K in (128, 512, 2048):
+    top = rank[:K]
+    topset = np.zeros(T, bool); topset[top] = True
+    tw = np.arange(W - auto_tail, W)
+    front = (tw[None, :, None] * T + top.reshape(-1, 64)[:, None, :]).reshape(-1) if K % 64 == 0 else None
+    base = cost_tail(rank, W, auto_tail)
+    keep = ~np.isin(base, front)
+    orders[f"front_top{K}_tail"] = np.concatenate([front, base[keep]])
+for tl in (auto_tail // 2, auto_tail * 2):
+    orders[f"tail{tl}"] = cost_tail(rank, W, min(W, tl))
+res = {}
+for name, perm in orders.items():
+    if a.only and name not in a.only.split(","):
+        continue
+    if perm is not None:
+        assert perm.size == T * W and np.unique(perm).size == perm.size
+    it.set_job_permutation(perm)
+    it.film.zero_(); it.render_waves(1, W); torch.cuda.synchronize()
+    best = 1e9
+    for _ in range(a.reps):
+        it.film.zero_(); torch.cuda.synchronize(); t = time.perf_counter()
+        it.render_waves(1, W); torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t)
+    assert (it.film_host()[..., 3] == W).all()
+    res[name] = round(best * 1e3, 2)
+    print(json.dumps({"order": name, "ms": res[name], "costs": a.costs or "estimated"}), flush=True)

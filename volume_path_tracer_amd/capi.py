@@ -239,6 +239,7 @@ def lib() -> C.CDLL:
     L.vpt_gpu_set_job_order_tail.argtypes = [vp, C.c_int]
     L.vpt_gpu_tile_costs.argtypes = [vp, fp, C.POINTER(C.c_uint32)]
     L.vpt_gpu_set_tile_costs.argtypes = [vp, fp]
+    L.vpt_gpu_set_job_permutation.argtypes = [vp, C.POINTER(C.c_uint32), C.c_uint64]
     _lib = L
     return L
 

@@ -53,6 +53,7 @@ constexpr int kBlockThreads = 256;
 // The lanes' cold state (vpt_integrator.h LaneCold), one slot per thread of the integrator's block.
 __shared__ LaneCold g_lane_cold[kBlockThreads];
 
+
 struct KernelEnv {
   uint64_t jid_begin;
   uint64_t jid_count;
@@ -64,6 +65,7 @@ struct KernelEnv {
   unsigned long long* lds_prof;  // this workgroup's section cycles (LDS, VPT_PROFILE builds)
   unsigned long long* lds_counters;  // this workgroup's event counters (LDS)
   const uint32_t* order;             // job order: tile ranks (nullptr = jid order), see ordered_job
+  const uint32_t* perm;              // explicit job order (item k -> job perm[k]), overrides order
   uint32_t order_tail_k0;
   uint32_t order_tail_n;
   vpt_event* events;                 // Logger events (trace launches only)
@@ -384,6 +386,8 @@ struct vpt_gpu_ctx {
   int order_tail_waves = 0;        // VPT_ORDER_COST_TAIL: tile-major waves (0 = auto)
   uint32_t* order = nullptr;       // tile ranks by descending cost (device), built on first use
   std::vector<float> tile_cost;    // host copy of the estimates
+  uint32_t* perm = nullptr;        // explicit job order of launches with perm_n jobs (device)
+  uint64_t perm_n = 0;
   std::vector<uint32_t> tile_rank;
 };
 
@@ -441,6 +445,7 @@ void destroy(vpt_gpu_ctx* ctx) {
   (void)hipFree(ctx->prof);
   (void)hipFree(ctx->scene_dev);
   (void)hipFree(ctx->order);
+  (void)hipFree(ctx->perm);
   for (uint32_t i = 0; i < kLaunchSlots; ++i)
     if (ctx->slot_done[i]) (void)hipEventDestroy(ctx->slot_done[i]);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -503,6 +508,7 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.tile_area = ctx->scene.tw * ctx->scene.th;
   env.prof_buf = ctx->prof;
   env.order = nullptr;
+  env.perm = nullptr;
   env.order_tail_k0 = 0;
   env.order_tail_n = 0;
   // Fewer work items than resident lanes (small frames, few waves): a launch lasts as long as its
@@ -531,6 +537,7 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
     env.order_tail_n = tail;
     env.order_tail_k0 = (n - tail) * (uint32_t)T;
   }
+  if (ctx->perm && ctx->perm_n == jid_count && !ctx->scene.pixel_mode) env.perm = ctx->perm;
   uint32_t slot = 0;
   if ((rc = take_slot(ctx, s, slot))) return rc;
   env.job_counter = ctx->job_counter + 2 * slot;
@@ -770,6 +777,27 @@ int vpt_gpu_set_tile_costs(vpt_gpu_ctx* ctx, const float* cost) {
   VPT_HIP(hipDeviceSynchronize());  // in-flight launches read the current order
   ctx->tile_cost.assign(cost, cost + ctx->scene.T);
   return rank_tiles(ctx);
+}
+
+int vpt_gpu_set_job_permutation(vpt_gpu_ctx* ctx, const uint32_t* perm, uint64_t n) {
+  if (!ctx || (n && !perm)) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_job_permutation: null argument");
+  if (n >= (1ULL << 32)) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_job_permutation: too many jobs");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  std::vector<uint8_t> seen(n, 0);
+  for (uint64_t i = 0; i < n; ++i) {
+    if (perm[i] >= n || seen[perm[i]]) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_job_permutation: not a permutation");
+    seen[perm[i]] = 1;
+  }
+  VPT_HIP(hipDeviceSynchronize());  // in-flight launches may read the current one
+  (void)hipFree(ctx->perm);
+  ctx->perm = nullptr;
+  ctx->perm_n = 0;
+  if (n == 0) return VPT_OK;
+  VPT_HIP(hipMalloc((void**)&ctx->perm, n * sizeof(uint32_t)));
+  VPT_HIP(hipMemcpy(ctx->perm, perm, n * sizeof(uint32_t), hipMemcpyHostToDevice));
+  ctx->perm_n = n;
+  return VPT_OK;
 }
 
 int vpt_gpu_sync(vpt_gpu_ctx* ctx) {

@@ -971,7 +971,10 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         p = (uint32_t)(j % S.tile_area);
         j /= S.tile_area;
       }
-      if (env.order) j = ordered_job((uint32_t)j, (uint32_t)S.T, env.order, env.order_tail_k0, env.order_tail_n);
+      if (env.perm)
+        j = env.perm[j];
+      else if (env.order)
+        j = ordered_job((uint32_t)j, (uint32_t)S.T, env.order, env.order_tail_k0, env.order_tail_n);
       if (Debug) {
         ln.jid_local = j;
         ln.n_events = 0;

@@ -218,6 +218,13 @@ class Integrator:
         capi.check(capi.lib().vpt_gpu_set_tile_costs(self.h, c.ctypes.data_as(C.POINTER(C.c_float))),
                    "vpt_gpu_set_tile_costs")
 
+    def set_job_permutation(self, perm) -> None:
+        """Explicit order of launches with len(perm) jobs: item k renders job jid_begin + perm[k]
+        (None or empty clears it).  Samples never depend on it."""
+        p = np.ascontiguousarray(perm if perm is not None else [], np.uint32)
+        capi.check(capi.lib().vpt_gpu_set_job_permutation(self.h, p.ctypes.data_as(C.POINTER(C.c_uint32)), p.size),
+                   "vpt_gpu_set_job_permutation")
+
     def counters(self, reset: bool = False) -> dict:
         c = capi.Counters()
         capi.check(capi.lib().vpt_gpu_counters(self.h, C.byref(c), 1 if reset else 0), "vpt_gpu_counters")
