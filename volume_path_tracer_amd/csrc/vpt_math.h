@@ -37,6 +37,28 @@ __host__ __device__ __forceinline__ uint32_t mul24(uint32_t a, uint32_t b) {
 #endif
 }
 
+// The double coefficients below, on the device, are read at each use from constant memory through an
+// opaque pointer (scalar loads into SGPR pairs).  As literals the compiler hoists them out of the
+// integrator's state-machine loop into VGPR pairs held for the whole kernel (r02: 4 VGPRs plus an
+// 8-byte spill in the 72-VGPR production kernel).
+enum : int { MK_LN2, MK_A0, MK_A1, MK_A2, MK_HPI_INV, MK_HPI, MK_C1, MK_C2, MK_C3, MK_C4, MK_S1, MK_S2, MK_S3, MK_COUNT };
+#if defined(__HIP_DEVICE_COMPILE__)
+static __constant__ double kMathK[MK_COUNT] = {
+    0x1.62e42fefa39efp-1,                                                        // Ln2
+    -0x1.00ea348b88334p-2, 0x1.5575b0be00b6ap-2, -0x1.ffffef20a4123p-2,            // logf A0..A2
+    0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,                                  // 1/(pi/2) scaled, pi/2
+    -0x1.ffffffd0c621cp-2, 0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10, 0x1.99343027bf8c3p-16,  // cos c1..c4
+    -0x1.555545995a603p-3, 0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13};         // sin s1..s3
+__device__ __forceinline__ double mk(int i) {
+  const __attribute__((address_space(4))) double* p = (const __attribute__((address_space(4))) double*)(const double*)kMathK;
+  asm volatile("" : "+s"(p));
+  return p[i];
+}
+#define VPT_MK(i, v) ::vpt::math::mk(i)
+#else
+#define VPT_MK(i, v) (v)
+#endif
+
 // logf: LOGF_TABLE_BITS = 4, polynomial order 4 (glibc sysdeps/ieee754/flt-32/e_logf.c).
 // Table entries: 1/c and log(c) for the 16 sub-intervals of [0x3f330000, 2*0x3f330000).
 // A memory-resident constexpr table (emitted as device constant data): a per-lane indexed load
@@ -85,8 +107,9 @@ __host__ __device__ __forceinline__ float logf_glibc(float x) {
 // sign) never fire and are omitted (x == 1 gives +0 on the main path too).  Checked against glibc
 // over every such x by tests/test_math_clone.py.
 __host__ __device__ __forceinline__ float logf_glibc_unit(float x) {
-  const double Ln2 = 0x1.62e42fefa39efp-1;
-  const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2, A2 = -0x1.ffffef20a4123p-2;
+  const double Ln2 = VPT_MK(MK_LN2, 0x1.62e42fefa39efp-1);
+  const double A0 = VPT_MK(MK_A0, -0x1.00ea348b88334p-2), A1 = VPT_MK(MK_A1, 0x1.5575b0be00b6ap-2),
+               A2 = VPT_MK(MK_A2, -0x1.ffffef20a4123p-2);
   const uint32_t ix = as_u32(x);
   const uint32_t tmp = ix - 0x3f330000u;
   const int i = (int)((tmp >> (23 - 4)) % 16u);
@@ -118,24 +141,24 @@ __host__ __device__ __forceinline__ uint32_t abstop12(float x) { return (as_u32(
 __host__ __device__ __forceinline__ float sinf_poly(double x, double x2, bool neg_cos, int n) {
   if ((n & 1) == 0) {
     double x3 = x * x2;
-    double s1 = __builtin_fma(x2, sc::s3, sc::s2);
+    double s1 = __builtin_fma(x2, VPT_MK(MK_S3, sc::s3), VPT_MK(MK_S2, sc::s2));
     double x7 = x3 * x2;
-    double s = __builtin_fma(x3, sc::s1, x);
+    double s = __builtin_fma(x3, VPT_MK(MK_S1, sc::s1), x);
     return (float)__builtin_fma(x7, s1, s);
   }
   double x4 = x2 * x2;
-  double c2 = __builtin_fma(x2, sc::c4, sc::c3);
-  double c1 = __builtin_fma(x2, sc::c1, sc::c0);
+  double c2 = __builtin_fma(x2, VPT_MK(MK_C4, sc::c4), VPT_MK(MK_C3, sc::c3));
+  double c1 = __builtin_fma(x2, VPT_MK(MK_C1, sc::c1), sc::c0);
   double x6 = x4 * x2;
-  double c = __builtin_fma(x4, sc::c2, c1);
+  double c = __builtin_fma(x4, VPT_MK(MK_C2, sc::c2), c1);
   double r = __builtin_fma(x6, c2, c);
   return (float)(neg_cos ? -r : r);
 }
 __host__ __device__ __forceinline__ double reduce_fast(double x, int* np) {
-  double r = x * sc::hpi_inv;
+  double r = x * VPT_MK(MK_HPI_INV, sc::hpi_inv);
   int n = ((int32_t)r + 0x800000) >> 24;
   *np = n;
-  return __builtin_fma(-(double)n, sc::hpi, x);
+  return __builtin_fma(-(double)n, VPT_MK(MK_HPI, sc::hpi), x);
 }
 // sign[4] = {1, -1, -1, 1}
 __host__ __device__ __forceinline__ double quadrant_sign(int n) { return ((n + 1) & 2) ? -1.0 : 1.0; }
