@@ -65,6 +65,22 @@ struct Cell {
   float value;
 };
 
+// A constant materialised where it is used.  Literal operands a VOP3 or LDS instruction cannot
+// encode are otherwise hoisted out of the state-machine loop into a VGPR held for the whole kernel
+// (r02: four such VGPRs in the 72-VGPR production kernel).
+__host__ __device__ __forceinline__ int32_t local_const(int32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(c));
+#endif
+  return c;
+}
+__host__ __device__ __forceinline__ float local_const(float c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(c));
+#endif
+  return c;
+}
+
 // cells8 entries carry one more bit: "interior" = this 8^3 cell and its 26 neighbours all have
 // HDDA dim 8 (leaf or lower-node tile) and lie inside the table.  It is stored as bit 30 differing
 // from the sign bit (codes are leaf indices < 2^30 or small negatives, where bit 30 == bit 31).
@@ -95,7 +111,7 @@ __host__ __device__ __forceinline__ Cell cell_at(const DevGrid& g, int32_t i, in
     if ((i & ~4095) == t.origin[0] && (j & ~4095) == t.origin[1] && (k & ~4095) == t.origin[2])
       return Cell{-(2 * 4096 + t.active), t.value};
   }
-  return Cell{-(2 * 4096), g.background};
+  return Cell{local_const(-(2 * 4096)), g.background};
 }
 
 // max(8, ReadAccessor::getDim(ijk)) (volume.cpp:11-14): a leaf's getDim is 1.
@@ -734,7 +750,7 @@ __host__ __device__ __forceinline__ void primary_event(const DevScene& S, const 
         lc.Tr = -1.0f;  // returns Li == 0 without draws
         ln.state = ST_NEE_DONE;
       } else {
-        lc.Tr = 1.0f;
+        lc.Tr = local_const(1.0f);
         ln.shadow = 1;
         ln.state = ST_SHADOW;
       }
@@ -918,9 +934,11 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         lc.L[1] = lc.L[1] + pt * S.Li[1];
         lc.L[2] = lc.L[2] + pt * S.Li[2];
       } else {
-        lc.L[0] = lc.L[0] + 0.0f;
-        lc.L[1] = lc.L[1] + 0.0f;
-        lc.L[2] = lc.L[2] + 0.0f;
+        // L + 0.0f (sample_Ld returned zero): the same value as L for every L but -0.0, which it
+        // turns into +0.0 -- written as a select, so no register holds a constant for it.
+        lc.L[0] = lc.L[0] == 0.0f ? 0.0f : lc.L[0];
+        lc.L[1] = lc.L[1] == 0.0f ? 0.0f : lc.L[1];
+        lc.L[2] = lc.L[2] == 0.0f ? 0.0f : lc.L[2];
       }
       float u0 = rng_uniform(ln.rng);
       float u1 = rng_uniform(ln.rng);
