@@ -40,6 +40,8 @@ struct HostEnv {
     j = next++;
     return true;
   }
+  const double (*logf_table() const)[2] { return vpt::math::kLogfTab; }
+  const float* bb_table(const vpt::DevScene& S) const { return S.bb; }
   void film_add(const vpt::DevScene& S, const vpt::Lane& ln, int32_t px, int32_t py, int32_t rw) {
     float* f = film + ((int64_t)py * S.W + px) * 4;
     f[3] += 1.0f;

@@ -52,6 +52,11 @@ constexpr int kBlockThreads = 256;
 
 // The lanes' cold state (vpt_integrator.h LaneCold), one slot per thread of the integrator's block.
 __shared__ LaneCold g_lane_cold[kBlockThreads];
+// LDS copies of the small lookup tables the evaluation reads per lane (logf's 16 x 2 doubles; the
+// temperature kernel's 501 x 3 blackbody table): LDS reads instead of vector-memory loads, which
+// would count in vmcnt with the walk's loads.
+__shared__ double g_logf_tab[16][2];
+constexpr int kBbFloats = 501 * 3;
 
 
 struct KernelEnv {
@@ -136,6 +141,9 @@ struct KernelEnv {
     e->v[6] = 0.0f;
   }
   __device__ __forceinline__ LaneCold& cold() { return g_lane_cold[threadIdx.x]; }
+  const float* bb_lds;  // the temperature kernel's LDS copy of S.bb
+  __device__ __forceinline__ const double (*logf_table() const)[2] { return g_logf_tab; }
+  __device__ __forceinline__ const float* bb_table(const DevScene&) const { return bb_lds; }
 #ifdef VPT_JOB_LOG
   // diagnostic build: per job (tile, fetch time, end time, hardware id) into the records buffer
   __device__ __forceinline__ void job_done(uint32_t job, uint32_t tile, uint32_t t0) {
@@ -184,6 +192,13 @@ __global__ __launch_bounds__(kBlockThreads, Debug ? VPT_WAVES_SLOW : (HasTemp ? 
                                                                        unsigned long long* counters) {
   __shared__ unsigned long long wg_counters[kCounterCount];
   if (threadIdx.x < kCounterCount) wg_counters[threadIdx.x] = 0;
+  if (threadIdx.x < 32) g_logf_tab[threadIdx.x >> 1][threadIdx.x & 1] = math::kLogfTab[threadIdx.x >> 1][threadIdx.x & 1];
+  __shared__ float bb_lds[HasTemp ? kBbFloats : 1];
+  if (HasTemp) {
+    const float* bb = scene->bb;
+    for (int i = threadIdx.x; i < kBbFloats; i += kBlockThreads) bb_lds[i] = bb[i];
+  }
+  env.bb_lds = bb_lds;
   __syncthreads();
   env.lds_counters = wg_counters;
 #if defined(VPT_PROFILE) || defined(VPT_PROFILE_TIME)

@@ -310,7 +310,8 @@ __host__ __device__ inline float planck_dev(float lambda_m, float t) {
   float e = expf((h * c) / (lambda_m * kb * t));
   return num / (lambda5 * (e - 1));
 }
-__host__ __device__ inline void blackbody_xyz(const DevScene& S, float t, float& X, float& Y, float& Z) {
+// bb: the blackbody table [501][3] (S.bb, or the kernel's LDS copy).
+__host__ __device__ inline void blackbody_xyz(const DevScene& S, const float* bb, float t, float& X, float& Y, float& Z) {
   if (!(t - t == 0.0f)) {  // !isfinite
     X = Y = Z = __builtin_nanf("");
     return;
@@ -336,7 +337,7 @@ __host__ __device__ inline void blackbody_xyz(const DevScene& S, float t, float&
   int dn = (int)math::div_by_recip(t, 100.0f, 0.01f);  // t / 100 (0.01f == RN(1/100))
   while (t <= bb_idx_to_temp(dn - 1)) --dn;
   while (t >= bb_idx_to_temp(dn + 1)) ++dn;
-  const float* a = S.bb + dn * 3;
+  const float* a = bb + dn * 3;
   if (t == bb_idx_to_temp(dn)) {
     X = a[0];
     Y = a[1];
@@ -713,7 +714,7 @@ __host__ __device__ __forceinline__ void primary_event(const DevScene& S, const 
     map_inv(S.temperature, cp[0], cp[1], cp[2], tx, ty, tz);
     env.tally(CNT_TEMP_STENCILS, trilinear(S.temperature, ln.temp_cell, tx, ty, tz, tadim) ? 1 : 0);
     float tK = tadim * S.temp_scale + S.temp_offset;
-    blackbody_xyz(S, tK, X, Y, Z);
+    blackbody_xyz(S, env.bb_table(S), tK, X, Y, Z);
     float sc = p_a * S.le_scale;
     lc.L[0] = lc.L[0] + sc * X;
     lc.L[1] = lc.L[1] + sc * Y;
@@ -769,7 +770,7 @@ __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const
   {
     // The draw's exact free-flight distance, deferred from SM_DRAW (majorant_transmittance_sampler.cpp:44-45):
     // dt = -log(1 - u) / sigma_maj (random.hpp:20-22), t = t0 + dt / m_scale.
-    const float dt_m = -math::logf_glibc_unit(lc.y_draw) / sigma_maj;
+    const float dt_m = -math::logf_glibc_unit(lc.y_draw, env.logf_table()) / sigma_maj;
     const float tc = ln.s_t0 + math::div_by_recip(dt_m, ln.scale, ln.rscale);  // == dt_m / m_scale
     if (!(tc < ln.s_t1)) {  // overshoot after all: drop the segment
       ln.sm = SM_NEED_SEG;

@@ -106,7 +106,9 @@ __host__ __device__ __forceinline__ float logf_glibc(float x) {
 // float in [2^-24, 1]: glibc's special-case branches (zero, subnormal, inf, nan, x == 1 rounding-mode
 // sign) never fire and are omitted (x == 1 gives +0 on the main path too).  Checked against glibc
 // over every such x by tests/test_math_clone.py.
-__host__ __device__ __forceinline__ float logf_glibc_unit(float x) {
+// tab: the kLogfTab values (the kernel passes its LDS copy: an LDS read instead of a vector-memory
+// load, which would count in vmcnt with the walk's loads).
+__host__ __device__ __forceinline__ float logf_glibc_unit(float x, const double (*tab)[2] = kLogfTab) {
   const double Ln2 = VPT_MK(MK_LN2, 0x1.62e42fefa39efp-1);
   const double A0 = VPT_MK(MK_A0, -0x1.00ea348b88334p-2), A1 = VPT_MK(MK_A1, 0x1.5575b0be00b6ap-2),
                A2 = VPT_MK(MK_A2, -0x1.ffffef20a4123p-2);
@@ -115,7 +117,7 @@ __host__ __device__ __forceinline__ float logf_glibc_unit(float x) {
   const int i = (int)((tmp >> (23 - 4)) % 16u);
   const int k = (int32_t)tmp >> 23;
   const uint32_t iz = ix - (tmp & (0x1ffu << 23));
-  const double invc = kLogfTab[i][0], logc = kLogfTab[i][1];
+  const double invc = tab[i][0], logc = tab[i][1];
   const double z = (double)as_f32(iz);
   const double r = __builtin_fma(z, invc, -1.0);
   const double y0 = __builtin_fma((double)k, Ln2, logc);

@@ -185,6 +185,6 @@ extern "C" int vpt_blackbody_xyz(const float* table, float t, float* out) {
     vpt::spectrum_to_xyz(t, out);
     return VPT_OK;
   }
-  vpt::blackbody_xyz(S, t, out[0], out[1], out[2]);
+  vpt::blackbody_xyz(S, S.bb, t, out[0], out[1], out[2]);
   return VPT_OK;
 }
