@@ -253,8 +253,8 @@ __global__ void vpt_majorant_trace_kernel(const DevScene* scene, float ox, float
   lane_init(ln);
   int n = 0;
   if (begin_ray(G, ln, o, ray_dir_setup(G, d))) {
-    while (ln.T0 < ln.T1) {  // RayMajorantIterator::next: segments until the HDDA leaves [t0, t1]
-      ln.s_t0 = ln.T0;
+    while (ln.s_t1 < ln.T1) {  // RayMajorantIterator::next: segments until the HDDA leaves [t0, t1]
+      ln.s_t0 = ln.s_t1;
       while (!hdda_step(G, ln)) {
       }
       if (n < max_rows) {
@@ -305,8 +305,8 @@ __global__ void vpt_tile_cost_kernel(const DevScene* scene, float* cost) {
     if (!begin_ray(G, ln, S.cam_pos, ray_dir_setup(G, dv))) continue;
     int steps = 0;
     float tau = 0.0f;
-    while (ln.T0 < ln.T1 && steps < (1 << 16)) {
-      ln.s_t0 = ln.T0;
+    while (ln.s_t1 < ln.T1 && steps < (1 << 16)) {
+      ln.s_t0 = ln.s_t1;
       bool done;
       do {
         ++steps;

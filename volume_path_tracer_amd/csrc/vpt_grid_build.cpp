@@ -5,8 +5,9 @@
 //            (x = leaf index or -(2*dim+active), y = leaf majorant or tile value bits)
 //   cells128 int2[...]                     one entry per 128^3 cell over every upper node
 //   root     RootTileDev[]                 value tiles at the root (outside every upper node)
-//   walk8    uint32[r8_n.x][r8_n.y][r8_n.z] the HDDA fast path's word per cells8 entry: the majorant's
-//                                          bits for an interior cell, kWalkSlow otherwise
+//   walk8    uint32[w8_n.x][w8_n.y][w8_n.z] the HDDA fast path's word per cells8 entry: the majorant's
+//                                          bits for an interior cell, kWalkSlow otherwise; padded by
+//                                          kWalkPad cells of kWalkSlow on every side (w8_n = r8_n + 4)
 //   bricks   float[leaf][8][8][8][8]       per leaf voxel its whole 2x2x2 trilinear stencil (built
 //                                          from 9^3 apron bricks: the leaf's voxels plus the +1
 //                                          neighbours), NanoVDB SampleFromVoxels semantics
@@ -142,15 +143,25 @@ void compute_runs(HostGrid& h, int threads) {
 }
 
 void build_walk_table(HostGrid& h, int threads) {
-  const size_t n = h.cells8.size();
+  DevGrid& G = h.dev;
+  const int32_t nx = G.r8_n[0], ny = G.r8_n[1], nz = G.r8_n[2];
+  for (int a = 0; a < 3; ++a) {
+    G.w8_org[a] = G.r8_org[a] - 8 * kWalkPad;
+    G.w8_n[a] = G.r8_n[a] + 2 * kWalkPad;
+  }
+  const size_t n = (size_t)G.w8_n[0] * G.w8_n[1] * G.w8_n[2];
+  G.w8_max = (uint32_t)(n - 1);
   h.walk8.assign(n, kWalkSlow);
-  parallel_for((int64_t)n, threads, [&](int64_t b0, int64_t e0) {
-    for (int64_t q = b0; q < e0; ++q) {
-      const int32_t x = h.cells8[q].x;
-      if (!cell8_interior(x)) continue;
-      const float m = majorant_of(Cell{cell8_code(x), math::as_f32((uint32_t)h.cells8[q].y)});
-      h.walk8[q] = math::as_u32(m);
-    }
+  parallel_for((int64_t)nx, threads, [&](int64_t b0, int64_t e0) {
+    for (int64_t a = b0; a < e0; ++a)
+      for (int32_t b = 0; b < ny; ++b)
+        for (int32_t c = 0; c < nz; ++c) {
+          const size_t q = ((size_t)a * ny + b) * nz + c;
+          const int32_t x = h.cells8[q].x;
+          if (!cell8_interior(x)) continue;
+          const float m = majorant_of(Cell{cell8_code(x), math::as_f32((uint32_t)h.cells8[q].y)});
+          h.walk8[((size_t)(a + kWalkPad) * G.w8_n[1] + (b + kWalkPad)) * G.w8_n[2] + (c + kWalkPad)] = math::as_u32(m);
+        }
   });
   h.dev.walk8 = h.walk8.data();
 }
@@ -343,6 +354,7 @@ int build_host_grid(const vpt_grid_desc& d, bool fix, int threads, HostGrid& out
     out.root.push_back(r);
   }
   G.root_count = (int32_t)out.root.size();
+  G.leaf_count = (int32_t)nleaf;
   G.cells8 = out.cells8.data();
   G.cells128 = out.cells128.data();
   G.root = out.root.data();

@@ -39,11 +39,13 @@ struct DevGrid {
   float background;
   int32_t bbox_min[3], bbox_max[3];  // indexBBox (inclusive)
   int32_t r8_org[3], r8_n[3];        // dense 8^3-cell table over all lower nodes
+  int32_t w8_org[3], w8_n[3];        // walk8: the r8 table padded by kWalkPad cells on every side
+  uint32_t w8_max;                   // last walk8 index
   int32_t r128_org[3], r128_n[3];    // dense 128^3-cell table over all upper nodes
-  int32_t root_count, pad0;
+  int32_t root_count, leaf_count;
   const int2* cells8;
   const uint8_t* runs8;  // per cells8 entry: run radius (see mark_runs), for the Runs kernel variant
-  const uint32_t* walk8; // per cells8 entry: the majorant's bits if the cell is interior, else kWalkSlow
+  const uint32_t* walk8; // per (padded) cells8 entry: the majorant's bits if the cell is interior, else kWalkSlow
   const int2* cells128;
   const RootTileDev* root;
   const float* bricks;  // [leaf][8][8][8][8]: per leaf voxel its 2x2x2 trilinear stencil (see brick_index)
@@ -88,6 +90,10 @@ constexpr int32_t kInteriorBit = 1 << 30;
 // walk8 entry of a cell the HDDA fast path cannot take (not interior; or an interior cell whose
 // majorant has exactly these NaN bits, which then takes the general path -- same result).
 constexpr uint32_t kWalkSlow = 0xFFFFFFFFu;
+// Cells of kWalkSlow padding around the walk table.  The HDDA prefetches the walk word of the cell
+// it is about to enter whenever it walks at dim 8; that cell is at most 2 cells outside the r8 table
+// (see hdda_prefetch), so the prefetch needs no bounds test.
+constexpr int32_t kWalkPad = 2;
 __host__ __device__ __forceinline__ int32_t cell8_code(int32_t x) {
   return (x & ~kInteriorBit) | ((x >> 1) & kInteriorBit);
 }
@@ -422,7 +428,8 @@ struct Lane {
   float scale, rscale;  // m_scale and recip_for_div(m_scale)
   float maj;
   int32_t dim;
-  float T0, T1;
+  float Tn, T1;     // Tn: HDDA time of the pending cell (the one the HDDA has been advanced into)
+  uint32_t pw;      // walk word of the pending cell (prefetched; kWalkSlow when not at dim 8)
   float nxt[3];
   int32_t vox[3];
   float finc[3];    // HDDA: dim * delta[axis] (the float product NanoVDB adds at every step)
@@ -462,6 +469,49 @@ __host__ __device__ __forceinline__ RayDir ray_dir_setup(const DevGrid& g, const
   r.scale = math::rcp_rn(math::sqrt_rn(jx * jx + jy * jy + jz * jz));
   r.rscale = math::recip_for_div(r.scale);
   return r;
+}
+
+// HDDA::step() without the time test: axis = MinIndex(next), mNext[axis] += mDim * mDelta[axis],
+// mVoxel[axis] += mDim * mStep[axis]; returns the new time.  Written as selects
+// over all three axes: branches (or an axis index) make the compiler move the HDDA state into an
+// indexed scratch array.
+__host__ __device__ __forceinline__ float hdda_advance(Lane& ln) {
+  const float n0 = ln.nxt[0], n1 = ln.nxt[1], n2 = ln.nxt[2];
+  const bool a0 = n0 < n1 && n0 < n2;
+  const bool a1 = !a0 && n1 < n2;
+  const bool a2 = !a0 && !a1;
+  const float tn = a0 ? n0 : (a1 ? n1 : n2);
+  ln.nxt[0] = a0 ? tn + ln.finc[0] : n0;
+  ln.nxt[1] = a1 ? tn + ln.finc[1] : n1;
+  ln.nxt[2] = a2 ? tn + ln.finc[2] : n2;
+  ln.vox[0] += a0 ? ln.vinc[0] : 0;
+  ln.vox[1] += a1 ? ln.vinc[1] : 0;
+  ln.vox[2] += a2 ? ln.vinc[2] : 0;
+  return tn;
+}
+
+// Walk-table index of the 8^3 cell holding voxel v (padded table).  The min() only guarantees a
+// memory-safe address; hdda_prefetch never asks for a cell beyond the padding.
+__host__ __device__ __forceinline__ uint32_t walk_index(const DevGrid& g, const int32_t v[3]) {
+  const uint32_t a = (uint32_t)((v[0] - g.w8_org[0]) >> 3), b = (uint32_t)((v[1] - g.w8_org[1]) >> 3),
+                 c = (uint32_t)((v[2] - g.w8_org[2]) >> 3);
+  const uint32_t idx = math::mul24(math::mul24(a, (uint32_t)g.w8_n[1]) + b, (uint32_t)g.w8_n[2]) + c;
+  return idx < g.w8_max ? idx : g.w8_max;
+}
+
+// The HDDA runs one step ahead of the segment logic: after a step has examined its cell (or at
+// begin_ray) the HDDA advances into the next cell (Tn = its entry time) and issues the load of that
+// cell's walk word, which the next step consumes -- the load is in flight while the lane draws
+// and the wavefront runs its other blocks.  The advance is the one the next step would make: the
+// HDDA state only changes in the step's slow path, which runs before the pre-advance.
+// Padding argument (kWalkPad = 2): at dim 8 the current cell is within one cell of the r8 table (it
+// was reached from an interior cell, or its lookahead cell -- within ~1 voxel -- has dim 8 and so
+// lies in the table), and the next cell is adjacent to it.
+__host__ __device__ __forceinline__ void hdda_pre_advance(const DevGrid& g, Lane& ln) {
+  ln.Tn = hdda_advance(ln);
+  uint32_t w = kWalkSlow;
+  if (ln.dim == 8) w = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(g.walk8) + walk_index(g, ln.vox) * 4u);
+  ln.pw = w;
 }
 
 // Volume::intersect (volume.cpp:78-88) + RayMajorantIterator ctor (volume.cpp:90-98).
@@ -504,8 +554,8 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
   // voxel answers every query of its d^3 block alike, so c0 gives the first segment's majorant.
   ln.maj = majorant_of(c0);
   ln.dim = dim;
-  ln.T0 = t0;
   ln.T1 = t1;
+  ln.s_t1 = t0;  // the sampler's position: NEED_SEG starts the first segment here
   const float P[3] = {px, py, pz}, D[3] = {dx, dy, dz};
   for (int a = 0; a < 3; ++a) {
     int32_t v = ((int32_t)floorf(P[a])) & (~(dim - 1));
@@ -519,101 +569,77 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
     else
       ln.nxt[a] = t0 + ((float)v - P[a]) * I[a];
   }
+  hdda_pre_advance(g, ln);
   ln.sm = SM_NEED_SEG;
   return true;
 }
 
-// HDDA::step() without the time test: axis = MinIndex(next), mNext[axis] += mDim * mDelta[axis],
-// mVoxel[axis] += mDim * mStep[axis]; returns the new time (also stored in T0).  Written as selects
-// over all three axes: branches (or an axis index) make the compiler move the HDDA state into an
-// indexed scratch array.
-__host__ __device__ __forceinline__ float hdda_advance(Lane& ln) {
-  const float n0 = ln.nxt[0], n1 = ln.nxt[1], n2 = ln.nxt[2];
-  const bool a0 = n0 < n1 && n0 < n2;
-  const bool a1 = !a0 && n1 < n2;
-  const bool a2 = !a0 && !a1;
-  const float tn = a0 ? n0 : (a1 ? n1 : n2);
-  ln.nxt[0] = a0 ? tn + ln.finc[0] : n0;
-  ln.nxt[1] = a1 ? tn + ln.finc[1] : n1;
-  ln.nxt[2] = a2 ? tn + ln.finc[2] : n2;
-  ln.vox[0] += a0 ? ln.vinc[0] : 0;
-  ln.vox[1] += a1 ? ln.vinc[1] : 0;
-  ln.vox[2] += a2 ? ln.vinc[2] : 0;
-  ln.T0 = tn;
-  return tn;
-}
-
-// One iteration of the do-while in RayMajorantIterator::next (volume.cpp:53-71).
+// One iteration of the do-while in RayMajorantIterator::next (volume.cpp:53-71), on the pending
+// cell (the HDDA was advanced into it by the previous step or by begin_ray, see hdda_pre_advance).
 // Returns true when the segment [s_t0, s_t1) with majorant s_dmaj is complete.
 // Runs: the grid's run radii (runs8) let an interior step that keeps the majorant take the next r
 // HDDA steps without loading their cells (grids with large equal-majorant regions, e.g. C2).
 template <bool Runs = false>
 __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
   ln.s_dmaj = ln.maj;
-  const float tn = hdda_advance(ln);
-  if (!(tn <= ln.T1)) {
+  const float tk = ln.Tn;  // the step's time (HDDA::step's mT0)
+  if (!(tk <= ln.T1)) {
     ln.s_t1 = ln.T1;
     return true;
   }
-  // Fast path: at dim 8 in an interior cell the lookahead point (within ~1 voxel of the cell)
-  // lies in a dim-8 cell, so getDim answers 8 == dim and HDDA::update is a no-op.  One 4-byte load
-  // of the walk table answers both "interior?" and the majorant; 24-bit index arithmetic (the table
-  // has < 2^24 cells per axis product) and a 32-bit byte offset from the table base.
-  if (ln.dim == 8) {
-    const int32_t a = (ln.vox[0] - g.r8_org[0]) >> 3, b = (ln.vox[1] - g.r8_org[1]) >> 3,
-                  c = (ln.vox[2] - g.r8_org[2]) >> 3;
-    if ((uint32_t)a < (uint32_t)g.r8_n[0] && (uint32_t)b < (uint32_t)g.r8_n[1] && (uint32_t)c < (uint32_t)g.r8_n[2]) {
-      const uint32_t idx = math::mul24(math::mul24((uint32_t)a, (uint32_t)g.r8_n[1]) + (uint32_t)b, (uint32_t)g.r8_n[2]) + (uint32_t)c;
-      const uint32_t w = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(g.walk8) + idx * 4u);
-      const int32_t run = Runs ? (int32_t)g.runs8[idx] : 0;
-      if (w != kWalkSlow) {
-        const float m = math::as_f32(w);
-        ln.maj = m;
-        if (m == ln.s_dmaj) {
-          if (Runs) {
-            for (int32_t r = run; r > 0; --r) {
-              ++ln.n_dda;
-              if (!(hdda_advance(ln) <= ln.T1)) {
-                ln.s_t1 = ln.T1;
-                return true;
-              }
-            }
-          }
-          return false;
+  // Fast path: at dim 8 in an interior cell the lookahead point (within ~1 voxel of the cell) lies
+  // in a dim-8 cell, so getDim answers 8 == dim and HDDA::update is a no-op; the prefetched walk word
+  // answers both "interior?" and the majorant.
+  const uint32_t w = ln.pw;
+  if (w != kWalkSlow) {
+    const float m = math::as_f32(w);
+    ln.maj = m;
+    if (Runs && m == ln.s_dmaj) {
+      // an interior cell lies in the r8 table: its run radius from the unpadded index
+      const uint32_t a = (uint32_t)((ln.vox[0] - g.r8_org[0]) >> 3), b = (uint32_t)((ln.vox[1] - g.r8_org[1]) >> 3),
+                     c = (uint32_t)((ln.vox[2] - g.r8_org[2]) >> 3);
+      for (int32_t r = (int32_t)g.runs8[math::mul24(math::mul24(a, (uint32_t)g.r8_n[1]) + b, (uint32_t)g.r8_n[2]) + c]; r > 0;
+           --r) {
+        ++ln.n_dda;
+        const float t = hdda_advance(ln);
+        if (!(t <= ln.T1)) {
+          ln.Tn = t;
+          ln.s_t1 = ln.T1;
+          return true;
         }
-        ln.s_t1 = ln.T0;
-        return true;
       }
     }
-  }
-  // new_dim = max(8, getDim(floor(ray(time + 1.0001f))))
-  float tl = ln.T0 + 1.0001f;
-  const int32_t lx = (int32_t)floorf(ln.e[0] + ln.d[0] * tl), ly = (int32_t)floorf(ln.e[1] + ln.d[1] * tl),
-                lz = (int32_t)floorf(ln.e[2] + ln.d[2] * tl);
-  Cell la = cell_at(g, lx, ly, lz);
-  int32_t nd = hdda_dim_of(la);
-  // HDDA::update(ray, dim)
-  if (nd != ln.dim) {
-    ln.dim = nd;
-    const float P[3] = {ln.e[0] + ln.d[0] * ln.T0, ln.e[1] + ln.d[1] * ln.T0, ln.e[2] + ln.d[2] * ln.T0};
-    for (int b = 0; b < 3; ++b) ln.vox[b] = ((int32_t)floorf(P[b])) & (~(nd - 1));
-    for (int b = 0; b < 3; ++b) {
-      const float inv = math::rcp_rn(ln.d[b]);  // == the ray's invDir (begin_ray / scene_finalize)
-      const int32_t st = hdda_stp(ln.d[b], inv);
-      ln.finc[b] = (float)nd * fabsf(inv);
-      ln.vinc[b] = nd * st;
-      if (st == 0) continue;
-      float n = ln.T0 + ((float)ln.vox[b] - P[b]) * inv;
-      if (st > 0) n += (float)nd * inv;
-      ln.nxt[b] = n;
+  } else {
+    // new_dim = max(8, getDim(floor(ray(time + 1.0001f))))
+    float tl = tk + 1.0001f;
+    const int32_t lx = (int32_t)floorf(ln.e[0] + ln.d[0] * tl), ly = (int32_t)floorf(ln.e[1] + ln.d[1] * tl),
+                  lz = (int32_t)floorf(ln.e[2] + ln.d[2] * tl);
+    Cell la = cell_at(g, lx, ly, lz);
+    int32_t nd = hdda_dim_of(la);
+    // HDDA::update(ray, dim)
+    if (nd != ln.dim) {
+      ln.dim = nd;
+      const float P[3] = {ln.e[0] + ln.d[0] * tk, ln.e[1] + ln.d[1] * tk, ln.e[2] + ln.d[2] * tk};
+      for (int b = 0; b < 3; ++b) ln.vox[b] = ((int32_t)floorf(P[b])) & (~(nd - 1));
+      for (int b = 0; b < 3; ++b) {
+        const float inv = math::rcp_rn(ln.d[b]);  // == the ray's invDir (begin_ray / scene_finalize)
+        const int32_t st = hdda_stp(ln.d[b], inv);
+        ln.finc[b] = (float)nd * fabsf(inv);
+        ln.vinc[b] = nd * st;
+        if (st == 0) continue;
+        float n = tk + ((float)ln.vox[b] - P[b]) * inv;
+        if (st > 0) n += (float)nd * inv;
+        ln.nxt[b] = n;
+      }
     }
+    // update_current_majorant at the (new) voxel: the lookahead cell answers it when both points lie
+    // in the same 8^3 cell (every query is a function of the 8^3 cell), saving a dependent load.
+    const int32_t dx = (ln.vox[0] ^ lx) | (ln.vox[1] ^ ly) | (ln.vox[2] ^ lz);
+    ln.maj = majorant_of((dx >= 0 && dx < 8) ? la : cell_at(g, ln.vox[0], ln.vox[1], ln.vox[2]));
   }
-  // update_current_majorant at the (new) voxel: the lookahead cell answers it when both points lie
-  // in the same 8^3 cell (every query is a function of the 8^3 cell), saving a dependent load.
-  const int32_t dx = (ln.vox[0] ^ lx) | (ln.vox[1] ^ ly) | (ln.vox[2] ^ lz);
-  ln.maj = majorant_of((dx >= 0 && dx < 8) ? la : cell_at(g, ln.vox[0], ln.vox[1], ln.vox[2]));
+  hdda_pre_advance(g, ln);  // the next step's advance, and its cell's walk word in flight
   if (ln.maj == ln.s_dmaj) return false;
-  ln.s_t1 = ln.T0;
+  ln.s_t1 = tk;
   return true;
 }
 
@@ -1141,12 +1167,13 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       if (ln.sm == SM_NEED_SEG) {
         env.prof(PB_NEED_SEG);
         // RayMajorantIterator::next prologue (volume.cpp:40-51)
-        if (ln.T0 >= ln.T1) {
+        // the sampler's position is the previous segment's end (or the clip entry, begin_ray)
+        if (ln.s_t1 >= ln.T1) {
           // the sampler ran dry: a shadow ray keeps T_ray; a primary ray did not scatter (break)
           ln.state = ln.shadow ? ST_NEE_DONE : ST_FINISH;
           env.prof(PB_NONE);
         } else {
-          ln.s_t0 = ln.T0;
+          ln.s_t0 = ln.s_t1;
           ln.sm = SM_STEP;
         }
       }
