@@ -6,7 +6,8 @@
 //   cells128 int2[...]                     one entry per 128^3 cell over every upper node
 //   root     RootTileDev[]                 value tiles at the root (outside every upper node)
 //   walk8    uint32[w8_n.x][w8_n.y][w8_n.z] the HDDA fast path's word per cells8 entry: the majorant's
-//                                          bits for an interior cell, kWalkSlow otherwise; padded by
+//                                          bits for an interior cell, the bits | kWalkEdge for another
+//                                          dim-8 cell, kWalkSlow otherwise; padded by
 //                                          kWalkPad cells of kWalkSlow on every side (w8_n = r8_n + 4)
 //   bricks   float[leaf][8][8][8][8]       per leaf voxel its whole 2x2x2 trilinear stencil (built
 //                                          from 9^3 apron bricks: the leaf's voxels plus the +1
@@ -158,9 +159,12 @@ void build_walk_table(HostGrid& h, int threads) {
         for (int32_t c = 0; c < nz; ++c) {
           const size_t q = ((size_t)a * ny + b) * nz + c;
           const int32_t x = h.cells8[q].x;
-          if (!cell8_interior(x)) continue;
-          const float m = majorant_of(Cell{cell8_code(x), math::as_f32((uint32_t)h.cells8[q].y)});
-          h.walk8[((size_t)(a + kWalkPad) * G.w8_n[1] + (b + kWalkPad)) * G.w8_n[2] + (c + kWalkPad)] = math::as_u32(m);
+          const int32_t code = cell8_code(x);
+          if (!cell8_dim8(code)) continue;
+          const uint32_t m = math::as_u32(majorant_of(Cell{code, math::as_f32((uint32_t)h.cells8[q].y)}));
+          if (m & kWalkEdge) continue;  // a majorant with the sign bit set: general path (same result)
+          h.walk8[((size_t)(a + kWalkPad) * G.w8_n[1] + (b + kWalkPad)) * G.w8_n[2] + (c + kWalkPad)] =
+              cell8_interior(x) ? m : (m | kWalkEdge);
         }
   });
   h.dev.walk8 = h.walk8.data();
@@ -173,7 +177,7 @@ void mark_interior(const DevGrid& G, std::vector<int2>& cells8, int threads) {
   const int32_t nx = G.r8_n[0], ny = G.r8_n[1], nz = G.r8_n[2];
   if (cells8.empty() || nx < 3 || ny < 3 || nz < 3) return;
   auto at = [&](int32_t a, int32_t b, int32_t c) -> int32_t { return cells8[((size_t)a * ny + b) * nz + c].x; };
-  auto dim8 = [](int32_t x) { return x >= 0 || x == -16 || x == -17; };
+  auto dim8 = [](int32_t x) { return cell8_dim8(x); };
   // pass 1: per cell, are the 3 cells along z all dim 8; pass 2 over y, pass 3 over x
   std::vector<uint8_t> d((size_t)nx * ny * nz), ez(d.size()), ey(d.size());
   parallel_for(nx, threads, [&](int64_t b0, int64_t e0) {

@@ -90,10 +90,17 @@ constexpr int32_t kInteriorBit = 1 << 30;
 // walk8 entry of a cell the HDDA fast path cannot take (not interior; or an interior cell whose
 // majorant has exactly these NaN bits, which then takes the general path -- same result).
 constexpr uint32_t kWalkSlow = 0xFFFFFFFFu;
+// walk8 flag of a dim-8 cell that is not interior (an "edge" cell: some cell of its 3x3x3
+// neighbourhood is not dim 8).  Its low bits are the cell's majorant; the fast path holds for a step
+// whose lookahead point lies in the cell itself.  Majorants with the sign bit set are stored as
+// kWalkSlow.
+constexpr uint32_t kWalkEdge = 0x80000000u;
 // Cells of kWalkSlow padding around the walk table.  The HDDA prefetches the walk word of the cell
 // it is about to enter whenever it walks at dim 8; that cell is at most 2 cells outside the r8 table
 // (see hdda_prefetch), so the prefetch needs no bounds test.
 constexpr int32_t kWalkPad = 2;
+// A cells8 code whose cell has HDDA dim 8: a leaf (code >= 0) or a lower-node tile (-16 / -17).
+__host__ __device__ __forceinline__ bool cell8_dim8(int32_t code) { return code >= 0 || code == -16 || code == -17; }
 __host__ __device__ __forceinline__ int32_t cell8_code(int32_t x) {
   return (x & ~kInteriorBit) | ((x >> 1) & kInteriorBit);
 }
@@ -591,7 +598,7 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
   // in a dim-8 cell, so getDim answers 8 == dim and HDDA::update is a no-op; the prefetched walk word
   // answers both "interior?" and the majorant.
   const uint32_t w = ln.pw;
-  if (w != kWalkSlow) {
+  if ((int32_t)w >= 0) {
     const float m = math::as_f32(w);
     ln.maj = m;
     if (Runs && m == ln.s_dmaj) {
@@ -614,28 +621,35 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
     float tl = tk + 1.0001f;
     const int32_t lx = (int32_t)floorf(ln.e[0] + ln.d[0] * tl), ly = (int32_t)floorf(ln.e[1] + ln.d[1] * tl),
                   lz = (int32_t)floorf(ln.e[2] + ln.d[2] * tl);
-    Cell la = cell_at(g, lx, ly, lz);
-    int32_t nd = hdda_dim_of(la);
-    // HDDA::update(ray, dim)
-    if (nd != ln.dim) {
-      ln.dim = nd;
-      const float P[3] = {ln.e[0] + ln.d[0] * tk, ln.e[1] + ln.d[1] * tk, ln.e[2] + ln.d[2] * tk};
-      for (int b = 0; b < 3; ++b) ln.vox[b] = ((int32_t)floorf(P[b])) & (~(nd - 1));
-      for (int b = 0; b < 3; ++b) {
-        const float inv = math::rcp_rn(ln.d[b]);  // == the ray's invDir (begin_ray / scene_finalize)
-        const int32_t st = hdda_stp(ln.d[b], inv);
-        ln.finc[b] = (float)nd * fabsf(inv);
-        ln.vinc[b] = nd * st;
-        if (st == 0) continue;
-        float n = tk + ((float)ln.vox[b] - P[b]) * inv;
-        if (st > 0) n += (float)nd * inv;
-        ln.nxt[b] = n;
+    const int32_t dl = (ln.vox[0] ^ lx) | (ln.vox[1] ^ ly) | (ln.vox[2] ^ lz);
+    if (w != kWalkSlow && dl >= 0 && dl < 8) {
+      // An edge cell (dim 8, not interior) whose lookahead point lies in the cell itself: getDim
+      // answers the cell's dim, 8 == dim, and update_current_majorant the cell's majorant.
+      ln.maj = math::as_f32(w & ~kWalkEdge);
+    } else {
+      Cell la = cell_at(g, lx, ly, lz);
+      int32_t nd = hdda_dim_of(la);
+      // HDDA::update(ray, dim)
+      if (nd != ln.dim) {
+        ln.dim = nd;
+        const float P[3] = {ln.e[0] + ln.d[0] * tk, ln.e[1] + ln.d[1] * tk, ln.e[2] + ln.d[2] * tk};
+        for (int b = 0; b < 3; ++b) ln.vox[b] = ((int32_t)floorf(P[b])) & (~(nd - 1));
+        for (int b = 0; b < 3; ++b) {
+          const float inv = math::rcp_rn(ln.d[b]);  // == the ray's invDir (begin_ray / scene_finalize)
+          const int32_t st = hdda_stp(ln.d[b], inv);
+          ln.finc[b] = (float)nd * fabsf(inv);
+          ln.vinc[b] = nd * st;
+          if (st == 0) continue;
+          float n = tk + ((float)ln.vox[b] - P[b]) * inv;
+          if (st > 0) n += (float)nd * inv;
+          ln.nxt[b] = n;
+        }
       }
+      // update_current_majorant at the (new) voxel: the lookahead cell answers it when both points lie
+      // in the same 8^3 cell (every query is a function of the 8^3 cell), saving a dependent load.
+      const int32_t dx = (ln.vox[0] ^ lx) | (ln.vox[1] ^ ly) | (ln.vox[2] ^ lz);
+      ln.maj = majorant_of((dx >= 0 && dx < 8) ? la : cell_at(g, ln.vox[0], ln.vox[1], ln.vox[2]));
     }
-    // update_current_majorant at the (new) voxel: the lookahead cell answers it when both points lie
-    // in the same 8^3 cell (every query is a function of the 8^3 cell), saving a dependent load.
-    const int32_t dx = (ln.vox[0] ^ lx) | (ln.vox[1] ^ ly) | (ln.vox[2] ^ lz);
-    ln.maj = majorant_of((dx >= 0 && dx < 8) ? la : cell_at(g, ln.vox[0], ln.vox[1], ln.vox[2]));
   }
   hdda_pre_advance(g, ln);  // the next step's advance, and its cell's walk word in flight
   if (ln.maj == ln.s_dmaj) return false;
