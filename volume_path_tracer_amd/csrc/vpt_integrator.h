@@ -635,8 +635,11 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
         const float P[3] = {ln.e[0] + ln.d[0] * tk, ln.e[1] + ln.d[1] * tk, ln.e[2] + ln.d[2] * tk};
         for (int b = 0; b < 3; ++b) ln.vox[b] = ((int32_t)floorf(P[b])) & (~(nd - 1));
         for (int b = 0; b < 3; ++b) {
-          const float inv = math::rcp_rn(ln.d[b]);  // == the ray's invDir (begin_ray / scene_finalize)
-          const int32_t st = hdda_stp(ln.d[b], inv);
+          // local_const: the direction is loop-invariant in the walk, and the compiler would compute
+          // invDir and the step signs before the loop and hold them in registers for this rare block.
+          const float db = local_const(ln.d[b]);
+          const float inv = math::rcp_rn(db);  // == the ray's invDir (begin_ray / scene_finalize)
+          const int32_t st = hdda_stp(db, inv);
           ln.finc[b] = (float)nd * fabsf(inv);
           ln.vinc[b] = nd * st;
           if (st == 0) continue;
