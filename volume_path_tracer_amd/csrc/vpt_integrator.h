@@ -70,17 +70,29 @@ struct Cell {
 // A constant materialised where it is used.  Literal operands a VOP3 or LDS instruction cannot
 // encode are otherwise hoisted out of the state-machine loop into a VGPR held for the whole kernel
 // (r02: four such VGPRs in the 72-VGPR production kernel).
+// The v_mov is part of the volatile asm, so the compiler can neither hoist nor share it.
 __host__ __device__ __forceinline__ int32_t local_const(int32_t c) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  asm volatile("" : "+v"(c));
-#endif
+  int32_t r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "i"(c));
+  return r;
+#else
   return c;
+#endif
 }
 __host__ __device__ __forceinline__ float local_const(float c) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  asm volatile("" : "+v"(c));
-#endif
+  return __builtin_bit_cast(float, local_const(__builtin_bit_cast(int32_t, c)));
+#else
   return c;
+#endif
+}
+// A value the compiler must treat as computed here (keeps loop-invariant work of a rare block in it).
+__host__ __device__ __forceinline__ float local_value(float v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(v));
+#endif
+  return v;
 }
 
 // cells8 entries carry one more bit: "interior" = this 8^3 cell and its 26 neighbours all have
@@ -635,9 +647,9 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
         const float P[3] = {ln.e[0] + ln.d[0] * tk, ln.e[1] + ln.d[1] * tk, ln.e[2] + ln.d[2] * tk};
         for (int b = 0; b < 3; ++b) ln.vox[b] = ((int32_t)floorf(P[b])) & (~(nd - 1));
         for (int b = 0; b < 3; ++b) {
-          // local_const: the direction is loop-invariant in the walk, and the compiler would compute
+          // local_value: the direction is loop-invariant in the walk, and the compiler would compute
           // invDir and the step signs before the loop and hold them in registers for this rare block.
-          const float db = local_const(ln.d[b]);
+          const float db = local_value(ln.d[b]);
           const float inv = math::rcp_rn(db);  // == the ray's invDir (begin_ray / scene_finalize)
           const int32_t st = hdda_stp(db, inv);
           ln.finc[b] = (float)nd * fabsf(inv);
