@@ -400,7 +400,9 @@ enum : int32_t {
   ST_SHADOW = 7,  // sample_Ld's Volume::intersect + iterator setup (direction wi: constants)
   ST_FINISH_T = 8 // pixel done after absorption / scatter past max_depth ("terminated": no env light)
 };
-enum : int32_t { SM_NEED_SEG = 0, SM_STEP = 1, SM_DRAW = 2, SM_EVAL = 3 };  // SM_EVAL: density at s_t0 pending
+// SM_EVAL: density at s_t0 pending.  SM_NONE: the lane is not sampling (state != ST_SAMPLE); every
+// transition out of ST_SAMPLE sets it, so the walk loop's blocks test sm alone.
+enum : int32_t { SM_NEED_SEG = 0, SM_STEP = 1, SM_DRAW = 2, SM_EVAL = 3, SM_NONE = 4 };
 // Block ids for the optional SIMT-utilisation profile (env.prof; a no-op unless VPT_PROFILE).
 enum : int32_t {
   PB_ITER = 0, PB_FETCH, PB_PIXEL, PB_RAY, PB_SAMPLE, PB_NEED_SEG, PB_STEP, PB_DRAW, PB_TRILINEAR,
@@ -496,10 +498,11 @@ __host__ __device__ __forceinline__ RayDir ray_dir_setup(const DevGrid& g, const
 // indexed scratch array.
 __host__ __device__ __forceinline__ float hdda_advance(Lane& ln) {
   const float n0 = ln.nxt[0], n1 = ln.nxt[1], n2 = ln.nxt[2];
+  const bool c12 = n1 < n2;
   const bool a0 = n0 < n1 && n0 < n2;
-  const bool a1 = !a0 && n1 < n2;
-  const bool a2 = !a0 && !a1;
-  const float tn = a0 ? n0 : (a1 ? n1 : n2);
+  const bool a1 = !a0 && c12;
+  const bool a2 = !(a0 || a1);
+  const float tn = a0 ? n0 : (c12 ? n1 : n2);
   ln.nxt[0] = a0 ? tn + ln.finc[0] : n0;
   ln.nxt[1] = a1 ? tn + ln.finc[1] : n1;
   ln.nxt[2] = a2 ? tn + ln.finc[2] : n2;
@@ -814,6 +817,7 @@ __host__ __device__ __forceinline__ void primary_event(const DevScene& S, const 
   }
   // ev == 0 (Null): keep drawing in the same segment.
   if (Debug && ev == 0) env.event(ln, VPT_EV_NULL, nullptr, nullptr, 0.0f);
+  if (ev != 0) ln.sm = SM_NONE;
 }
 
 // A tentative collision at s_t0 (SM_EVAL): density, then the primary path's event
@@ -868,6 +872,7 @@ __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const
         if (T <= 0.0f) {
           lc.Tr = -1.0f;  // returns Zero()
           ln.state = ST_NEE_DONE;
+          ln.sm = SM_NONE;
         }
       }
     } else if (!ln.shadow) {
@@ -891,6 +896,7 @@ __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const
       if (lc.Tr <= 0.0f) {
         lc.Tr = -1.0f;  // returns Zero()
         ln.state = ST_NEE_DONE;
+        ln.sm = SM_NONE;
       }
     }
   }
@@ -1200,6 +1206,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         if (ln.s_t1 >= ln.T1) {
           // the sampler ran dry: a shadow ray keeps T_ray; a primary ray did not scatter (break)
           ln.state = ln.shadow ? ST_NEE_DONE : ST_FINISH;
+          ln.sm = SM_NONE;
           env.prof(PB_NONE);
         } else {
           ln.s_t0 = ln.s_t1;
@@ -1207,7 +1214,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         }
       }
       env.tick(PT_SEG);
-      if (ln.state == ST_SAMPLE && ln.sm == SM_STEP) {
+      if (ln.sm == SM_STEP) {
         env.prof(PB_STEP);
         ++ln.n_dda;
         if (hdda_step<Runs>(G, ln)) {
@@ -1216,7 +1223,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         }
       }
       env.tick(PT_STEP);
-      if (ln.state == ST_SAMPLE && ln.sm == SM_DRAW) {
+      if (ln.sm == SM_DRAW) {
         env.prof(PB_DRAW);
         // MajorantTransmittanceSampler::next body (majorant_transmittance_sampler.cpp:39-79).  Most draws
         // overshoot the segment (C3: 45 of 57 per sample) and their distance is never used, so the
@@ -1267,7 +1274,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
 
 __host__ __device__ __forceinline__ void lane_init(Lane& ln) {
   ln.state = ST_FETCH;
-  ln.sm = SM_NEED_SEG;
+  ln.sm = SM_NONE;
   ln.shadow = 0;
   ln.temp_cell.i = kNoCell;
   ln.temp_cell.code = -1;
