@@ -43,3 +43,24 @@ def tiles_only_grid() -> capi.Grid:
                      leaf_max=np.zeros(0, np.float32),
                      tile_origin=[[0, 0, 0], [128, 0, 0], [0, 128, 8], [4096, 0, 0]],
                      tile_level=[2, 2, 1, 3], tile_value=[0.02, 0.0, 0.5, 0.01], tile_active=[1, 0, 1, 1])
+
+
+def signed_grid() -> capi.Grid:
+    """The 64^3 cloud with the leaves of one slab negated (negative leaf maxima, so negative
+    majorants deep in the slab and mixed signs at its faces), plus active lower-node tiles holding
+    -0.3 and -0.0: majorants with the sign bit set, which the walk table must not take for its
+    edge-cell flag (kWalkEdge)."""
+    base = SynthGrid(1, 64).grid(copy=True)
+    origin = base.leaf_origin.copy()
+    values = base.leaf_values.copy()
+    slab = origin[:, 0] < 32
+    values[slab] = -values[slab]
+    vmax = values.max(axis=1).astype(np.float32)
+    tiles = dict(tile_origin=[[64, 0, 0], [64, 8, 0], [64, 16, 8]], tile_level=[1, 1, 1],
+                 tile_value=[-0.3, -0.0, 0.2], tile_active=[1, 1, 1])
+    lo = np.minimum(origin.min(0), 0)
+    hi = np.maximum(origin.max(0) + 7, [71, 23, 15])
+    return capi.Grid(map_mat=list(base.desc.map_mat), map_inv_mat=list(base.desc.map_inv_mat),
+                     map_vec=list(base.desc.map_vec), background=0.0, bbox_min=lo.tolist(), bbox_max=hi.tolist(),
+                     leaf_origin=origin, leaf_values=values, leaf_max=vmax, leaf_value_mask=base.leaf_value_mask,
+                     **tiles)

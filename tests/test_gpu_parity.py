@@ -191,11 +191,11 @@ def _records_equal(wl, dens, temp, jid_begin, count):
     return c_o
 
 
-@pytest.mark.parametrize("case", ["tiles_only", "tiny_image", "odd_tiles", "no_jitter_single_pixel",
+@pytest.mark.parametrize("case", ["tiles_only", "signed_values", "tiny_image", "odd_tiles", "no_jitter_single_pixel",
                                   "unaligned_jobs", "max_depth_0", "beyond_num_waves"])
 def test_gpu_edge_cases_bit_exact(case):
     """Edge cases of the reference loop (worker.cpp:104-207) and of the tile/job mapping."""
-    from grids import look_at, tiles_only_grid
+    from grids import look_at, signed_grid, tiles_only_grid
 
     wl = workload("c3", width=24, height=16, spp=2, grid_n=64)
     dens = SynthGrid(1, 64).grid()
@@ -203,6 +203,8 @@ def test_gpu_edge_cases_bit_exact(case):
     if case == "tiles_only":
         dens = tiles_only_grid()
         look_at(wl.cfg, (-500.0, 30.0, -300.0), (500.0, 30.0, 60.0))
+    elif case == "signed_values":
+        dens = signed_grid()
     elif case == "tiny_image":
         wl.cfg.output_size[0], wl.cfg.output_size[1] = 5, 3
     elif case == "odd_tiles":

@@ -73,6 +73,23 @@ def test_sparse_grid_all_hdda_levels():
     assert c_o["density_evals"] > 1000 and c_o["dda_steps"] > 5 * c_o["samples"]
 
 
+def test_signed_values_grid():
+    """Negative leaf values and negative / -0.0 tile values (majorants with the sign bit set) through
+    the walk table's interior / edge / general paths."""
+    from grids import signed_grid
+
+    dens = signed_grid()
+    wl = workload("c3", width=40, height=32, spp=2, grid_n=64)
+    od = O.OracleGrid(dens, fix_majorants=True)
+    jobs = wl.cfg.jobs_per_wave() * 2
+    f_o, r_o, c_o = O.render_jobs(wl.cfg, od, None, 0, jobs, records=True)
+    f_h, r_h, c_h = HS.render_jobs(wl.cfg, dens, None, 0, jobs, records=True)
+    assert r_o.tobytes() == r_h.tobytes()
+    for k in ("dda_steps", "segments", "draws", "density_evals", "rng_draws"):
+        assert c_o[k] == c_h[k], k
+    assert c_o["density_evals"] > 100
+
+
 def test_tiles_only_grid():
     """A grid without leaves (upper/root/lower-node tiles only) through the device state machine."""
     from grids import look_at, tiles_only_grid
