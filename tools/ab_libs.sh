@@ -12,7 +12,7 @@ for L in ${LIBS}; do
 done
 for R in ${ROUNDS:-1 2}; do
   for L in ${LIBS}; do
-    VPT_LIB=$PWD/volume_path_tracer_amd/lib/$L.so timeout -k 10 300 python tools/tune.py --config ${CONFIG:-c3} --spp ${SPP:-256} --gates ${GATES:-6:12:32:4} --reps ${REPS:-2} "$@" > $O/$L.r$R.log 2>&1
+    VPT_LIB=$PWD/volume_path_tracer_amd/lib/$L.so timeout -k 10 300 python tools/tune.py --config ${CONFIG:-c3} --spp ${SPP:-256} --gates ${GATES:-6:8:36:4} --reps ${REPS:-2} "$@" > $O/$L.r$R.log 2>&1
     rc=$?; echo "$L round $R rc=$rc $(grep Msps $O/$L.r$R.log | tail -1 | grep -o '"ms".*')"; if [ $rc -ne 0 ]; then tail -3 $O/$L.r$R.log; exit $rc; fi
   done
 done

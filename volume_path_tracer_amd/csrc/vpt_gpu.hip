@@ -657,11 +657,12 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   ctx->grid_blocks = per_cu * cus;
   ctx->cus = cus > 0 ? cus : 1;
   // Scheduling defaults from tools/tune.py sweeps on MI355X (C3, 256 spp): rare states run for >= 6
-  // waiting lanes, density evaluations (with the deferred exact draw) for >= 32, everything runs when
-  // < 12 lanes are walking; the walk loops while >= 4 lanes walk.
+  // waiting lanes, density evaluations (with the deferred exact draw) for >= 36, everything runs when
+  // < 8 lanes are walking; the walk loops while >= 4 lanes walk (r02 sweep: 6:8:36:4 363.7 ms vs
+  // 6:12:32:4 366.6 ms, C4 103.7 vs 104.4).
   ctx->scene.gate_min = 6;
-  ctx->scene.gate_idle = 12;
-  ctx->scene.gate_eval = 32;
+  ctx->scene.gate_idle = 8;
+  ctx->scene.gate_eval = 36;
   ctx->scene.gate_walk = 4;
   ctx->scene.pixel_mode = 0;
   ctx->scene.tile_area = (uint32_t)(ctx->scene.tw * ctx->scene.th);
