@@ -29,6 +29,8 @@ def lib():
         L.vpths_probe.argtypes = [gp, C.POINTER(C.c_int32), C.c_int, fp, C.POINTER(C.c_int32), fp]
         L.vpths_check_runs.argtypes = [gp, C.POINTER(C.c_int64), C.POINTER(C.c_double)]
         L.vpths_check_runs.restype = C.c_int64
+        L.vpths_check_walk.argtypes = [gp, C.POINTER(C.c_int64)]
+        L.vpths_check_walk.restype = C.c_int64
         L.vpths_math_mismatches.argtypes = [C.c_int]
         L.vpths_math_mismatches.restype = C.c_int64
         L.vpths_pow2_mismatches.restype = C.c_int64

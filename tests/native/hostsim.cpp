@@ -152,6 +152,54 @@ extern "C" int vpths_probe(const vpt_grid_desc* d, const int32_t* ijk, int n, fl
   return 0;
 }
 
+// The HDDA walk table (build_walk_table) checked by brute force through cell_at: an interior word
+// (sign bit clear) needs all 27 cells of its neighbourhood at HDDA dim 8 and holds the cell's
+// majorant bits; an edge word (kWalkEdge set) needs the cell itself at dim 8 and holds its majorant
+// bits | kWalkEdge; every dim-8 cell of the r8 table whose majorant has the sign bit clear is one of
+// the two; the padding is kWalkSlow.  counts = {interior, edge, slow, padding}; returns violations.
+extern "C" int64_t vpths_check_walk(const vpt_grid_desc* d, int64_t* counts) {
+  vpt::HostGrid h;
+  if (vpt::build_host_grid(*d, true, 0, h)) return -1;
+  const vpt::DevGrid& G = h.dev;
+  auto bits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
+  int64_t bad = 0;
+  for (int k = 0; k < 4; ++k) counts[k] = 0;
+  for (int32_t a = 0; a < G.w8_n[0]; ++a)
+    for (int32_t b = 0; b < G.w8_n[1]; ++b)
+      for (int32_t c = 0; c < G.w8_n[2]; ++c) {
+        const uint32_t w = h.walk8[((size_t)a * G.w8_n[1] + b) * G.w8_n[2] + c];
+        const int32_t o[3] = {G.w8_org[0] + 8 * a, G.w8_org[1] + 8 * b, G.w8_org[2] + 8 * c};
+        const bool in_r8 = a >= vpt::kWalkPad && a < vpt::kWalkPad + G.r8_n[0] && b >= vpt::kWalkPad &&
+                           b < vpt::kWalkPad + G.r8_n[1] && c >= vpt::kWalkPad && c < vpt::kWalkPad + G.r8_n[2];
+        if (!in_r8) {
+          ++counts[3];
+          bad += w != vpt::kWalkSlow;
+          continue;
+        }
+        const vpt::Cell C = vpt::cell_at(G, o[0], o[1], o[2]);
+        const uint32_t m = bits(vpt::majorant_of(C));
+        const bool dim8 = vpt::hdda_dim_of(C) == 8;
+        if (w == vpt::kWalkSlow) {
+          ++counts[2];
+          bad += dim8 && !(m & vpt::kWalkEdge) && m != vpt::kWalkSlow;  // a fast cell left slow
+          continue;
+        }
+        if (w & vpt::kWalkEdge) {
+          ++counts[1];
+          bad += !dim8 || (m & vpt::kWalkEdge) || (w & ~vpt::kWalkEdge) != m;
+          continue;
+        }
+        ++counts[0];
+        bool all8 = true;
+        for (int da = -1; da <= 1; ++da)
+          for (int db = -1; db <= 1; ++db)
+            for (int dc = -1; dc <= 1; ++dc)
+              all8 = all8 && vpt::hdda_dim_of(vpt::cell_at(G, o[0] + 8 * da, o[1] + 8 * db, o[2] + 8 * dc)) == 8;
+        bad += !all8 || w != m;
+      }
+  return bad;
+}
+
 // Run radii (vpt::compute_runs) checked by brute force: every cell within Chebyshev distance r of a
 // cell with radius r is in the table, interior, and has the same majorant bits.  hist[r] = cells
 // with radius r (r = 0..15); *fraction = HostGrid::run_fraction; returns the violations.

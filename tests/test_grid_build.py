@@ -97,3 +97,23 @@ def test_run_radii_hold(which):
         assert frac.value >= 0.25 and hist[2:].sum() > 0
     if which.startswith("cloud"):
         assert frac.value < 0.25 and hist[1:].sum() > 0
+
+
+@pytest.mark.parametrize("which", ["cloud128", "constant", "sparse", "tiles_only", "signed"])
+def test_walk_table_words(which):
+    """The HDDA walk table (interior / edge / slow words, kWalkPad padding) against cell_at by brute
+    force (tests/native/hostsim.cpp vpths_check_walk): the fast paths' preconditions hold for every
+    word, and every dim-8 cell with a sign-clear majorant takes one of them."""
+    import ctypes as C
+    import grids
+    g = {"cloud128": lambda: SynthGrid(1, 128).grid(), "constant": lambda: SynthGrid(0, 128).grid(),
+         "sparse": grids.sparse_grid, "tiles_only": grids.tiles_only_grid, "signed": grids.signed_grid}[which]()
+    counts = np.zeros(4, np.int64)
+    bad = HS.lib().vpths_check_walk(C.byref(g.desc), counts.ctypes.data_as(C.POINTER(C.c_int64)))
+    assert bad == 0
+    interior, edge, slow, pad = counts.tolist()
+    assert pad > 0
+    if which in ("cloud128", "constant", "sparse"):
+        assert interior > 0 and edge > 0
+    if which == "signed":
+        assert slow > 0 and edge > 0  # negative majorants and the -0.0 tile stay slow
