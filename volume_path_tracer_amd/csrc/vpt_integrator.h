@@ -109,7 +109,7 @@ constexpr uint32_t kWalkSlow = 0xFFFFFFFFu;
 constexpr uint32_t kWalkEdge = 0x80000000u;
 // Cells of kWalkSlow padding around the walk table.  The HDDA prefetches the walk word of the cell
 // it is about to enter whenever it walks at dim 8; that cell is at most 2 cells outside the r8 table
-// (see hdda_prefetch), so the prefetch needs no bounds test.
+// (see hdda_pre_advance), so the prefetch needs no bounds test.
 constexpr int32_t kWalkPad = 2;
 // A cells8 code whose cell has HDDA dim 8: a leaf (code >= 0) or a lower-node tile (-16 / -17).
 __host__ __device__ __forceinline__ bool cell8_dim8(int32_t code) { return code >= 0 || code == -16 || code == -17; }
@@ -513,7 +513,7 @@ __host__ __device__ __forceinline__ float hdda_advance(Lane& ln) {
 }
 
 // Walk-table index of the 8^3 cell holding voxel v (padded table).  The min() only guarantees a
-// memory-safe address; hdda_prefetch never asks for a cell beyond the padding.
+// memory-safe address; hdda_pre_advance never asks for a cell beyond the padding.
 __host__ __device__ __forceinline__ uint32_t walk_index(const DevGrid& g, const int32_t v[3]) {
   const uint32_t a = (uint32_t)((v[0] - g.w8_org[0]) >> 3), b = (uint32_t)((v[1] - g.w8_org[1]) >> 3),
                  c = (uint32_t)((v[2] - g.w8_org[2]) >> 3);
@@ -532,7 +532,10 @@ __host__ __device__ __forceinline__ uint32_t walk_index(const DevGrid& g, const 
 __host__ __device__ __forceinline__ void hdda_pre_advance(const DevGrid& g, Lane& ln) {
   ln.Tn = hdda_advance(ln);
   uint32_t w = kWalkSlow;
-  if (ln.dim == 8) w = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(g.walk8) + walk_index(g, ln.vox) * 4u);
+  if (ln.dim == 8) {
+    const uint32_t off = walk_index(g, ln.vox) * 4u;
+    w = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(g.walk8) + off);
+  }
   ln.pw = w;
 }
 
@@ -558,8 +561,10 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
     }
     if (lo > t0) t0 = lo;
     if (hi < t1) t1 = hi;
-    if (t0 > t1) return false;
   }
+  // One test after the three slabs: t0 never decreases and t1 never increases (and neither becomes
+  // NaN), so an empty interval after any axis stays empty -- the same answer as Ray::clip's early exit.
+  if (t0 > t1) return false;
   ln.e[0] = ex;
   ln.e[1] = ey;
   ln.e[2] = ez;
@@ -584,12 +589,9 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
     ln.vox[a] = v;
     ln.finc[a] = (float)dim * fabsf(I[a]);
     ln.vinc[a] = dim * hdda_stp(D[a], I[a]);
-    if (D[a] == 0.0f)
-      ln.nxt[a] = 3.40282347e+38f;
-    else if (I[a] > 0)
-      ln.nxt[a] = t0 + ((float)(v + dim) - P[a]) * I[a];
-    else
-      ln.nxt[a] = t0 + ((float)v - P[a]) * I[a];
+    // HDDA::init: the next boundary at v + dim (I > 0) or v; none for D == 0 (selects, not branches)
+    const float n = t0 + ((float)(I[a] > 0 ? v + dim : v) - P[a]) * I[a];
+    ln.nxt[a] = D[a] == 0.0f ? 3.40282347e+38f : n;
   }
   hdda_pre_advance(g, ln);
   ln.sm = SM_NEED_SEG;
@@ -664,9 +666,11 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
         }
       }
       // update_current_majorant at the (new) voxel: the lookahead cell answers it when both points lie
-      // in the same 8^3 cell (every query is a function of the 8^3 cell), saving a dependent load.
+      // in the same nd^3 block, saving a dependent load.  nd = 8: every query is a function of the
+      // 8^3 cell; nd = 128 / 4096: the lookahead's cell is an upper-node tile / root tile /
+      // background, which covers its whole nd^3 block.  (Here ln.dim == nd.)
       const int32_t dx = (ln.vox[0] ^ lx) | (ln.vox[1] ^ ly) | (ln.vox[2] ^ lz);
-      ln.maj = majorant_of((dx >= 0 && dx < 8) ? la : cell_at(g, ln.vox[0], ln.vox[1], ln.vox[2]));
+      ln.maj = majorant_of((dx & ~(nd - 1)) == 0 ? la : cell_at(g, ln.vox[0], ln.vox[1], ln.vox[2]));
     }
   }
   hdda_pre_advance(g, ln);  // the next step's advance, and its cell's walk word in flight
@@ -711,12 +715,12 @@ __host__ __device__ __forceinline__ void sample_hg(const DevScene& S, const floa
 #endif
   float n2 = lx * lx + (ly * ly + lz * lz);  // local.normalize()
   if (n2 > 0.0f) {
-    float s = sqrtf(n2);
-    lx = lx / s;
-    ly = ly / s;
-    lz = lz / s;
-  }
-  // coordinate_system(w, x, y)
+    // three correctly rounded divisions by s through one reciprocal (vpt_math.h div_by_recip)
+    const float s = sqrtf(n2), rs = math::recip_for_div(s);
+    lx = math::div_by_recip(lx, s, rs);
+    ly = math::div_by_recip(ly, s, rs);
+    lz = math::div_by_recip(lz, s, rs);
+  }  // coordinate_system(w, x, y)
   float sign = copysignf(1.0f, w[2]);
   float a = -1.0f / (sign + w[2]);
   float b = w[0] * w[1] * a;
