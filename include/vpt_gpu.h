@@ -303,9 +303,18 @@ int vpt_gpu_counters(vpt_gpu_ctx* ctx, vpt_counters* out, int reset);
  * fewer than gate_idle lanes are walking rays; a tentative collision's density evaluation waits
  * for gate_eval lanes likewise; grid_blocks overrides the persistent grid size; the ray walk
  * repeats in an inner loop while >= gate_walk lanes walk (0: one step per pass).
- * Pass <= 0 (gate_idle, gate_walk < 0) to keep a value. */
+ * Pass <= 0 (gate_idle, gate_walk < 0) to keep a value; gate_idle 0 is rejected (VPT_E_INVALID): a
+ * wavefront with no walking lane must run its waiting blocks. */
 int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_blocks, int gate_eval,
                        int gate_walk);
+/* Latency-bound launches: a launch with fewer work items than its grid has lanes (e.g. C1, 4 096
+ * jobs) lasts as long as its slowest job.  Such launches spread their items over the grid's
+ * wavefronts -- the first wave_lanes lanes of each wavefront take jobs (0 = auto: ceil(items /
+ * wavefronts)) -- and run with their own gates (meaning as in vpt_gpu_set_tuning; defaults 1, 65, 1, 1:
+ * every block runs as soon as one lane needs it).  Results never depend on them.  Pass < 0 (gate_min,
+ * gate_eval: <= 0) to keep a value; gate_idle 0 is rejected. */
+int vpt_gpu_set_latency_tuning(vpt_gpu_ctx* ctx, int wave_lanes, int gate_min, int gate_idle, int gate_eval,
+                               int gate_walk);
 /* SIMT-utilisation profile of profiling builds (-DVPT_PROFILE): for each block of the lane state
  * machine, [wave executions, active lanes] as 2*21 uint64 (the last 7: lanes per state at each walk-loop iteration), then the shader cycles the wavefronts
  * spent in each of 10 sections (fetch, pixel, ray, walk-loop control, eval, nee, finish, and the

@@ -280,3 +280,42 @@ def test_concurrent_launches_on_three_streams():
     od, ot = _oracle_grids(dens, temp)
     f_o, _, _ = O.render_jobs(wl.cfg, od, ot, 0, T)
     _assert_bitwise(film.cpu().numpy(), f_o, "3-stream film")
+
+
+@pytest.mark.parametrize("name", ["c3", "c4"])
+def test_latency_launch_knobs_keep_films_bit_exact(name):
+    """Latency-bound launches (fewer jobs than grid lanes) spread their jobs over the wavefronts and run
+    with their own gates (vpt_gpu_set_latency_tuning); a launch that fills the grid uses the normal
+    path.  Every setting renders the oracle's single-wave films bit for bit, with equal counters."""
+    from volume_path_tracer_amd.render import Integrator
+
+    wl = workload(name, width=48, height=40, spp=12, grid_n=64)
+    dens, temp = _grids(wl)
+    it = Integrator(wl.cfg, dens, temp, device=0)
+    od, ot = _oracle_grids(dens, temp)
+    T = wl.cfg.jobs_per_wave()
+    ref = [O.render_jobs(wl.cfg, od, ot, w * T, T) for w in range(2)]
+    settings = [  # (wave_lanes, gate_min, gate_idle, gate_eval, gate_walk)
+        (0, 1, 65, 1, 1),    # the defaults: auto spreading, every block runs for one lane
+        (1, 1, 65, 1, 1),    # one lane per wavefront: some lanes take several jobs
+        (5, 6, 8, 36, 4),    # the throughput gates
+        (64, 2, 1, 64, 0),   # no spreading; evaluations only once no lane walks, one walk step per pass
+    ]
+    for s in settings:
+        it.set_latency_tuning(*s)
+        it.counters(reset=True)
+        for w in range(2):
+            _assert_bitwise(_prod_film(it, w * T, T), ref[w][0], f"{name} {s} wave {w + 1}")
+        c = it.counters()
+        for k in COUNTERS:
+            assert c[k] == ref[0][2][k] + ref[1][2][k], (s, k)
+    with pytest.raises(RuntimeError):
+        it.set_latency_tuning(0, 1, 0, 1, 1)  # gate_idle 0 could stall a wavefront: rejected
+    with pytest.raises(RuntimeError):
+        it.set_tuning(gate_idle=0)
+    # a grid of one block (256 lanes) that the 12 waves' 360 jobs fill: the throughput path
+    it.set_tuning(grid_blocks=1)
+    f_g = _prod_film(it, 0, 12 * T)
+    f_o, _, _ = O.render_jobs(wl.cfg, od, ot, 0, 12 * T)
+    np.testing.assert_array_equal(f_g[..., 3], 12.0)
+    np.testing.assert_allclose(f_g[..., :3], f_o[..., :3], rtol=1e-5, atol=1e-6)

@@ -9,6 +9,7 @@ ap.add_argument("--config", default="c3")
 ap.add_argument("--gates", default="16:16")
 ap.add_argument("--blocks", default="0")
 ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--lat", default="", help="latency-launch knobs wave_lanes:gate_min:gate_idle:gate_eval:gate_walk, comma-separated")
 ap.add_argument("--profile", action="store_true")
 ap.add_argument("--rng-mode", default="reference")
 ap.add_argument("--order", type=int, default=-1, help="job order mode (-1: library default)")
@@ -39,8 +40,10 @@ for g in a.gates.split(","):
     gm, gi = parts[0], parts[1]
     ge = parts[2] if len(parts) > 2 else 1
     gw = parts[3] if len(parts) > 3 else 0
-    for b in map(int, a.blocks.split(",")):
+    for b, lat in [(b, l) for b in map(int, a.blocks.split(",")) for l in (a.lat.split(",") if a.lat else [""])]:
         it.set_tuning(gm, gi, b if b > 0 else base_blocks, ge, gw)
+        if lat:
+            it.set_latency_tuning(*map(int, lat.split(":")))
         best = 1e9
         for _ in range(a.reps):
             it.film.zero_(); torch.cuda.synchronize(); t = time.perf_counter()
@@ -50,5 +53,5 @@ for g in a.gates.split(","):
         if a.profile:
             prof = it.profile(reset=True)
             print(json.dumps({"gate": g, "profile": prof}), flush=True)
-        print(json.dumps({"lib": os.environ.get("VPT_LIB", "default"), "order": a.order, "tail": a.tail, "gate": g, "blocks": b or base_blocks,
+        print(json.dumps({"lib": os.environ.get("VPT_LIB", "default"), "order": a.order, "tail": a.tail, "gate": g, "lat": lat, "blocks": b or base_blocks,
                           "spp": a.spp, "ms": round(ms, 2), "Msps": round(wl.cfg.width * wl.cfg.height * a.spp / best / 1e6, 2)}), flush=True)

@@ -157,7 +157,13 @@ struct KernelEnv {
   // lanes of this wavefront for which pred holds
   // (ballot_w64 on the bool itself: the compare folds into the mask, no materialised 0/1 VGPR)
   __device__ __forceinline__ int32_t count(bool pred) { return (int32_t)__popcll(__builtin_amdgcn_ballot_w64(pred)); }
-  __device__ __forceinline__ bool fetch_job(uint64_t& j) {
+  // wave_lanes: the lanes of each wavefront that take jobs (64: all; fewer in latency-bound launches,
+  // see render(); 0 = about items / wavefronts); the others end at their first fetch.  Any value >= 1
+  // renders every job: a lane takes jobs until none is left.
+  __device__ __forceinline__ bool fetch_job(uint64_t& j, int32_t wave_lanes) {
+    if (wave_lanes == 0)
+      wave_lanes = 1 + (int32_t)((float)jid_count * __builtin_amdgcn_rcpf((float)(gridDim.x * (kBlockThreads / 64))));
+    if ((int32_t)__lane_id() >= wave_lanes) return false;
     unsigned long long v = atomicAdd(job_counter, 1ULL);
     if (v >= jid_count) return false;
     j = v;
@@ -392,6 +398,11 @@ struct vpt_gpu_ctx {
   unsigned long long* counters = nullptr;
   unsigned long long* prof = nullptr;
   vpt::DevScene* scene_dev = nullptr;  // the kernel's copy of scene (read through ScenePtr)
+  // Latency-bound launches (fewer work items than the grid has lanes): their own gates (a second
+  // device copy of the scene with lat_gate[] in place of the gates) and jobs spread over wavefronts.
+  vpt::DevScene* scene_lat_dev = nullptr;
+  int lat_gate[4] = {1, 65, 1, 1};   // gate_min, gate_idle, gate_eval, gate_walk
+  int lat_wave_lanes = 0;            // 0: spread the items evenly over the grid's wavefronts
   hipStream_t stream = nullptr;
   bool use_runs = false;             // density-only kernel variant with run skipping (see create)
   int grid_blocks = 0;               // resident capacity (or the set_tuning override)
@@ -410,6 +421,8 @@ namespace {
 
 constexpr int kProfWords = 2 * vpt::PB_COUNT + vpt::PT_COUNT;
 constexpr uint32_t kLaunchSlots = 64;
+// Latency-bound launches: at most this many work items per wavefront of the grid (see render()).
+constexpr uint64_t kSpreadLanes = 6;
 
 int ctx_device(vpt_gpu_ctx* ctx);
 
@@ -419,6 +432,13 @@ int ctx_device(vpt_gpu_ctx* ctx);
 int push_scene(vpt_gpu_ctx* ctx) {
   VPT_HIP(hipDeviceSynchronize());
   VPT_HIP(hipMemcpy(ctx->scene_dev, &ctx->scene, sizeof(vpt::DevScene), hipMemcpyHostToDevice));
+  vpt::DevScene lat = ctx->scene;
+  lat.gate_min = ctx->lat_gate[0];
+  lat.gate_idle = ctx->lat_gate[1];
+  lat.gate_eval = ctx->lat_gate[2];
+  lat.gate_walk = ctx->lat_gate[3];
+  lat.wave_lanes = ctx->lat_wave_lanes;
+  VPT_HIP(hipMemcpy(ctx->scene_lat_dev, &lat, sizeof(vpt::DevScene), hipMemcpyHostToDevice));
   VPT_HIP(hipDeviceSynchronize());
   return VPT_OK;
 }
@@ -459,6 +479,7 @@ void destroy(vpt_gpu_ctx* ctx) {
   (void)hipFree(ctx->counters);
   (void)hipFree(ctx->prof);
   (void)hipFree(ctx->scene_dev);
+  (void)hipFree(ctx->scene_lat_dev);
   (void)hipFree(ctx->order);
   (void)hipFree(ctx->perm);
   for (uint32_t i = 0; i < kLaunchSlots; ++i)
@@ -531,7 +552,14 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   // items per lane (at least one block per CU).  C2: 1792 -> 768 blocks, 133 -> 143 Msps; C1: 256
   // blocks, 4.55 -> 4.84.  Same jobs, same samples.
   uint32_t blocks = (uint32_t)ctx->grid_blocks;
-  if (!ctx->grid_user) {
+  // Latency-bound launch (at most kSpreadLanes items per wavefront of the grid, e.g. C1's 4 096 jobs):
+  // the launch lasts as long as its slowest job, and a job runs fastest on a wavefront with few other
+  // paths (the wavefront executes every block any of its lanes needs).  Such a launch keeps the whole
+  // grid, the first ~items / wavefronts lanes of each wavefront take the jobs, and it runs with the
+  // latency gates (every block runs for one lane).  Measured, C1 (r02): 43.3 ms (256 blocks x 64
+  // lanes) -> 20.5 ms (1 792 blocks, one lane per wavefront, gates 1:65:1:1).  Same jobs, same samples.
+  const bool latency = env.jid_count <= kSpreadLanes * ((uint64_t)blocks * (vpt::kBlockThreads / 64));
+  if (!ctx->grid_user && !latency) {
     const uint64_t want = (env.jid_count * 3 / 4 + vpt::kBlockThreads - 1) / vpt::kBlockThreads;
     blocks = (uint32_t)std::min<uint64_t>(blocks, std::max<uint64_t>(want, (uint64_t)ctx->cus));
   }
@@ -569,7 +597,8 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
                      : ctx->use_runs
                          ? (dbg ? vpt::vpt_integrate_kernel<false, true, true> : vpt::vpt_integrate_kernel<false, false, true>)
                          : (dbg ? vpt::vpt_integrate_kernel<false, true, false> : vpt::vpt_integrate_kernel<false, false, false>);
-  hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, ctx->scene_dev, env, ctx->counters);
+  hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, latency ? ctx->scene_lat_dev : ctx->scene_dev,
+                     env, ctx->counters);
   VPT_HIP(hipGetLastError());
   const uint64_t npix = (uint64_t)ctx->scene.W * (uint64_t)ctx->scene.H;
   hipLaunchKernelGGL(vpt::vpt_count_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, ctx->scene_dev,
@@ -665,8 +694,10 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   ctx->scene.gate_eval = 36;
   ctx->scene.gate_walk = 4;
   ctx->scene.pixel_mode = 0;
+  ctx->scene.wave_lanes = 64;
   ctx->scene.tile_area = (uint32_t)(ctx->scene.tw * ctx->scene.th);
   VPT_HIP(hipMalloc((void**)&ctx->scene_dev, sizeof(vpt::DevScene)));
+  VPT_HIP(hipMalloc((void**)&ctx->scene_lat_dev, sizeof(vpt::DevScene)));
   if ((rc = push_scene(ctx.get()))) return rc;
   *out = ctx.release();
   return VPT_OK;
@@ -869,6 +900,8 @@ int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_b
   if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
   int rc = ctx_device(ctx);
   if (rc) return rc;
+  // gate_idle >= 1 is what guarantees progress: with no lane walking, every waiting block runs.
+  if (gate_idle == 0) return vpt::set_error(VPT_E_INVALID, "gate_idle must be >= 1 (0 can stall a wavefront)");
   if (gate_eval > 0) ctx->scene.gate_eval = gate_eval;
   if (gate_walk >= 0) ctx->scene.gate_walk = gate_walk;
   if (gate_min > 0) ctx->scene.gate_min = gate_min;
@@ -879,6 +912,21 @@ int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_b
     ctx->grid_user = true;
   }
   return VPT_OK;
+}
+
+int vpt_gpu_set_latency_tuning(vpt_gpu_ctx* ctx, int wave_lanes, int gate_min, int gate_idle, int gate_eval,
+                               int gate_walk) {
+  if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
+  if (wave_lanes > 64) return vpt::set_error(VPT_E_INVALID, "wave_lanes must be <= 64");
+  if (gate_idle == 0) return vpt::set_error(VPT_E_INVALID, "gate_idle must be >= 1 (0 can stall a wavefront)");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  if (wave_lanes >= 0) ctx->lat_wave_lanes = wave_lanes;
+  if (gate_min > 0) ctx->lat_gate[0] = gate_min;
+  if (gate_idle >= 0) ctx->lat_gate[1] = gate_idle;
+  if (gate_eval > 0) ctx->lat_gate[2] = gate_eval;
+  if (gate_walk >= 0) ctx->lat_gate[3] = gate_walk;
+  return push_scene(ctx);
 }
 
 int vpt_gpu_profile(vpt_gpu_ctx* ctx, uint64_t* out, int n, int reset) {

@@ -284,6 +284,7 @@ struct DevScene {
   // is hash(seed, jid * tile_area + pixel).  0 = the reference's per-job stream.
   int32_t pixel_mode;
   uint32_t tile_area;
+  int32_t wave_lanes;   // lanes of each wavefront that take jobs (64; latency-bound launches: 0 = auto)
   const float* bb;      // blackbody table [501][3] (row 500 = 0)
   const float* cie;     // [471][3] for T >= 49900 K
   float y_integral;
@@ -951,7 +952,7 @@ __host__ __device__ __forceinline__ uint64_t ordered_job(uint32_t k, uint32_t T,
 }
 
 // ------------------------------------------------------------------------------------------------
-// One iteration of the lane loop.  Env supplies fetch_job(uint64_t& item) -> bool, jid_begin, the
+// One iteration of the lane loop.  Env supplies fetch_job(uint64_t& item, wave_lanes) -> bool, jid_begin, the
 // job order (order == nullptr: item k is job jid_begin + k; else ordered_job()),
 // film_add(S, lane, px, py, rw).  HasTemp: the scene has a temperature grid (fire).
 // Debug: keep every counter and the job index (per-sample records).
@@ -1061,7 +1062,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
     if (go(ST_FETCH)) {
       env.prof(PB_FETCH);
       uint64_t j;
-      if (!env.fetch_job(j)) {
+      if (!env.fetch_job(j, S.wave_lanes)) {
         ln.state = ST_DONE;
         return;
       }

@@ -235,6 +235,13 @@ class Integrator:
         capi.check(capi.lib().vpt_gpu_set_tuning(self.h, gate_min, gate_idle, grid_blocks, gate_eval, gate_walk),
                    "vpt_gpu_set_tuning")
 
+    def set_latency_tuning(self, wave_lanes: int = -1, gate_min: int = 0, gate_idle: int = -1, gate_eval: int = 0,
+                           gate_walk: int = -1):
+        """Knobs of latency-bound launches (fewer items than grid lanes): lanes per wavefront that take
+        jobs (0 = auto) and their gates; see include/vpt_gpu.h."""
+        capi.check(capi.lib().vpt_gpu_set_latency_tuning(self.h, wave_lanes, gate_min, gate_idle, gate_eval, gate_walk),
+                   "vpt_gpu_set_latency_tuning")
+
     PROFILE_BLOCKS = ["iter", "fetch", "pixel", "ray", "sample", "need_seg", "step", "draw", "trilinear",
                       "event", "shadow_hit", "none", "nee_done", "finish",
                       "w_walk", "w_eval", "w_nee", "w_finish", "w_ray", "w_pixel", "w_done"]
