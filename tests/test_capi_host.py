@@ -125,3 +125,13 @@ def test_tile_provider_semantics():
     b, n = tp.next_batch(100)
     assert (b, n) == (8, 4)  # finishes wave 2, never starts wave 3
     assert tp.next_batch(100)[1] == 0
+
+
+def test_tuning_calls_reject_bad_arguments_without_a_device():
+    """The scheduling knobs reject a null context before touching a device (their gate_idle 0 check is
+    a GPU test: tests/test_gpu_production.py::test_latency_launch_knobs_keep_films_bit_exact)."""
+    L = capi.lib()
+    assert L.vpt_gpu_set_tuning(None, 6, 8, 0, 36, 4) != capi.VPT_OK
+    assert b"null context" in L.vpt_last_error()
+    assert L.vpt_gpu_set_latency_tuning(None, 0, 1, 65, 1, 1) != capi.VPT_OK
+    assert b"null context" in L.vpt_last_error()
