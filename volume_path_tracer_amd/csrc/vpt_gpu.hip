@@ -548,9 +548,11 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.order_tail_k0 = 0;
   env.order_tail_n = 0;
   // Fewer work items than resident lanes (small frames, few waves): a launch lasts as long as its
-  // slowest job, and a job's lane runs faster with fewer waves per SIMD, so size the grid to ~4/3
-  // items per lane (at least one block per CU).  C2: 1792 -> 768 blocks, 133 -> 143 Msps; C1: 256
-  // blocks, 4.55 -> 4.84.  Same jobs, same samples.
+  // slowest job, and a job's lane runs faster with fewer waves per SIMD, so the grid is sized to ~2
+  // items per lane in whole blocks per CU (at least one).  C2 (262 144 jobs, r02g sweep,
+  // profiles/r02g_c2_grid_sweep.txt): 1 / 1.5 / 1.75 / 2 / 2.5 / 3 / 4 / 5 blocks per CU 167.7 /
+  // 124.4 / 112.9 / 98.7-99.3 / 104.4 / 104.5-105.3 / 106.7 / 109.9 ms (the r01 rule, ~4/3 items per
+  // lane, gave 3).  Same jobs, same samples.
   uint32_t blocks = (uint32_t)ctx->grid_blocks;
   // Latency-bound launch (at most kSpreadLanes items per wavefront of the grid, e.g. C1's 4 096 jobs):
   // the launch lasts as long as its slowest job, and a job runs fastest on a wavefront with few other
@@ -560,8 +562,8 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   // lanes) -> 20.5 ms (1 792 blocks, one lane per wavefront, gates 1:65:1:1).  Same jobs, same samples.
   const bool latency = env.jid_count <= kSpreadLanes * ((uint64_t)blocks * (vpt::kBlockThreads / 64));
   if (!ctx->grid_user && !latency) {
-    const uint64_t want = (env.jid_count * 3 / 4 + vpt::kBlockThreads - 1) / vpt::kBlockThreads;
-    blocks = (uint32_t)std::min<uint64_t>(blocks, std::max<uint64_t>(want, (uint64_t)ctx->cus));
+    const uint64_t cus = (uint64_t)ctx->cus, per_cu = (env.jid_count + cus * vpt::kBlockThreads) / (2 * cus * vpt::kBlockThreads);
+    blocks = (uint32_t)std::min<uint64_t>(blocks, cus * std::max<uint64_t>(per_cu, 1));
   }
   const uint64_t T = ctx->scene.T;
   if (ctx->order_mode != VPT_ORDER_JID && jid_begin % T == 0 && jid_count % T == 0 && jid_count < (1ULL << 32)) {
