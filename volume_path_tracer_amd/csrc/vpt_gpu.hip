@@ -158,11 +158,17 @@ struct KernelEnv {
   // (ballot_w64 on the bool itself: the compare folds into the mask, no materialised 0/1 VGPR)
   __device__ __forceinline__ int32_t count(bool pred) { return (int32_t)__popcll(__builtin_amdgcn_ballot_w64(pred)); }
   // wave_lanes: the lanes of each wavefront that take jobs (64: all; fewer in latency-bound launches,
-  // see render(); 0 = about items / wavefronts); the others end at their first fetch.  Any value >= 1
-  // renders every job: a lane takes jobs until none is left.
+  // see render()); the others end at their first fetch.  Any value >= 1 renders every job: a lane
+  // takes jobs until none is left.  0 = auto from x = items / wavefronts: one lane (its jobs in
+  // sequence) while x < 3, else 1 + floor(x).  A second path in a wavefront slows the first ~1.6x, so
+  // one lane with a few jobs in a row wins: C1 frames on the full grid (r02g,
+  // profiles/r02g_c1_lanes_sweep.txt), 1 / 2 / 3 lanes: 8 spp (x = 1.1) 23.3 / 29.3 / - ms, 16 spp
+  // (x = 2.3) 31.7 / 32.5 / 35.6, 32 spp (x = 4.6) 51.9 / 43.1 / 42.1 (5 lanes: 41.5).
   __device__ __forceinline__ bool fetch_job(uint64_t& j, int32_t wave_lanes) {
-    if (wave_lanes == 0)
-      wave_lanes = 1 + (int32_t)((float)jid_count * __builtin_amdgcn_rcpf((float)(gridDim.x * (kBlockThreads / 64))));
+    if (wave_lanes == 0) {
+      const float x = (float)jid_count * __builtin_amdgcn_rcpf((float)(gridDim.x * (kBlockThreads / 64)));
+      wave_lanes = x < 3.0f ? 1 : 1 + (int32_t)x;
+    }
     if ((int32_t)__lane_id() >= wave_lanes) return false;
     unsigned long long v = atomicAdd(job_counter, 1ULL);
     if (v >= jid_count) return false;
