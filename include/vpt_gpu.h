@@ -309,8 +309,8 @@ int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_b
                        int gate_walk);
 /* Latency-bound launches: a launch with fewer work items than its grid has lanes (e.g. C1, 4 096
  * jobs) lasts as long as its slowest job.  Such launches spread their items over the grid's
- * wavefronts -- the first wave_lanes lanes of each wavefront take jobs (0 = auto: ceil(items /
- * wavefronts)) -- and run with their own gates (meaning as in vpt_gpu_set_tuning; defaults 1, 65, 1, 1:
+ * wavefronts -- the first wave_lanes lanes of each wavefront take jobs (0 = auto: 1 while items /
+ * wavefronts < 3, each lane taking its jobs in sequence, else 1 + floor(items / wavefronts)) -- and run with their own gates (meaning as in vpt_gpu_set_tuning; defaults 1, 65, 1, 1:
  * every block runs as soon as one lane needs it).  Results never depend on them.  Pass < 0 (gate_min,
  * gate_eval: <= 0) to keep a value; gate_idle 0 is rejected. */
 int vpt_gpu_set_latency_tuning(vpt_gpu_ctx* ctx, int wave_lanes, int gate_min, int gate_idle, int gate_eval,
