@@ -64,3 +64,38 @@ def signed_grid() -> capi.Grid:
                      map_vec=list(base.desc.map_vec), background=0.0, bbox_min=lo.tolist(), bbox_max=hi.tolist(),
                      leaf_origin=origin, leaf_values=values, leaf_max=vmax, leaf_value_mask=base.leaf_value_mask,
                      **tiles)
+
+
+def mapped_grid(scale, angles_deg=(0.0, 0.0, 0.0), n=64, kind=1) -> capi.Grid:
+    """The n^3 cloud (kind 1) or cube (kind 0) under a non-identity nanovdb::Map: index -> world =
+    R(angles) @ diag(scale) @ ijk + vec, with vec putting the grid's centre at the world origin.  Both
+    matrices are float32 roundings of the float64 ones, as NanoVDB stores mMatF / mInvMatF.  Voxel
+    sizes far from 1 exercise the index-space lookahead and the walk-table padding argument
+    (vpt_integrator.h walk_index)."""
+    base = SynthGrid(kind, n).grid(copy=True)
+    ax, ay, az = np.radians(angles_deg)
+    rx = np.array([[1, 0, 0], [0, np.cos(ax), -np.sin(ax)], [0, np.sin(ax), np.cos(ax)]])
+    ry = np.array([[np.cos(ay), 0, np.sin(ay)], [0, 1, 0], [-np.sin(ay), 0, np.cos(ay)]])
+    rz = np.array([[np.cos(az), -np.sin(az), 0], [np.sin(az), np.cos(az), 0], [0, 0, 1]])
+    m = rz @ ry @ rx @ np.diag(np.asarray(scale, np.float64))
+    vec = -m @ np.full(3, n / 2.0)
+    return capi.Grid(map_mat=m.astype(np.float32), map_inv_mat=np.linalg.inv(m).astype(np.float32),
+                     map_vec=vec.astype(np.float32), background=0.0, bbox_min=list(base.desc.index_bbox_min),
+                     bbox_max=list(base.desc.index_bbox_max), leaf_origin=base.leaf_origin, leaf_values=base.leaf_values,
+                     leaf_max=base.leaf_max, leaf_value_mask=base.leaf_value_mask)
+
+
+def mapped_scene(cfg, world_extent, sigma_scale):
+    """Camera 2.6 world extents from the grid's centre (off axis), and sigma_a / sigma_s scaled so the
+    optical depths match the unit-voxel scene (sigma is per world unit, volume.cpp:90-98 m_scale)."""
+    look_at(cfg, (0.11 * world_extent, -0.07 * world_extent, -2.6 * world_extent), (0.0, 0.0, 0.0))
+    v = cfg.volume_parameters
+    v.sigma_a *= sigma_scale
+    v.sigma_s *= sigma_scale
+
+
+MAPPED_CASES = [  # (id, per-axis voxel size, rotation in degrees)
+    ("small_voxels", (0.05, 0.04, 0.07), (20.0, -35.0, 10.0)),
+    ("large_voxels", (20.0, 25.0, 18.0), (-15.0, 40.0, 5.0)),
+    ("unit_rotated", (1.0, 1.0, 1.0), (30.0, 45.0, 60.0)),
+]

@@ -34,6 +34,8 @@ def lib():
         L.vpths_math_mismatches.argtypes = [C.c_int]
         L.vpths_math_mismatches.restype = C.c_int64
         L.vpths_pow2_mismatches.restype = C.c_int64
+        L.vpths_walk_outside.argtypes = [C.c_int]
+        L.vpths_walk_outside.restype = C.c_uint64
         _L = L
     return _L
 
@@ -60,6 +62,11 @@ def render_jobs(cfg, density, temperature, jid_begin, jid_count, records=False, 
                                        op, int(tail_waves))
     assert rc == 0
     return film, rec, cnt.as_dict()
+
+
+def walk_outside(reset=True):
+    """Walk-table lookups outside the padded table since the last reset (must stay 0)."""
+    return int(lib().vpths_walk_outside(1 if reset else 0))
 
 
 def fixed_leaf_max(grid):

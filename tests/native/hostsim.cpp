@@ -286,3 +286,11 @@ extern "C" int64_t vpths_pow2_mismatches(void) {
   }
   return bad;
 }
+
+// Walk-table lookups outside the padded table since the last reset (vpt_integrator.h walk_index):
+// the padding argument of hdda_pre_advance says there are none.
+extern "C" uint64_t vpths_walk_outside(int reset) {
+  const uint64_t n = vpt::g_walk_outside;
+  if (reset) vpt::g_walk_outside = 0;
+  return n;
+}

@@ -135,3 +135,18 @@ def test_tuning_calls_reject_bad_arguments_without_a_device():
     assert b"null context" in L.vpt_last_error()
     assert L.vpt_gpu_set_latency_tuning(None, 0, 1, 65, 1, 1) != capi.VPT_OK
     assert b"null context" in L.vpt_last_error()
+
+
+def test_grid_build_rejects_extents_beyond_the_24_bit_walk_index():
+    """The device indexes the walk table with 24-bit multiplies: a lower-node extent whose x-y face
+    reaches 2^24 cells is rejected at build time (VPT_E_INVALID) instead of diverging silently
+    (ADVICE r02).  Two leaves 255 lower nodes apart in x and y: a 4100 x 4100-cell padded face."""
+    vals = np.zeros((2, 512), np.float32)
+    far = 255 * 128
+    g = capi.Grid(map_mat=np.eye(3), map_inv_mat=np.eye(3), map_vec=[0, 0, 0], background=0.0,
+                  bbox_min=[0, 0, 0], bbox_max=[far + 7, far + 7, 7],
+                  leaf_origin=[[0, 0, 0], [far, far, 0]], leaf_values=vals, leaf_max=np.zeros(2, np.float32))
+    out = np.zeros(2, np.float32)
+    rc = capi.lib().vpt_fix_majorants(C.byref(g.desc), out.ctypes.data_as(C.POINTER(C.c_float)), 2)
+    assert rc == 1, rc  # VPT_E_INVALID, before any table is allocated
+    assert b"24-bit" in capi.lib().vpt_last_error()

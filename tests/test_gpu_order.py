@@ -67,6 +67,18 @@ def test_job_permutation_rejects_non_permutations(setup):
         it.set_job_permutation(np.array([0, 3, 1], np.uint32))
 
 
+def test_tile_costs_reject_non_finite(setup):
+    """NaN / inf costs would make the ranking's comparator no strict weak ordering."""
+    _, it, _ = setup
+    est, rank = it.tile_costs()
+    for bad in (np.nan, np.inf):
+        c = est.copy()
+        c[len(c) // 2] = bad
+        with pytest.raises(RuntimeError):
+            it.set_tile_costs(c)
+    np.testing.assert_array_equal(it.tile_costs()[1], rank)  # the ranking is unchanged
+
+
 def test_sample_counts_for_partial_job_ranges(setup):
     """The count kernel's per-pixel job count for ranges that start and end inside waves."""
     wl, it, _ = setup

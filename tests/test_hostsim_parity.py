@@ -122,3 +122,27 @@ def test_job_order_permutation_keeps_samples(tail_waves, size):
     np.testing.assert_array_equal(f_a[..., 3], f_b[..., 3])
     np.testing.assert_allclose(f_a[..., :3], f_b[..., :3], rtol=1e-5, atol=1e-6)
     assert c_a == c_b
+
+
+@pytest.mark.parametrize("case", [c[0] for c in __import__("grids").MAPPED_CASES])
+def test_mapped_grids_and_walk_padding(case):
+    """Non-identity maps (voxel sizes 0.05 and 20, anisotropic, rotated): the device state machine
+    equals the oracle bit for bit, and no walk-table lookup falls outside the padded table -- the
+    lookahead of RayMajorantIterator::next (volume.cpp:63) is 1.0001 along the index-space ray, so the
+    padding argument does not depend on the voxel size."""
+    from grids import MAPPED_CASES, mapped_grid, mapped_scene
+
+    _, scale, ang = next(c for c in MAPPED_CASES if c[0] == case)
+    dens = mapped_grid(scale, ang)
+    wl = workload("c3", width=40, height=32, spp=2, grid_n=64)
+    mapped_scene(wl.cfg, 64 * max(scale), 1.0 / min(scale))
+    od = O.OracleGrid(dens, fix_majorants=True)
+    jobs = wl.cfg.jobs_per_wave() * 2
+    HS.walk_outside(reset=True)
+    f_o, r_o, c_o = O.render_jobs(wl.cfg, od, None, 0, jobs, records=True)
+    f_h, r_h, c_h = HS.render_jobs(wl.cfg, dens, None, 0, jobs, records=True)
+    assert r_o.tobytes() == r_h.tobytes()
+    for k in ("dda_steps", "segments", "draws", "density_evals", "rng_draws"):
+        assert c_o[k] == c_h[k], k
+    assert c_o["density_evals"] > 500 and c_o["scatters"] > 50, c_o
+    assert HS.walk_outside() == 0

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -356,6 +357,17 @@ static int upload(const void* src, size_t n, void** dst, size_t& bytes) {
 static int upload_grid(const HostGrid& h, DeviceGrid& d) {
   d.dev = h.dev;
   int rc;
+  // The stencil-major pool is 16 KiB per leaf (8x the voxels): a large sparse volume can exceed the
+  // device's memory.  Say so before the first allocation instead of failing inside hipMalloc.
+  const size_t need = h.cells8.size() * sizeof(int2) + h.runs8.size() + h.walk8.size() * sizeof(uint32_t) +
+                      h.cells128.size() * sizeof(int2) + h.root.size() * sizeof(RootTileDev) +
+                      h.bricks.size() * sizeof(float);
+  size_t free_b = 0, total_b = 0;
+  VPT_HIP(hipMemGetInfo(&free_b, &total_b));
+  if (need > free_b)
+    return set_error(VPT_E_NOMEM, "grid upload: needs " + std::to_string(need >> 20) + " MiB (" +
+                                      std::to_string(h.dev.leaf_count) + " leaves x 16 KiB stencil pool + tables), " +
+                                      std::to_string(free_b >> 20) + " MiB free on the device");
   if ((rc = upload(h.cells8.data(), h.cells8.size() * sizeof(int2), &d.cells8, d.bytes))) return rc;
   if ((rc = upload(h.runs8.data(), h.runs8.size(), &d.runs8, d.bytes))) return rc;
   if ((rc = upload(h.walk8.data(), h.walk8.size() * sizeof(uint32_t), &d.walk8, d.bytes))) return rc;
@@ -431,21 +443,23 @@ constexpr uint32_t kLaunchSlots = 64;
 constexpr uint64_t kSpreadLanes = 6;
 
 int ctx_device(vpt_gpu_ctx* ctx);
+int wait_ctx(vpt_gpu_ctx* ctx);
 
-// Device copy of the scene constants, which every in-flight launch reads: wait for all work on the
-// device (launches may sit on any stream, including non-blocking ones), copy, and wait again (a
-// pageable hipMemcpy may return before its DMA lands, and the next render may use another stream).
+// Device copy of the scene constants, which every in-flight launch of this context reads: wait for
+// the context's launches (wait_ctx), copy on the context's stream and wait for the copy (the next
+// render may use another stream).
 int push_scene(vpt_gpu_ctx* ctx) {
-  VPT_HIP(hipDeviceSynchronize());
-  VPT_HIP(hipMemcpy(ctx->scene_dev, &ctx->scene, sizeof(vpt::DevScene), hipMemcpyHostToDevice));
+  int rc = wait_ctx(ctx);
+  if (rc) return rc;
   vpt::DevScene lat = ctx->scene;
   lat.gate_min = ctx->lat_gate[0];
   lat.gate_idle = ctx->lat_gate[1];
   lat.gate_eval = ctx->lat_gate[2];
   lat.gate_walk = ctx->lat_gate[3];
   lat.wave_lanes = ctx->lat_wave_lanes;
-  VPT_HIP(hipMemcpy(ctx->scene_lat_dev, &lat, sizeof(vpt::DevScene), hipMemcpyHostToDevice));
-  VPT_HIP(hipDeviceSynchronize());
+  VPT_HIP(hipMemcpyAsync(ctx->scene_dev, &ctx->scene, sizeof(vpt::DevScene), hipMemcpyHostToDevice, ctx->stream));
+  VPT_HIP(hipMemcpyAsync(ctx->scene_lat_dev, &lat, sizeof(vpt::DevScene), hipMemcpyHostToDevice, ctx->stream));
+  VPT_HIP(hipStreamSynchronize(ctx->stream));
   return VPT_OK;
 }
 
@@ -464,6 +478,21 @@ int release_slot(vpt_gpu_ctx* ctx, hipStream_t s, uint32_t slot) {
   std::lock_guard<std::mutex> lock(ctx->slot_mu);
   VPT_HIP(hipEventRecord(ctx->slot_done[slot], s));
   ctx->slot_used[slot] = true;
+  return VPT_OK;
+}
+
+// Waits for every launch of this context, whatever stream it was enqueued on, and for the context's
+// own stream -- not for other contexts' work on the device (a context per thread never stalls
+// behind another's frames).  Each launch records its ring slot's event after its kernels
+// (release_slot), and a launch that reuses a slot is ordered after the slot's previous launch
+// (take_slot), so the latest event of every used slot covers all of them.
+int wait_ctx(vpt_gpu_ctx* ctx) {
+  {
+    std::lock_guard<std::mutex> lock(ctx->slot_mu);
+    for (uint32_t i = 0; i < kLaunchSlots; ++i)
+      if (ctx->slot_used[i]) VPT_HIP(hipEventSynchronize(ctx->slot_done[i]));
+  }
+  if (ctx->stream) VPT_HIP(hipStreamSynchronize(ctx->stream));
   return VPT_OK;
 }
 
@@ -829,7 +858,9 @@ int vpt_gpu_set_tile_costs(vpt_gpu_ctx* ctx, const float* cost) {
   if (!ctx || !cost) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_tile_costs: null argument");
   int rc = ctx_device(ctx);
   if (rc) return rc;
-  VPT_HIP(hipDeviceSynchronize());  // in-flight launches read the current order
+  for (uint64_t i = 0; i < ctx->scene.T; ++i)  // NaN would break the sort's strict weak ordering
+    if (!std::isfinite(cost[i])) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_tile_costs: non-finite cost");
+  if ((rc = wait_ctx(ctx))) return rc;  // in-flight launches read the current order
   ctx->tile_cost.assign(cost, cost + ctx->scene.T);
   return rank_tiles(ctx);
 }
@@ -844,7 +875,7 @@ int vpt_gpu_set_job_permutation(vpt_gpu_ctx* ctx, const uint32_t* perm, uint64_t
     if (perm[i] >= n || seen[perm[i]]) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_job_permutation: not a permutation");
     seen[perm[i]] = 1;
   }
-  VPT_HIP(hipDeviceSynchronize());  // in-flight launches may read the current one
+  if ((rc = wait_ctx(ctx))) return rc;  // in-flight launches may read the current one
   (void)hipFree(ctx->perm);
   ctx->perm = nullptr;
   ctx->perm_n = 0;
@@ -859,15 +890,14 @@ int vpt_gpu_sync(vpt_gpu_ctx* ctx) {
   if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
   int rc = ctx_device(ctx);
   if (rc) return rc;
-  VPT_HIP(hipDeviceSynchronize());
-  return VPT_OK;
+  return wait_ctx(ctx);
 }
 
 int vpt_gpu_film_clear(vpt_gpu_ctx* ctx) {
   if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
   int rc = ctx_device(ctx);
   if (rc) return rc;
-  VPT_HIP(hipDeviceSynchronize());  // renders into the film may be in flight on any stream
+  if ((rc = wait_ctx(ctx))) return rc;  // renders into the film may be in flight on any stream
   VPT_HIP(hipMemsetAsync(ctx->film, 0, ctx->film_count * sizeof(float), ctx->stream));
   VPT_HIP(hipStreamSynchronize(ctx->stream));
   return VPT_OK;
@@ -884,7 +914,7 @@ int vpt_gpu_film_add_to_host(vpt_gpu_ctx* ctx, float* film_host) {
   if (!ctx || !film_host) return vpt::set_error(VPT_E_INVALID, "null argument");
   int rc = ctx_device(ctx);
   if (rc) return rc;
-  VPT_HIP(hipDeviceSynchronize());
+  if ((rc = wait_ctx(ctx))) return rc;
   std::vector<float> tmp(ctx->film_count);
   VPT_HIP(hipMemcpy(tmp.data(), ctx->film, ctx->film_count * sizeof(float), hipMemcpyDeviceToHost));
   for (uint64_t i = 0; i < ctx->film_count; ++i) film_host[i] += tmp[i];
@@ -895,7 +925,7 @@ int vpt_gpu_counters(vpt_gpu_ctx* ctx, vpt_counters* out, int reset) {
   if (!ctx || !out) return vpt::set_error(VPT_E_INVALID, "null argument");
   int rc = ctx_device(ctx);
   if (rc) return rc;
-  VPT_HIP(hipDeviceSynchronize());
+  if ((rc = wait_ctx(ctx))) return rc;
   unsigned long long c[vpt::kCounterCount];
   VPT_HIP(hipMemcpy(c, ctx->counters, sizeof c, hipMemcpyDeviceToHost));
   uint64_t* o = reinterpret_cast<uint64_t*>(out);
@@ -941,7 +971,7 @@ int vpt_gpu_profile(vpt_gpu_ctx* ctx, uint64_t* out, int n, int reset) {
   if (!ctx || !out) return vpt::set_error(VPT_E_INVALID, "null argument");
   int rc = ctx_device(ctx);
   if (rc) return rc;
-  VPT_HIP(hipDeviceSynchronize());
+  if ((rc = wait_ctx(ctx))) return rc;
   std::vector<unsigned long long> v(kProfWords);
   VPT_HIP(hipMemcpy(v.data(), ctx->prof, v.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   if (n < (int)v.size()) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_profile: output too small");

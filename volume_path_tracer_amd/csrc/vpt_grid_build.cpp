@@ -321,6 +321,12 @@ int build_host_grid(const vpt_grid_desc& d, bool fix, int threads, HostGrid& out
       cnt *= G.r8_n[a];
     }
     if (cnt > (int64_t)1 << 32) return set_error(VPT_E_NOMEM, "grid: leaf-slot table too large");
+    // The device indexes the padded walk table and the run radii with 24-bit multiplies
+    // ((a * ny + b) * nz + c, math::mul24): the x-y face must stay below 2^24 cells and the table
+    // below 2^32 entries, or the device index would silently diverge from the host's.
+    const int64_t wx = G.r8_n[0] + 2 * kWalkPad, wy = G.r8_n[1] + 2 * kWalkPad, wz = G.r8_n[2] + 2 * kWalkPad;
+    if (wx * wy >= ((int64_t)1 << 24) || wx * wy * wz > ((int64_t)1 << 32))
+      return set_error(VPT_E_INVALID, "grid: lower-node extent too large for the 24-bit walk-table index (x*y face >= 2^24 cells)");
     out.cells8.resize((size_t)cnt);
     std::vector<uint8_t> lower_present((size_t)nl[0] * nl[1] * nl[2], 0);
     for (const Key3& l : lowers)

@@ -513,11 +513,22 @@ __host__ __device__ __forceinline__ float hdda_advance(Lane& ln) {
   return tn;
 }
 
+#if !defined(__HIP_DEVICE_COMPILE__)
+// Host builds only (the CPU simulator, tests/native/hostsim.cpp): walk-table lookups of a cell outside
+// the padded table, which the padding argument of hdda_pre_advance rules out.  Tests read it as 0.
+inline uint64_t g_walk_outside = 0;
+#endif
+
 // Walk-table index of the 8^3 cell holding voxel v (padded table).  The min() only guarantees a
-// memory-safe address; hdda_pre_advance never asks for a cell beyond the padding.
+// memory-safe address; hdda_pre_advance never asks for a cell beyond the padding.  The padding is in
+// index space, and so is the HDDA's lookahead (1.0001 along the index-space ray, whose direction
+// Ray::worldToIndexF normalises): the argument holds for every voxel size and any affine map.
 __host__ __device__ __forceinline__ uint32_t walk_index(const DevGrid& g, const int32_t v[3]) {
   const uint32_t a = (uint32_t)((v[0] - g.w8_org[0]) >> 3), b = (uint32_t)((v[1] - g.w8_org[1]) >> 3),
                  c = (uint32_t)((v[2] - g.w8_org[2]) >> 3);
+#if !defined(__HIP_DEVICE_COMPILE__)
+  if (a >= (uint32_t)g.w8_n[0] || b >= (uint32_t)g.w8_n[1] || c >= (uint32_t)g.w8_n[2]) ++g_walk_outside;
+#endif
   const uint32_t idx = math::mul24(math::mul24(a, (uint32_t)g.w8_n[1]) + b, (uint32_t)g.w8_n[2]) + c;
   return idx < g.w8_max ? idx : g.w8_max;
 }
