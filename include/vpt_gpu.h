@@ -127,6 +127,22 @@ typedef struct vpt_grid_desc {
   const int32_t* upper_origin;
 } vpt_grid_desc;
 
+/* A nanovdb::NanoGrid<float> in memory -> vpt_grid_desc.  grid_buffer = the grid's own bytes, as the
+ * reference holds them (&vol.grids().density(), grid.gridSize() bytes = GridHandle::data(); NanoVDB
+ * 32.x layout restated, include/vpt/volume_grids.hpp:12-33): leaves with their values, value masks and
+ * stored maxima, lower / upper node tiles (non-child slots that are active or differ from the
+ * background), root tiles, and every internal node's origin.  Every offset in the buffer is
+ * bounds-checked (VPT_E_INVALID on a malformed buffer).  *out owns its arrays: release it with
+ * vpt_grid_free.  Replaces the NanoVDB tree walk a caller of vpt_gpu_create would otherwise write. */
+int vpt_grid_from_nanovdb(const void* grid_buffer, size_t bytes, vpt_grid_desc** out);
+/* nanovdb::io::readGrid(path, grid_name) for a float grid (src/volume_grids.cpp:38-67): .nvdb files
+ * of NanoVDB 32.x, codec NONE or ZIP.  A file without a grid of that name returns VPT_OK with
+ * *out = NULL (the reference's nanovdb_try_read_grid, volume_grids.cpp:38-46); an unreadable file is
+ * VPT_E_IO, a malformed one VPT_E_INVALID.  Release *out with vpt_grid_free. */
+int vpt_grid_read_nvdb(const char* path, const char* grid_name, vpt_grid_desc** out);
+/* Releases a desc from vpt_grid_from_nanovdb / vpt_grid_read_nvdb / vpt_synth_grid. */
+void vpt_grid_free(vpt_grid_desc* desc);
+
 /* fix_majorants_for_interpolation(grid, order=1) (src/volume.cpp:104-160), host side:
  * out_leaf_max[i] = max(desc.leaf_max[i], getValue(c) for c in the 26 neighbour leaf boxes
  * intersected with leaf i's bbox expanded by 1).  Idempotent.  Uses up to num_threads threads. */

@@ -230,6 +230,9 @@ def lib() -> C.CDLL:
     L.vpt_synth_grid.argtypes = [C.c_int, C.c_int]
     L.vpt_synth_grid.restype = gridp
     L.vpt_synth_free.argtypes = [gridp]
+    L.vpt_grid_from_nanovdb.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(gridp)]
+    L.vpt_grid_read_nvdb.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(gridp)]
+    L.vpt_grid_free.argtypes = [gridp]
     L.vpt_film_to_srgb8.argtypes = [fp, C.c_int64, C.c_int64, C.POINTER(C.c_uint8)]
     L.vpt_gpu_trace_jobs.argtypes = [vp, C.c_uint64, C.c_uint64, vp, vp, C.c_uint64, C.POINTER(C.c_uint64), vp]
     L.vpt_gpu_majorant_trace.argtypes = [vp, fp, fp, fp, C.c_int, C.POINTER(C.c_int)]
@@ -244,6 +247,29 @@ def lib() -> C.CDLL:
     L.vpt_gpu_set_job_permutation.argtypes = [vp, C.POINTER(C.c_uint32), C.c_uint64]
     _lib = L
     return L
+
+
+def grid_from_nanovdb(buffer: bytes) -> "Grid":
+    """vpt_grid_from_nanovdb: a NanoGrid<float> buffer flattened by the C++ reader (copied out)."""
+    p = C.POINTER(GridDesc)()
+    raw = C.create_string_buffer(bytes(buffer), len(buffer))
+    check(lib().vpt_grid_from_nanovdb(raw, len(buffer), C.byref(p)), "vpt_grid_from_nanovdb")
+    try:
+        return Grid.from_desc(p.contents, copy=True)
+    finally:
+        lib().vpt_grid_free(p)
+
+
+def read_nvdb_grid(path, name: str) -> "Grid | None":
+    """vpt_grid_read_nvdb: the named float grid of a .nvdb file (C++ reader), or None if absent."""
+    p = C.POINTER(GridDesc)()
+    check(lib().vpt_grid_read_nvdb(str(path).encode(), name.encode(), C.byref(p)), "vpt_grid_read_nvdb")
+    if not p:
+        return None
+    try:
+        return Grid.from_desc(p.contents, copy=True)
+    finally:
+        lib().vpt_grid_free(p)
 
 
 def check(rc: int, what: str = "") -> None:

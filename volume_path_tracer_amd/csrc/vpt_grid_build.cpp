@@ -453,12 +453,6 @@ int build_host_grid(const vpt_grid_desc& d, bool fix, int threads, HostGrid& out
 // Synthetic stand-in volumes: the real wdas_cloud.nvdb / fire.nvdb are not available.
 // ------------------------------------------------------------------------------------------------
 namespace {
-struct SynthDesc {
-  vpt_grid_desc d;  // must stay first
-  std::vector<int32_t> origin;
-  std::vector<float> values, maxv;
-  std::vector<uint64_t> mask;
-};
 
 double synth_voxel(int kind, int n, int i, int j, int k) {
   if (kind == 0) return 1.0;
@@ -491,7 +485,7 @@ extern "C" vpt_grid_desc* vpt_synth_grid(int kind, int n) {
     vpt::set_error(VPT_E_INVALID, "vpt_synth_grid: kind in {0,1,2}, n a positive multiple of 8");
     return nullptr;
   }
-  auto* s = new vpt::SynthDesc();
+  auto* s = vpt::owned_grid_new();
   const int nl = n / 8;
   const int T = vpt::default_threads();
   struct Part {
@@ -538,17 +532,16 @@ extern "C" vpt_grid_desc* vpt_synth_grid(int kind, int n) {
   });
   int32_t lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
   for (auto& P : parts) {
-    s->origin.insert(s->origin.end(), P.origin.begin(), P.origin.end());
-    s->values.insert(s->values.end(), P.values.begin(), P.values.end());
-    s->mask.insert(s->mask.end(), P.mask.begin(), P.mask.end());
-    s->maxv.insert(s->maxv.end(), P.maxv.begin(), P.maxv.end());
+    s->leaf_origin.insert(s->leaf_origin.end(), P.origin.begin(), P.origin.end());
+    s->leaf_values.insert(s->leaf_values.end(), P.values.begin(), P.values.end());
+    s->leaf_mask.insert(s->leaf_mask.end(), P.mask.begin(), P.mask.end());
+    s->leaf_max.insert(s->leaf_max.end(), P.maxv.begin(), P.maxv.end());
     for (int q = 0; q < 3; ++q) {
       lo[q] = std::min(lo[q], P.lo[q]);
       hi[q] = std::max(hi[q], P.hi[q]);
     }
   }
   vpt_grid_desc& d = s->d;
-  std::memset(&d, 0, sizeof d);
   const float half = (float)(n / 2);
   for (int a = 0; a < 9; ++a) d.map_mat[a] = d.map_inv_mat[a] = (a % 4 == 0) ? 1.0f : 0.0f;
   for (int q = 0; q < 3; ++q) {
@@ -557,12 +550,8 @@ extern "C" vpt_grid_desc* vpt_synth_grid(int kind, int n) {
     d.index_bbox_max[q] = hi[q];
   }
   d.background = 0.0f;
-  d.leaf_count = s->maxv.size();
-  d.leaf_origin = s->origin.data();
-  d.leaf_values = s->values.data();
-  d.leaf_value_mask = s->mask.data();
-  d.leaf_max = s->maxv.data();
+  s->finish();
   return &s->d;
 }
 
-extern "C" void vpt_synth_free(vpt_grid_desc* d) { delete reinterpret_cast<vpt::SynthDesc*>(d); }
+extern "C" void vpt_synth_free(vpt_grid_desc* d) { delete reinterpret_cast<vpt::OwnedGrid*>(d); }

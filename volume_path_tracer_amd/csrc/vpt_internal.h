@@ -51,4 +51,16 @@ float cie_y_integral();
 
 int default_threads();
 
+// A vpt_grid_desc that owns its arrays (vpt_synth_grid, vpt_grid_from_nanovdb, vpt_grid_read_nvdb;
+// released by vpt_synth_free / vpt_grid_free).  d must stay the first member.
+struct OwnedGrid {
+  vpt_grid_desc d{};
+  std::vector<int32_t> leaf_origin, tile_origin, tile_level, lower_origin, upper_origin;
+  std::vector<float> leaf_values, leaf_max, tile_value;
+  std::vector<uint64_t> leaf_mask;
+  std::vector<uint8_t> tile_active;
+  void finish();  // points d's arrays at the vectors
+};
+OwnedGrid* owned_grid_new();
+
 }  // namespace vpt
