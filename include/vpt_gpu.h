@@ -338,6 +338,8 @@ int vpt_gpu_set_latency_tuning(vpt_gpu_ctx* ctx, int wave_lanes, int gate_min, i
 int vpt_gpu_profile(vpt_gpu_ctx* ctx, uint64_t* out, int n, int reset);
 /* Launch geometry used by the integrator kernel (for reports). */
 int vpt_gpu_launch_info(const vpt_gpu_ctx* ctx, int* grid_blocks, int* block_threads);
+/* Number of HIP devices (0 without a GPU: VPT_OK, *count = 0). */
+int vpt_gpu_device_count(int* count);
 
 /* ---- synthetic stand-in volumes (the reference's .nvdb files are not available) ---------- */
 

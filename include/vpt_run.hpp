@@ -1,58 +1,3 @@
-# INTEGRATION — replacing `vpt::run` with the MI355X integrator
-
-The reference calls `vpt::run(params, vol, camera, provider, film, rng)` from `num_workers`
-threads (`src/main.cpp:63-68`). A maintainer replaces that one call with `vpt_gpu::run` (same
-arguments); underneath, one GPU context per device renders job-id batches through the C ABI.
-Nothing in the scene files, the camera/film types or the job ids changes.
-
-## 1. The drop-in: one changed line in `main.cpp`
-
-```cpp
-#include <vpt_run.hpp>                      // this repo's include/ (C++20, header-only over vpt_gpu.h)
-...
-      vpt::RandomNumberGenerator rng(cfg.seed);
-      vpt_gpu::run(cfg.worker_parameters, vol, camera, provider, film, rng);   // was vpt::run(...)
-```
-
-Link `volume_path_tracer_amd/lib/libvpt_amd.so` (built by `python -m volume_path_tracer_amd.build`).
-Nothing else in `main.cpp:26-146` changes: the scene JSON, `VolumeGrids::read_from_file`, `Volume`
-(with its majorant fix), `TileProvider`, `Camera`, the film, the worker threads and their timing, the
-window and `stop_at_next_wave()` all stay. `vpt_gpu::run` has `run`'s signature
-(`include/vpt/worker.hpp:11`) and reads the reference's objects through their public interfaces only:
-
-| Argument | What the drop-in takes from it |
-|---|---|
-| `WorkerParameters` | every field (`configuration.hpp:34-44`) |
-| `Volume` | `params()`, and `grids().density()` / `temperature()`: the `NanoGrid<float>` memory itself, flattened by `vpt_grid_from_nanovdb(&grid, grid.gridSize(), ...)` (§2) |
-| `Camera` | `params()`; the raster-to-world matrix is rebuilt as `Camera::Camera` builds it (`camera.cpp:45-57`) |
-| `TileProvider` | `next()` tokens (`jid()`, `compute_rect()`); the tile size, private to the provider, is the largest rect of the first batch, and every rect is checked against the jid mapping |
-| `Image<float,4>` | `size()`, `data().data()`: the XYZW film the GPU film is added into |
-| `RandomNumberGenerator` | the seed: `seed()` if the type has one; the reference keeps it private, so the drop-in finds the u32 seed whose job-0 stream starts with the same two outputs (2^32 candidates, 1-3 s on 8-16 threads, once per process) |
-
-Threads: `main.cpp` starts `num_workers` threads. Each GPU is claimed by one of them for the length of
-its `run()` call (one context per device); the other threads return at once and the device threads
-drain the provider. A thread builds its context only after its first batch of tokens, so a thread that
-finds the provider already drained returns without building one. Errors exit with status 1 like
-`vptFATAL`; `vpt_gpu::run_checked` returns the code instead.
-
-The code below is `include/vpt_run.hpp`, verbatim (a CPU test checks that this section still matches
-the file). `tests/native/run_gpu_harness.cpp` compiles it against headless restatements of the
-reference types (`tests/native/reference_types_headless.hpp`: the argument types with the accessors
-above, the RNG with its seed private; `tests/native/tile_provider_headless.hpp`: `TileProvider` with
-its wave gating and token destructor). `tests/test_gpu_integration.py` drives it on the GPU:
-- `mode=run`: `vpt_gpu::run` called from 3 worker threads exactly as `main.cpp:63-68` calls `vpt::run`,
-  the grids given as `NanoGrid<float>` bytes (density, and temperature for `fire.json`);
-- `mode=drain`: `vpt_gpu::drain` on 2-4 threads with one context each, batches smaller and larger
-  than a wave, `stop_at_next_wave()`, and a volume read from an `.nvdb` file (ZIP codec, tiles at every
-  tree level) through `vpt_grid_read_nvdb`.
-Every film must equal the oracle's, with exact sample counts.
-
-Holding a token while calling `next()` deadlocks. `next()` waits until the same tile's previous wave
-has been released. Once other threads have taken a wave's worth of jobs, the job counter can land on
-a token this thread holds. That can happen at any batch size. So the drop-in releases each token as
-soon as it has recorded the job id. It still renders every job it takes.
-
-```cpp
 // vpt_run.hpp — the reference-side drop-in for vpt::run (include/vpt/worker.hpp:11, src/worker.cpp:92-208)
 // on MI355X GPUs, written against the C ABI of vpt_gpu.h only (header-only C++20).
 //
@@ -378,113 +323,3 @@ void run(const WorkerParameters& params, const Volume& vol, const Camera& camera
 }
 
 }  // namespace vpt_gpu
-```
-
-Cost of the token interface. One `next()` hands out one 8x8 job. That is 64 samples, about 50 ns of
-GPU time at the C3 rate. A thread that takes tokens one at a time keeps up with one GPU, because the
-launches overlap the next round of taking. It cannot keep up with eight GPUs sharing one provider.
-For that case, partition the job space per GPU with `TileProvider`'s pure mapping
-(`distributed.rank_job_ranges`: contiguous wave blocks per rank). Then keep the provider only for
-progress, ETA and stop.
-
-## 2. Grids: `vpt_grid_from_nanovdb`, `vpt_grid_read_nvdb`
-
-The C ABI takes a flattened `vpt_grid_desc` (`include/vpt_gpu.h`). The reference never needs to
-write that flattening itself:
-- `vpt_grid_from_nanovdb(const void* grid, size_t bytes, vpt_grid_desc** out)` reads a
-  `NanoGrid<float>` from its own memory (`&grids.density()`, `grids.density().gridSize()` bytes, i.e.
-  `GridHandle::data()`): leaves (values, value masks, stored maxima), lower- and upper-node tiles
-  (non-child slots that are active or hold a non-background value), root tiles, and every internal
-  node. Every offset is bounds-checked; a malformed buffer is `VPT_E_INVALID`.
-- `vpt_grid_read_nvdb(path, name, &out)` is `nanovdb::io::readGrid(path, name)` for float grids
-  (codec NONE or ZIP): `out == NULL` when the file has no such grid, like `nanovdb_try_read_grid`
-  (`volume_grids.cpp:38-46`).
-- `vpt_grid_free(out)` releases either.
-
-The layout is NanoVDB 32.x restated (NanoVDB is not in the reference tree), checked against the
-independent Python restatement (`volume_path_tracer_amd/nvdb.py`) on files with tiles at every level,
-scaled maps, signed values and both codecs (`tests/test_nanovdb_native.py`); parity with the real
-library is unpinned. Without the drop-in, a C caller does:
-
-```c
-vpt_configuration c;  vpt_config_read(config_path, &c);
-vpt_grid_desc *d, *t;
-vpt_grid_read_nvdb(volume_path, "density", &d);        /* d == NULL: fatal, as read_from_file */
-vpt_grid_read_nvdb(volume_path, "temperature", &t);    /* t may be NULL */
-vpt_gpu_ctx* ctx;
-vpt_gpu_create(&c, d, t, NULL /* computes init_blackbody_radiation_xyz */, device, &ctx);
-vpt_grid_free(d); if (t) vpt_grid_free(t);             /* the context keeps its own copy */
-vpt_gpu_render_jobs(ctx, 0, total_jobs, NULL, NULL);   /* any jid ranges, any streams */
-vpt_gpu_film_add_to_host(ctx, film_hxwx4);
-vpt_gpu_destroy(ctx);
-```
-
-## 3. Python (ctypes)
-
-`volume_path_tracer_amd/capi.py` is the complete ctypes mirror of `include/vpt_gpu.h`;
-`volume_path_tracer_amd/render.py` wraps it:
-
-```python
-from volume_path_tracer_amd.scenes import read_configuration, SynthGrid
-from volume_path_tracer_amd.render import Integrator, TileProvider, run
-
-cfg = read_configuration("volume_path_tracer_amd/scenes/wdas_cloud.json")
-density = SynthGrid(1, 512).grid(copy=False)          # or capi.Grid(...) from your own arrays
-it = Integrator(cfg, density, temperature=None, device=0)
-tp = TileProvider(cfg.output_size, cfg.num_waves, cfg.tile_size)
-film = run(cfg, it, tp)                               # float32 [H][W][4], XYZW like Image<float,4>
-```
-
-Multi-GPU (one process per GPU, `torch.distributed` over RCCL):
-
-```python
-from volume_path_tracer_amd import distributed as D
-for b, n in D.rank_job_ranges(rank, world, cfg.num_waves, it.jobs_per_wave, "strong"):
-    it.render_jobs(b, n)
-D.reduce_film(it.film)      # all-reduce of the H*W*4 fp32 film
-```
-
-## 4. Headless renderer, output and debug traces
-
-`main.cpp` without the window:
-
-```sh
-python -m volume_path_tracer_amd scenes/wdas_cloud.json out.png            # volume from the scene file (.nvdb / .npz)
-python -m volume_path_tracer_amd scenes/fire.json out.png --synthetic fire  # stand-in volume
-python -m volume_path_tracer_amd scene.json out.png --event-log log.csv --event-jobs 4
-```
-
-From C/C++: `vpt_film_to_srgb8(film, w, h, rgb)` is `film_to_image` (`main.cpp:12-24`);
-`vpt_gpu_trace_jobs` returns the `Logger` events (`worker.cpp:16-48`) of a job range and
-`vpt_gpu_majorant_trace` the `log_majorant_trace` rows of one ray; `traces.py` prints both in the
-reference's CSV format. `vpt_gpu_set_rng_mode(ctx, VPT_RNG_PIXEL)` switches to the throughput mode
-(per-pixel streams; statistically equivalent, not the reference's samples).
-
-## 5. Scheduling knobs (samples never depend on them)
-
-A launch's jobs keep their jid and RNG stream whatever order the GPU takes them in, so only the
-launch's drain changes:
-- `vpt_gpu_set_job_order(ctx, VPT_ORDER_*)`: jid order (TileProvider's), cost-ordered wave-major /
-  tile-major, or the default cost-ordered tail (`DESIGN.md` §4);
-- `vpt_gpu_set_tile_costs(ctx, cost_T)`: per-tile costs for that order, e.g. measured job times of an
-  earlier frame instead of the built-in estimate (`tools/job_log.py` measures them);
-- `vpt_gpu_set_job_permutation(ctx, perm, n)`: an explicit order for launches of exactly n jobs.
-- `vpt_gpu_set_tuning(ctx, gate_min, gate_idle, grid_blocks, gate_eval, gate_walk)`: the wavefront
-  gates of full launches and the persistent grid size (`gate_idle` must be >= 1: it is what lets a
-  wavefront with no walking lane run its waiting blocks);
-- `vpt_gpu_set_latency_tuning(ctx, wave_lanes, gate_min, gate_idle, gate_eval, gate_walk)`: launches
-  with at most 6 jobs per wavefront of the grid (a small batch from `run_gpu`, C1's 4 096-job frame)
-  spread their jobs over every wavefront, `wave_lanes` per wavefront (0 = auto), with their own gates
-  (default: every block runs for one lane). C1: 42.9 -> 20.7 ms per frame (`DESIGN.md` §7). A
-  drop-in that hands the GPU small token batches gets this automatically.
-
-The film's sample-count channel is written once per launch (a count kernel on the launch's stream),
-so a caller reading the film after `vpt_gpu_sync` sees exact counts.
-
-## 6. Error behaviour
-
-The reference `exit(1)`s on fatal errors (`vptFATAL`, `include/vpt/logging.hpp:16`). Every ABI
-function returns `VPT_OK` or an error code and sets `vpt_last_error()`:
-`VPT_E_PARSE` (missing/unknown JSON key, bad type), `VPT_E_IO` (unreadable file),
-`VPT_E_INVALID` (bad argument / grid), `VPT_E_HIP` (no HIP device — there is no CPU fallback — or
-a HIP runtime failure), `VPT_E_NOMEM`.

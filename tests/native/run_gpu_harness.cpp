@@ -1,25 +1,36 @@
-// run_gpu_harness.cpp — TEST HARNESS: main.cpp:46-87 headless, with run_gpu (the documented drop-in
-// for vpt::run) in place of run, over the restated TileProvider.  N host threads each own one GPU
-// context and drain one shared provider into one shared host film, which is written to a file for
-// tests/test_gpu_integration.py to compare with the oracle.
+// run_gpu_harness.cpp — TEST HARNESS: main.cpp:46-87 headless over the restated TileProvider, with
+// the reference-side drop-in of include/vpt_run.hpp in place of vpt::run.  N host threads share one
+// provider and one host film, which is written to a file for tests/test_gpu_integration.py to compare
+// with the oracle.
 //
-//   run_gpu_harness config=<scene.json> out=<film.f32> [w= h= waves= threads= batch= grid_n= dist=
-//                   temperature=0|1 stop_after=<jobs>]
+//   run_gpu_harness config=<scene.json> out=<film.f32> [mode=drain|run w= h= waves= threads= batch=
+//                   grid_n= dist= temperature=0|1 stop_after=<jobs> nvdb=<file.nvdb> gridbuf=<file>
+//                   tempbuf=<file>]
 //
-// The volume is the product library's synthetic stand-in (vpt_synth_grid: cloud density, plus the
-// 40*base temperature grid with temperature=1); the camera looks at it from (0, 0, -dist).
+// mode=drain (default): each thread owns a context made with vpt_gpu_create and calls
+//   vpt_gpu::drain(ctx, tp, film, batch).  The volume is nvdb= (vpt_grid_read_nvdb: "density", and
+//   "temperature" when present) or the product library's synthetic stand-in (cloud density, plus the
+//   40*base temperature grid with temperature=1).
+// mode=run: each thread calls vpt_gpu::run(params, vol, camera, tp, film, rng) with the reference's
+//   own argument types (tests/native/reference_types_headless.hpp), exactly as main.cpp:63-68 calls
+//   vpt::run; the volume is the NanoGrid<float> bytes of gridbuf= (and tempbuf=), the seed is private
+//   to the RandomNumberGenerator.
+// The camera looks at the volume from (0, 0, -dist) unless dist=0 (then the scene file's camera).
 // stop_after: after that many jobs thread 0 calls tp.stop_at_next_wave() (tile_provider.cpp:107-110).
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
+#include <iterator>
 #include <map>
 #include <string>
 #include <thread>
 #include <vector>
 
-#include "run_gpu.hpp"
+#include "reference_types_headless.hpp"
 #include "tile_provider_headless.hpp"
+#include "vpt_run.hpp"
 
 namespace {
 
@@ -38,6 +49,13 @@ int fail(const char* what) {
   std::fprintf(stderr, "run_gpu_harness: %s: %s\n", what, vpt_last_error());
   return 1;
 }
+
+std::vector<char> slurp(const std::string& path) {
+  std::ifstream in(path, std::ios::binary);
+  return std::vector<char>((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+}
+
+vpt_headless::Vector3f v3(const float* f) { return vpt_headless::Vector3f{{f[0], f[1], f[2]}}; }
 
 }  // namespace
 
@@ -63,43 +81,99 @@ int main(int argc, char** argv) {
   cfg.num_waves = (uint32_t)num("waves", cfg.num_waves);
   const int grid_n = (int)num("grid_n", 64);
   const float dist = (float)num("dist", 800 * grid_n / 512);
-  const float cam[9] = {0, 0, -dist, 0, 0, 0, 0, 1, 0};
-  std::memcpy(cfg.camera_parameters.position, cam, 3 * sizeof(float));
-  std::memcpy(cfg.camera_parameters.look, cam + 3, 3 * sizeof(float));
-  std::memcpy(cfg.camera_parameters.up, cam + 6, 3 * sizeof(float));
+  if (dist != 0.0f) {
+    const float cam[9] = {0, 0, -dist, 0, 0, 0, 0, 1, 0};
+    std::memcpy(cfg.camera_parameters.position, cam, 3 * sizeof(float));
+    std::memcpy(cfg.camera_parameters.look, cam + 3, 3 * sizeof(float));
+    std::memcpy(cfg.camera_parameters.up, cam + 6, 3 * sizeof(float));
+  }
   const int threads = (int)num("threads", 2);
   const uint64_t batch = (uint64_t)num("batch", 1000);
+  const std::string mode = a.count("mode") ? a["mode"] : "drain";
 
-  vpt_grid_desc* dens = vpt_synth_grid(1, grid_n);
-  vpt_grid_desc* temp = num("temperature", 0) ? vpt_synth_grid(2, grid_n) : nullptr;
-  if (!dens || (num("temperature", 0) && !temp)) return fail("vpt_synth_grid");
-
-  // main.cpp:46-55: provider and film; then one worker per context (main.cpp:62-68)
+  // main.cpp:46-55: provider and film; then num_workers threads (main.cpp:62-68)
   vpt_headless::TileProvider tp(cfg.output_size[0], cfg.output_size[1], cfg.num_waves, cfg.tile_size[0],
                                 cfg.tile_size[1]);
   StoppingProvider sp{tp, (uint64_t)num("stop_after", 0)};
-  std::vector<float> film((size_t)(cfg.output_size[0] * cfg.output_size[1] * 4), 0.0f);
-  std::vector<vpt_gpu_ctx*> ctx(threads, nullptr);
-  const int ndev = (int)num("devices", 1);
-  for (int i = 0; i < threads; ++i)
-    if (vpt_gpu_create(&cfg, dens, temp, nullptr, i % ndev, &ctx[i])) return fail("vpt_gpu_create");
+  vpt_headless::Image<float, 4> film(cfg.output_size[0], cfg.output_size[1]);
   std::vector<int> rc(threads, 0);
-  {
+
+  if (mode == "seed") {  // the drop-in's seed recovery (no GPU): the RNG's seed is private
+    vpt_headless::RandomNumberGenerator rng(cfg.seed);
+    uint32_t seed = 0;
+    const int r = vpt_gpu::detail::rng_seed(rng, seed);
+    std::printf("run_gpu_harness: seed %d %u\n", r, seed);
+    return 0;
+  }
+  if (mode == "tiles") {  // the drop-in's tile-size derivation from a first batch of `batch` tokens (no GPU)
+    vpt_gpu::detail::TokenRects rects;
+    vpt_gpu::JobRuns runs;
+    vpt_gpu::take_jobs(sp, batch, runs, [&](auto& t) {
+      const auto r = t.compute_rect();
+      rects.push_back({(uint64_t)t.jid(), {r.start.x(), r.start.y(), r.size.x(), r.size.y()}});
+    });
+    int64_t tw = 0, th = 0;
+    const bool ok = vpt_gpu::detail::tile_size_from_rects(rects, cfg.output_size[0], cfg.output_size[1], tw, th);
+    std::printf("run_gpu_harness: tiles %d %lld %lld %zu\n", ok ? 1 : 0, (long long)tw, (long long)th, runs.size());
+    return 0;
+  }
+  if (mode == "run") {
+    // The reference's objects, built from the same configuration as main.cpp builds them.
+    const std::vector<char> gbuf = slurp(a["gridbuf"]), tbuf = a.count("tempbuf") ? slurp(a["tempbuf"]) : std::vector<char>();
+    if (gbuf.size() < 672) return fail("gridbuf");
+    const vpt_worker_params& w = cfg.worker_parameters;
+    vpt_headless::WorkerParameters params{{w.single_pixel_enabled != 0, {{w.single_pixel_coord[0], w.single_pixel_coord[1]}}},
+                                          w.use_jitter != 0,
+                                          {v3(w.infinite_light_xyz), w.infinite_light_multiplier},
+                                          {v3(w.distant_light_xyz), w.distant_light_multiplier, v3(w.distant_light_inv_direction)},
+                                          w.max_depth};
+    const vpt_volume_params& v = cfg.volume_parameters;
+    vpt_headless::Volume vol{{reinterpret_cast<const vpt_headless::NanoGridF*>(gbuf.data()),
+                              tbuf.empty() ? nullptr : reinterpret_cast<const vpt_headless::NanoGridF*>(tbuf.data())},
+                             {v.henyey_greenstein_g, v.le_scale, v.sigma_a, v.sigma_s, v.temperature_offset, v.temperature_scale}};
+    const vpt_camera_params& c = cfg.camera_parameters;
+    vpt_headless::Camera camera{{v3(c.position), v3(c.look), v3(c.up), c.vfov_deg, c.imaging_ratio}};
     std::vector<std::thread> pool;
     for (int i = 0; i < threads; ++i)
-      pool.emplace_back([&, i] { rc[i] = run_gpu(ctx[i], sp, film.data(), batch); });
+      pool.emplace_back([&, i] {
+        vpt_headless::RandomNumberGenerator rng(cfg.seed);
+        rc[i] = vpt_gpu::run_checked(params, vol, camera, sp, film, rng);  // vpt::run(...) in main.cpp
+      });
     for (auto& t : pool) t.join();
+    for (int i = 0; i < threads; ++i)
+      if (rc[i]) return fail("vpt_gpu::run");
+  } else {
+    vpt_grid_desc *dens = nullptr, *temp = nullptr;
+    if (a.count("nvdb")) {
+      if (vpt_grid_read_nvdb(a["nvdb"].c_str(), "density", &dens) || !dens) return fail("vpt_grid_read_nvdb density");
+      if (vpt_grid_read_nvdb(a["nvdb"].c_str(), "temperature", &temp)) return fail("vpt_grid_read_nvdb temperature");
+    } else {
+      dens = vpt_synth_grid(1, grid_n);
+      temp = num("temperature", 0) ? vpt_synth_grid(2, grid_n) : nullptr;
+      if (!dens || (num("temperature", 0) && !temp)) return fail("vpt_synth_grid");
+    }
+    std::vector<vpt_gpu_ctx*> ctx(threads, nullptr);
+    const int ndev = (int)num("devices", 1);
+    for (int i = 0; i < threads; ++i)
+      if (vpt_gpu_create(&cfg, dens, temp, nullptr, i % ndev, &ctx[i])) return fail("vpt_gpu_create");
+    float* fh = reinterpret_cast<float*>(film.data().data());
+    {
+      std::vector<std::thread> pool;
+      for (int i = 0; i < threads; ++i) pool.emplace_back([&, i] { rc[i] = vpt_gpu::drain(ctx[i], sp, fh, batch); });
+      for (auto& t : pool) t.join();
+    }
+    for (int i = 0; i < threads; ++i)
+      if (rc[i]) return fail("vpt_gpu::drain");
+    for (auto* c : ctx) vpt_gpu_destroy(c);
+    vpt_grid_free(dens);
+    if (temp) vpt_grid_free(temp);
   }
-  for (int i = 0; i < threads; ++i)
-    if (rc[i]) return fail("run_gpu");
-  for (auto* c : ctx) vpt_gpu_destroy(c);
-  vpt_synth_free(dens);
-  if (temp) vpt_synth_free(temp);
 
   FILE* f = std::fopen(a["out"].c_str(), "wb");
-  if (!f || std::fwrite(film.data(), sizeof(float), film.size(), f) != film.size()) return fail("write film");
+  const size_t n = film.px.size() * 4;
+  if (!f || std::fwrite(film.px.data(), sizeof(float), n, f) != n) return fail("write film");
   std::fclose(f);
-  std::printf("run_gpu_harness: %d threads, %u waves started, %llu jobs handed out\n", threads, tp.max_wave_started(),
-              (unsigned long long)sp.handed.load());
+  std::printf("run_gpu_harness: %s, %d threads, %u waves started, %llu jobs handed out\n", mode.c_str(), threads,
+              tp.max_wave_started(), (unsigned long long)sp.handed.load());
   return 0;
 }

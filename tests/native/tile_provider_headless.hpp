@@ -23,8 +23,14 @@
 
 namespace vpt_headless {
 
+// image_rect_t (include/vpt/image.hpp:31-38): start and size with Eigen's x() / y()
+struct Point {
+  int64_t px, py;
+  int64_t x() const { return px; }
+  int64_t y() const { return py; }
+};
 struct Rect {
-  int64_t x0, y0, w, h;
+  Point start, size;
 };
 
 class TileProvider {
@@ -48,7 +54,7 @@ class TileProvider {
     explicit operator bool() const { return valid(); }
     size_t wave() const { return wave_; }
     size_t jid() const { return jid_; }
-    Rect compute_rect() const { return owner_.compute_tile_rect(tile_); }
+    Rect compute_rect() { return owner_.compute_tile_rect(tile_); }
 
    private:
     friend class TileProvider;
@@ -105,7 +111,7 @@ class TileProvider {
     const int64_t y0 = (int64_t)(tile / (tile_index_t)ntx_) * tile_h_;
     const int64_t w = img_w_ - x0 < tile_w_ ? img_w_ - x0 : tile_w_;
     const int64_t h = img_h_ - y0 < tile_h_ ? img_h_ - y0 : tile_h_;
-    return Rect{x0, y0, w, h};
+    return Rect{Point{x0, y0}, Point{w, h}};
   }
 
  private:

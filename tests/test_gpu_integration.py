@@ -1,10 +1,16 @@
-"""The reference-side drop-in (tests/native/run_gpu.hpp) compiled and driven the way
-main.cpp:62-87 drives vpt::run: several host threads, one GPU context each, one shared TileProvider
-(restated with its wave gating, tests/native/tile_provider_headless.hpp) and one shared host film.
+"""The reference-side drop-in (include/vpt_run.hpp) compiled and driven the way
+main.cpp:62-87 drives vpt::run: several host threads, one shared TileProvider (restated with its wave
+gating, tests/native/tile_provider_headless.hpp) and one shared host film, either
+  * mode=drain: one GPU context per thread (vpt_gpu_create) and vpt_gpu::drain, the volume from an
+    .nvdb file through the C++ reader (vpt_grid_read_nvdb) or the synthetic stand-in, or
+  * mode=run: vpt_gpu::run(params, vol, camera, provider, film, rng) with the reference's own argument
+    types (tests/native/reference_types_headless.hpp), the volume as NanoGrid<float> bytes and the seed
+    private to the RNG -- the call main.cpp:63-68 makes, with only the function name changed.
 
 Bar: no hang (the harness runs under a timeout), every pixel's sample count equals the number of
 waves rendered, and the film equals the oracle's serial render of the same job ids to fp32
 atomic-order rounding."""
+import json
 import subprocess
 from pathlib import Path
 
@@ -19,12 +25,13 @@ ROOT = Path(__file__).resolve().parents[1]
 HARNESS = ROOT / "tests" / "native" / "build" / "run_gpu_harness"
 
 
-def _harness(tmp_path, scene, w, h, waves, threads, batch, grid_n=64, temperature=0, stop_after=0):
+def _harness(tmp_path, scene, w, h, waves, threads, batch, grid_n=64, temperature=0, stop_after=0, **extra):
     assert_hip_untouched()
     out = tmp_path / "film.f32"
-    args = [str(HARNESS), f"config={SCENE_DIR / scene}", f"out={out}", f"w={w}", f"h={h}", f"waves={waves}",
+    config = scene if Path(str(scene)).is_absolute() else SCENE_DIR / scene
+    args = [str(HARNESS), f"config={config}", f"out={out}", f"w={w}", f"h={h}", f"waves={waves}",
             f"threads={threads}", f"batch={batch}", f"grid_n={grid_n}", f"temperature={temperature}",
-            f"stop_after={stop_after}"]
+            f"stop_after={stop_after}"] + [f"{k}={v}" for k, v in extra.items()]
     r = subprocess.run(args, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr + r.stdout
     return np.fromfile(out, np.float32).reshape(h, w, 4), r.stdout
@@ -84,8 +91,91 @@ def test_run_gpu_stop_at_next_wave(tmp_path):
     assert "2 waves started" in log
 
 
-def test_integration_doc_shows_run_gpu_verbatim():
+def test_integration_doc_shows_the_drop_in_verbatim():
     """INTEGRATION.md §2 is the compiled, tested drop-in, not a sketch."""
     doc = (ROOT / "INTEGRATION.md").read_text()
-    src = (ROOT / "tests" / "native" / "run_gpu.hpp").read_text()
+    src = (ROOT / "include" / "vpt_run.hpp").read_text()
     assert src.strip() in doc
+
+
+@pytest.mark.parametrize("seed", [0, 10, 500, 4294967295])
+def test_drop_in_recovers_the_private_seed(tmp_path, seed):
+    """The reference's RandomNumberGenerator keeps its seed private (random.hpp:86-115): the drop-in
+    finds it from the job-0 stream (no GPU needed)."""
+    scene = json.loads((SCENE_DIR / "wdas_cloud.json").read_text())
+    scene["seed"] = seed
+    p = tmp_path / "s.json"
+    p.write_text(json.dumps(scene))
+    r = subprocess.run([str(HARNESS), f"config={p}", f"out={tmp_path / 'x'}", "mode=seed"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0 and f"seed 0 {seed}" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("w,h,tile,batch", [(72, 40, 8, 3), (70, 38, 8, 1), (70, 38, 16, 100), (4, 4, 8, 1),
+                                            (20, 12, 8, 2), (64, 48, 8, 500)])
+def test_drop_in_reads_the_tile_size_off_the_tokens(tmp_path, w, h, tile, batch):
+    """TileProvider keeps its tile size private: the drop-in takes the largest rect of its first batch
+    and checks every rect against the jid mapping (an image narrower than a tile gives the image width,
+    which maps every jid the same way)."""
+    scene = json.loads((SCENE_DIR / "wdas_cloud.json").read_text())
+    scene["tile_size"] = [tile, tile]
+    p = tmp_path / "t.json"
+    p.write_text(json.dumps(scene))
+    r = subprocess.run([str(HARNESS), f"config={p}", f"out={tmp_path / 'x'}", "mode=tiles", f"w={w}", f"h={h}",
+                        "waves=2", f"batch={batch}"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    ok, tw, th, _ = (int(x) for x in r.stdout.split("tiles")[1].split())
+    assert ok == 1 and tw == min(tile, w) and (th == min(tile, h) or batch < -(-w // tile)), r.stdout
+
+
+def _write_buffer(tmp_path, grid, name):
+    from volume_path_tracer_amd import nvdb
+
+    p = tmp_path / f"{name}.grid"
+    p.write_bytes(nvdb.buffer_from_grid(grid, name))
+    return p
+
+
+@pytest.mark.gpu
+@pytest.mark.spawns
+@pytest.mark.parametrize("scene,name", [("wdas_cloud.json", "c3"), ("fire.json", "c4")])
+def test_reference_signature_run_from_main_threads(tmp_path, scene, name):
+    """vpt_gpu::run with main.cpp's arguments from 3 worker threads on one GPU: one thread drives the
+    device, the others return; the seed is recovered from the RNG (private in the reference); the
+    tile size from the tokens; the grids are read from NanoGrid<float> memory."""
+    w, h, waves = 72, 40, 3
+    extra = dict(mode="run", gridbuf=_write_buffer(tmp_path, SynthGrid(1, 64).grid(copy=True), "density"))
+    if name == "c4":
+        extra["tempbuf"] = _write_buffer(tmp_path, SynthGrid(2, 64).grid(copy=True), "temperature")
+    film, log = _harness(tmp_path, scene, w, h, waves, 3, 0, **extra)
+    np.testing.assert_array_equal(film[..., 3], waves)
+    ref = _oracle_film(name, w, h, waves)
+    np.testing.assert_allclose(film[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
+    assert f"{waves} waves started" in log
+
+
+@pytest.mark.gpu
+@pytest.mark.spawns
+def test_drain_from_nvdb_file_with_tiles_at_every_level(tmp_path):
+    """An .nvdb file (ZIP codec) of a grid with lower / upper / root tiles and sparse lower nodes, read
+    by the C++ reader inside the harness and rendered by 2 threads, against the oracle on the grid."""
+    from grids import sparse_grid
+    from volume_path_tracer_amd import nvdb
+
+    g = sparse_grid()
+    path = tmp_path / "sparse.nvdb"
+    nvdb.write_nvdb(path, {"density": g}, codec=nvdb.CODEC_ZIP)
+    scene = json.loads((SCENE_DIR / "wdas_cloud.json").read_text())
+    scene["camera_parameters"].update(position=[-40.0, -90.0, -700.0], look=[-40.0, -90.0, 10.0], vfov_deg=50.0)
+    cfg_path = tmp_path / "scene.json"
+    cfg_path.write_text(json.dumps(scene))
+    w, h, waves = 64, 48, 2
+    film, _ = _harness(tmp_path, cfg_path, w, h, waves, 2, 50, nvdb=path, dist=0)
+    np.testing.assert_array_equal(film[..., 3], waves)
+    wl = workload("c3", width=w, height=h, spp=waves)
+    from grids import look_at
+    look_at(wl.cfg, (-40.0, -90.0, -700.0), (-40.0, -90.0, 10.0))
+    wl.cfg.camera_parameters.vfov_deg = 50.0
+    f_o, _, c = O.render_jobs(wl.cfg, O.OracleGrid(g, fix_majorants=True), None, 0, wl.cfg.jobs_per_wave() * waves)
+    assert c["density_evals"] > 1000
+    np.testing.assert_allclose(film[..., :3], f_o[..., :3], rtol=1e-5, atol=1e-6)

@@ -651,6 +651,14 @@ extern "C" {
 const char* vpt_last_error(void) { return vpt::g_last_error.c_str(); }
 int vpt_abi_version(void) { return VPT_ABI_VERSION; }
 
+int vpt_gpu_device_count(int* count) {
+  if (!count) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_device_count: null argument");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return VPT_OK;
+}
+
 int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, const vpt_grid_desc* temperature,
                    const float* blackbody_500x3, int device, vpt_gpu_ctx** out) {
   if (!cfg || !density || !out) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_create: null argument");

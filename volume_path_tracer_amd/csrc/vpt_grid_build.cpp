@@ -73,6 +73,27 @@ inline int2 enc(int32_t code, float v) {
 
 float host_value_at(const HostGrid& g, int32_t i, int32_t j, int32_t k) { return value_at(g.dev, i, j, k); }
 
+OwnedGrid* owned_grid_new() { return new OwnedGrid(); }
+
+void OwnedGrid::finish() {
+  vpt_grid_desc& g = d;
+  g.leaf_count = leaf_max.size();
+  g.leaf_origin = leaf_origin.data();
+  g.leaf_values = leaf_values.data();
+  g.leaf_value_mask = leaf_mask.data();
+  g.leaf_max = leaf_max.data();
+  g.tile_count = tile_value.size();
+  g.tile_origin = tile_origin.data();
+  g.tile_level = tile_level.data();
+  g.tile_value = tile_value.data();
+  g.tile_active = tile_active.data();
+  g.lower_count = lower_origin.size() / 3;
+  g.lower_origin = lower_origin.data();
+  g.upper_count = upper_origin.size() / 3;
+  g.upper_origin = upper_origin.data();
+}
+
+
 void compute_runs(HostGrid& h, int threads) {
   if (threads <= 0) threads = default_threads();
   const DevGrid& G = h.dev;

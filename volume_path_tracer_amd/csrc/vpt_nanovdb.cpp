@@ -36,26 +36,6 @@
 
 namespace vpt {
 
-OwnedGrid* owned_grid_new() { return new OwnedGrid(); }
-
-void OwnedGrid::finish() {
-  vpt_grid_desc& g = d;
-  g.leaf_count = leaf_max.size();
-  g.leaf_origin = leaf_origin.data();
-  g.leaf_values = leaf_values.data();
-  g.leaf_value_mask = leaf_mask.data();
-  g.leaf_max = leaf_max.data();
-  g.tile_count = tile_value.size();
-  g.tile_origin = tile_origin.data();
-  g.tile_level = tile_level.data();
-  g.tile_value = tile_value.data();
-  g.tile_active = tile_active.data();
-  g.lower_count = lower_origin.size() / 3;
-  g.lower_origin = lower_origin.data();
-  g.upper_count = upper_origin.size() / 3;
-  g.upper_origin = upper_origin.data();
-}
-
 namespace {
 
 constexpr uint64_t kMagicNumber = 0x304244566F6E614EULL;  // "NanoVDB0"
