@@ -13,15 +13,19 @@ WORLD_SIZE is unset, by starting torch.distributed.run itself before anything to
   * default `--mode weak` (the driver's SCALE runs): every rank renders its own block of the C3
     frame's 256 waves (rank r: waves r*256+1 .. (r+1)*256), so N = 1 is exactly BENCH's C3 line and
     the per-GPU work is fixed;
-  * the 8-GPU configuration of BASELINE.json (configs[4], C5: one 3840x2160 frame at 1024 spp dealt
-    across the GPUs) is `--config c5 --mode strong --gpus 8`.
+  * for N > 1 the line also carries `scaling_strong`: the C3 frame (256 waves) and the C5 frame
+    (BASELINE.json configs[4], 3840x2160 at 1024 spp) each dealt across the N ranks and timed the same
+    way (barrier + synchronize, max over ranks, film all-reduce inside the step): the strong scaling
+    that north_star's ">= 6x at 8 GPUs" asks about (`--strong-configs`, '' to skip);
+  * `--config c5 --mode strong --gpus 8` makes the C5 frame the main measurement.
 
 The JSON line also carries:
   roofline      the integrator kernel's algorithmic bytes per launch (SURVEY §8d:
                 32*stencils + 8*dda_steps + 32*temp_stencils + 32*samples, from the kernel's own
                 event counters) / its average launch time (HIP events on the launch stream), against
-                the 8 TB/s HBM peak; `traffic` = PMC-measured HBM bytes per launch from
-                profiles/<round>_pmc.json when that file exists (rocprofv3 --pmc pass), else null.
+                the 8 TB/s HBM peak; `traffic` = PMC-measured HBM bytes per launch from the newest
+                committed profiles/<round>_<config>_pmc.json (a builder rocprofv3 --pmc pass, named in
+                `traffic_source`), else null.
   cpu_baseline  the CPU oracle (headless restatement of the reference worker pool, main.cpp:62-87)
                 timed on this host's cores on a bounded sample (whole waves of the same frame).
 """
@@ -133,6 +137,115 @@ def spawn_ranks(args) -> int:
     return subprocess.run(cmd).returncode
 
 
+def init_rank(args, env=None):
+    """(rank, world, device, scalar device) of this process.  One process per GPU: device LOCAL_RANK
+    (device 0 for --one-device, the one-GPU multi-process tests).  For world > 1 the process group is
+    RCCL over xGMI ("nccl", bound to the rank's device with device_id) or gloo (CPU-side tests);
+    scalars (timings, sample counts) travel on the device with RCCL, through the host with gloo."""
+    import torch
+    import torch.distributed as dist
+
+    env = os.environ if env is None else env
+    world = int(env.get("WORLD_SIZE", "1"))
+    rank = int(env.get("RANK", "0"))
+    local = int(env.get("LOCAL_RANK", "0"))
+    dev_index = 0 if (world == 1 or args.one_device) else local
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    if world > 1:
+        env.setdefault("MASTER_ADDR", "127.0.0.1")
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    sdev = dev if args.backend == "nccl" else torch.device("cpu")
+    return rank, world, dev, sdev
+
+
+def max_over_ranks(x: float, world: int, sdev) -> float:
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=sdev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: int, world: int, sdev) -> int:
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64, device=sdev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
+
+
+def timed_frames(it, rank, world, spp, mode, steps, warmup, stream, launch_ms=None):
+    """`warmup` untimed then `steps` timed frames (this rank's share of the spp waves, then the film
+    all-reduce), bracketed by a barrier and torch.cuda.synchronize() on both sides; returns the MAX
+    over ranks of the timed region (seconds).  launch_ms collects HIP-event pairs around each frame's
+    kernel launches (on the launch stream)."""
+    import torch
+    import torch.distributed as dist
+
+    from volume_path_tracer_amd import distributed as D
+
+    def step(timed: bool):
+        it.film.zero_()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)  # the kernel runs on this stream: the events bracket exactly its launches
+        D.render_rank(it, rank, world, spp, mode, stream=stream)
+        ev1.record(stream)
+        if timed and launch_ms is not None:
+            launch_ms.append((ev0, ev1))
+        D.reduce_film(it.film)
+
+    for _ in range(warmup):
+        step(False)
+    torch.cuda.synchronize()
+    it.counters(reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t_start
+
+
+def strong_scaling(configs, dens, rank, world, dev, sdev, steps, warmup, stream):
+    """For N > 1: each config's whole frame (its spp waves) dealt across the N ranks (distributed
+    "strong" ranges), timed like the main loop -- the work the north_star's "scaling at 8 GPUs" means
+    (C3: the headline frame; C5: BASELINE's 8-GPU configuration, 3840x2160 at 1024 spp)."""
+    from volume_path_tracer_amd import distributed as D
+    from volume_path_tracer_amd.render import Integrator
+    from volume_path_tracer_amd.scenes import workload
+
+    out = {}
+    for name in configs:
+        wl = workload(name)
+        if wl.temperature or wl.density_kind != 1 or wl.grid_n != 512:
+            raise ValueError(f"--strong-configs: {name} does not share the 512^3 cloud stand-in")
+        it = Integrator(wl.cfg, dens, None, device=dev.index)
+        elapsed = max_over_ranks(timed_frames(it, rank, world, wl.spp, "strong", steps, warmup, stream), world, sdev)
+        samples = sum_over_ranks(it.counters()["samples"], world, sdev)
+        film = it.film_host()
+        assert (film[..., 3] == D.total_samples_per_pixel(world, wl.spp, "strong")).all(), "sample-count channel mismatch"
+        assert samples == wl.cfg.width * wl.cfg.height * wl.spp * steps, samples
+        out[name] = {"workload": f"{name}: {wl.cfg.width}x{wl.cfg.height}, {wl.spp} spp per image, dealt over {world} GPUs",
+                     "ms_per_step": round(elapsed / steps * 1e3, 3), "value": round(samples / elapsed / 1e6, 3),
+                     "unit": "Msamples/s", "steps": steps, "warmup": warmup}
+        del it
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -142,6 +255,8 @@ def main():
     ap.add_argument("--spp", type=int, default=None, help="override waves per step (default: the config's)")
     ap.add_argument("--mode", choices=["weak", "strong"], default="weak",
                     help="weak: each rank renders its own spp waves; strong: the spp waves are dealt across ranks")
+    ap.add_argument("--strong-configs", default="c3,c5",
+                    help="N > 1: configs whose whole frame is also timed dealt across the ranks ('' = none)")
     ap.add_argument("--rng-mode", choices=["reference", "pixel"], default="reference",
                     help="pixel = throughput mode (per-pixel streams; not the reference's samples)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -158,21 +273,11 @@ def main():
     if world != args.gpus:
         log(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}: launch with --nproc-per-node equal to --gpus")
         sys.exit(2)
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
     import torch.distributed as dist
 
-    dev_index = 0 if (world == 1 or args.one_device) else local
-    torch.cuda.set_device(dev_index)
-    dev = torch.device("cuda", dev_index)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+    rank, world, dev, sdev = init_rank(args)
 
     from volume_path_tracer_amd import distributed as D
     from volume_path_tracer_amd.render import Integrator
@@ -195,57 +300,32 @@ def main():
     jobs_rank = sum(n for _, n in ranges)
     stream = torch.cuda.current_stream(dev)
     launch_ms = []
-
-    def step(timed: bool):
-        it.film.zero_()
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        ev0.record(stream)  # the kernel runs on this stream: the events bracket exactly its launches
-        D.render_rank(it, rank, world, spp, args.mode, stream=stream)
-        ev1.record(stream)
-        if timed:
-            launch_ms.append((ev0, ev1))
-        D.reduce_film(it.film)
-
-    for _ in range(args.warmup):
-        step(False)
-    torch.cuda.synchronize()
-    it.counters(reset=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    # scalars travel on the device with RCCL, through the host with gloo
-    sdev = dev if args.backend == "nccl" else torch.device("cpu")
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=sdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(timed_frames(it, rank, world, spp, args.mode, args.steps, args.warmup, stream, launch_ms),
+                             world, sdev)
 
     kernel_ms = [a.elapsed_time(b) for a, b in launch_ms]
     counters = it.counters()
-    area = int(wl.cfg.tile_size[0] * wl.cfg.tile_size[1])
     samples_rank = counters["samples"]
     assert samples_rank == (wl.cfg.width * wl.cfg.height * jobs_rank // it.jobs_per_wave) * args.steps, samples_rank
-    t = torch.tensor([samples_rank], dtype=torch.float64, device=sdev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    total_samples = int(t.item())
+    total_samples = sum_over_ranks(samples_rank, world, sdev)
     value = total_samples / elapsed / 1e6
     launches_per_step = max(1, len(ranges))
+    film = it.film_host()
+    assert (film[..., 3] == D.total_samples_per_pixel(world, spp, args.mode)).all(), "sample-count channel mismatch"
+    del it
+
+    strong = None
+    if world > 1 and args.strong_configs and args.rng_mode == "reference":
+        strong = strong_scaling([c for c in args.strong_configs.split(",") if c], dens, rank, world, dev, sdev,
+                                args.steps, args.warmup, stream)
 
     if rank == 0:
         avg_launch_s = sum(kernel_ms) / len(kernel_ms) / 1e3 / launches_per_step
         bytes_per_launch = algorithmic_bytes(counters) / (args.steps * launches_per_step)
         achieved = bytes_per_launch / avg_launch_s / 1e9
-        traffic = None
-        # the newest round's PMC measurement of this workload (tools/profile_round.sh), if any
+        traffic, traffic_source = None, None
+        # PMC-measured HBM bytes of this workload from the newest committed rocprofv3 pass
+        # (tools/profile_round.sh): a builder measurement, labelled with its file, not this run's
         for pf in sorted((ROOT / "profiles").glob("*_pmc.json"), reverse=True):
             try:
                 pj = json.loads(pf.read_text())
@@ -253,9 +333,8 @@ def main():
                 continue
             if pj.get("config") == args.config and pj.get("spp") == spp:
                 traffic = pj.get("hbm_bytes_per_launch")
+                traffic_source = f"profiles/{pf.name}"
                 break
-        film = it.film_host()
-        assert (film[..., 3] == D.total_samples_per_pixel(world, spp, args.mode)).all(), "sample-count channel mismatch"
         out = {
             "metric": baseline_metric(),
             "value": round(value, 3),
@@ -280,6 +359,7 @@ def main():
                        "rng_mode": args.rng_mode},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "traffic_source": traffic_source,
                          "kernel": "vpt_integrate_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                          "algorithmic_bytes_per_launch": int(bytes_per_launch),
                          "bytes_per_sample": round(algorithmic_bytes(counters) / samples_rank, 2)},
@@ -287,6 +367,8 @@ def main():
             "counters_per_sample": {k: round(counters[k] / samples_rank, 3)
                                     for k in ("dda_steps", "stencils", "temp_stencils")},
         }
+        if strong is not None:
+            out["scaling_strong"] = strong
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(wl, dens, temp, args.cpu_budget)
             out["cpu_baseline"] = cb

@@ -1,0 +1,54 @@
+"""bench.py's process setup without a GPU: the RCCL ("nccl") branch binds each rank to device
+LOCAL_RANK and hands that device to init_process_group (the communicator's device), --one-device puts
+every rank on device 0, gloo keeps scalars on the host, and a single process initialises no group.
+torch.cuda.set_device / dist.init_process_group are recorded, not called."""
+import argparse
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import bench  # noqa: E402
+
+
+@pytest.fixture
+def recorded(monkeypatch):
+    calls = {"set_device": [], "init": []}
+    monkeypatch.setattr(torch.cuda, "set_device", lambda d: calls["set_device"].append(d))
+    monkeypatch.setattr(dist, "init_process_group", lambda *a, **k: calls["init"].append((a, k)))
+    return calls
+
+
+def _args(backend="nccl", one_device=False):
+    return argparse.Namespace(backend=backend, one_device=one_device)
+
+
+def test_nccl_rank_binds_its_local_device(recorded):
+    env = {"WORLD_SIZE": "8", "RANK": "13", "LOCAL_RANK": "5"}
+    rank, world, dev, sdev = bench.init_rank(_args(), env)
+    assert (rank, world) == (13, 8) and dev == torch.device("cuda", 5) and sdev == dev
+    assert recorded["set_device"] == [5]
+    assert recorded["init"] == [(("nccl",), {"device_id": torch.device("cuda", 5)})]
+    assert env["MASTER_ADDR"] == "127.0.0.1"
+
+
+def test_one_device_and_gloo(recorded):
+    rank, world, dev, sdev = bench.init_rank(_args("gloo", True), {"WORLD_SIZE": "2", "RANK": "1", "LOCAL_RANK": "1"})
+    assert dev == torch.device("cuda", 0) and sdev == torch.device("cpu")
+    assert recorded["set_device"] == [0] and recorded["init"] == [(("gloo",), {})]
+
+
+def test_single_process_initialises_no_group(recorded):
+    rank, world, dev, sdev = bench.init_rank(_args(), {})
+    assert (rank, world) == (0, 1) and dev == torch.device("cuda", 0)
+    assert recorded["init"] == []
+
+
+def test_strong_scaling_configs_share_the_cloud():
+    """--strong-configs only accepts frames of the 512^3 cloud (the grid is built once)."""
+    with pytest.raises(ValueError, match="c4"):
+        bench.strong_scaling(["c4"], None, 0, 2, torch.device("cuda", 0), torch.device("cpu"), 1, 0, None)

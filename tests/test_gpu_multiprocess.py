@@ -81,11 +81,14 @@ def test_bench_gpus2_spawns_two_ranks(tmp_path):
     assert_hip_untouched()
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
-                        "--spp", "2", "--no-cpu-baseline", "--backend", "gloo", "--one-device"],
+                        "--spp", "2", "--no-cpu-baseline", "--backend", "gloo", "--one-device", "--strong-configs", "c3"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["value"] > 0
+    # and the strong-scaling record: the whole C3 frame dealt over the 2 ranks, timed the same way
+    s = line["scaling_strong"]["c3"]
+    assert s["value"] > 0 and s["ms_per_step"] > 0 and "1920x1080, 256 spp" in s["workload"]
     # WORLD_SIZE that disagrees with --gpus is an error
     env2 = dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r2 = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1"], cwd=ROOT, env=env2,
