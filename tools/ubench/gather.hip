@@ -1,0 +1,91 @@
+// Ceiling of divergent 4-byte per-lane gathers (tools only): the access pattern of the integrator's
+// HDDA walk-word loads (one 4-byte word per lane from a table of ~1.2 MiB, each lane at a different
+// line).  Every lane follows `Chains` independent random walks through the table (next = t[cur]),
+// so a wavefront keeps Chains divergent loads in flight; occupancy is set with dynamic LDS.  Reports
+// loads/s per CU for table sizes from L2-resident (1.2 MiB, the C3 walk table) to HBM-resident, and
+// the memory-level parallelism (chains x waves/SIMD) the request rate saturates at.
+//   hipcc -O3 --offload-arch=gfx950 -o gather gather.hip && ./gather
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CHECK(x)                                                                              \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess) {                                                                   \
+      std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                           \
+      std::exit(1);                                                                           \
+    }                                                                                         \
+  } while (0)
+
+template <int Chains>
+__global__ __launch_bounds__(256) void chase(const uint32_t* __restrict__ t, uint32_t n, int iters, uint32_t* out) {
+  extern __shared__ uint32_t occupancy_lds[];  // only sizes the block (waves per SIMD)
+  uint32_t idx[Chains];
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+#pragma unroll
+  for (int c = 0; c < Chains; ++c) idx[c] = (g * 2654435761u + c * 40503u) % n;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int c = 0; c < Chains; ++c) idx[c] = t[idx[c]];
+  }
+  uint32_t r = 0;
+#pragma unroll
+  for (int c = 0; c < Chains; ++c) r ^= idx[c];
+  if (r == 0xFFFFFFFFu) out[0] = r + occupancy_lds[0];
+}
+
+template <int Chains>
+double run(const uint32_t* t, uint32_t n, int waves, int cus, uint32_t* out, size_t lds_total) {
+  const int blocks = cus * waves;  // 256 threads = 4 waves per block, one per SIMD
+  const size_t lds = lds_total / waves - 1024;
+  const int iters = 512;
+  CHECK(hipFuncSetAttribute((const void*)chase<Chains>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  hipLaunchKernelGGL(chase<Chains>, dim3(blocks), dim3(256), lds, 0, t, n, iters, out);
+  CHECK(hipEventRecord(e0));
+  hipLaunchKernelGGL(chase<Chains>, dim3(blocks), dim3(256), lds, 0, t, n, iters, out);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  CHECK(hipGetLastError());
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  const double loads = (double)blocks * 256 * iters * Chains;
+  return loads / (ms * 1e-3) / cus;  // loads per second per CU
+}
+
+int main(int argc, char** argv) {
+  int cus = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const size_t lds_total = 160 * 1024;
+  uint32_t* out;
+  CHECK(hipMalloc(&out, 4));
+  const size_t sizes[] = {307200, 1u << 22, 1u << 26};  // 1.2 MiB (L2), 16 MiB (MALL), 256 MiB (HBM)
+  std::printf("gather ceiling: %d CUs, divergent 4-B loads, loads/s per CU (G)\n", cus);
+  std::printf("%10s %6s %6s %10s\n", "table_MiB", "chains", "waves", "Gload/s/CU");
+  for (size_t n : sizes) {
+    std::vector<uint32_t> h(n);
+    uint64_t s = 88172645463325252ull;
+    for (size_t i = 0; i < n; ++i) {
+      s ^= s << 13;
+      s ^= s >> 7;
+      s ^= s << 17;
+      h[i] = (uint32_t)(s % n);
+    }
+    uint32_t* t;
+    CHECK(hipMalloc(&t, n * 4));
+    CHECK(hipMemcpy(t, h.data(), n * 4, hipMemcpyHostToDevice));
+    for (int waves : {1, 2, 4, 7, 8}) {
+      std::printf("%10.2f %6d %6d %10.4f\n", n * 4.0 / (1 << 20), 1, waves, run<1>(t, (uint32_t)n, waves, cus, out, lds_total) * 1e-9);
+      std::printf("%10.2f %6d %6d %10.4f\n", n * 4.0 / (1 << 20), 2, waves, run<2>(t, (uint32_t)n, waves, cus, out, lds_total) * 1e-9);
+      std::printf("%10.2f %6d %6d %10.4f\n", n * 4.0 / (1 << 20), 4, waves, run<4>(t, (uint32_t)n, waves, cus, out, lds_total) * 1e-9);
+    }
+    CHECK(hipFree(t));
+  }
+  return 0;
+}
