@@ -2,6 +2,7 @@
 // serially on the CPU so that its control flow and float semantics can be checked bit-for-bit
 // against the oracle without a GPU.  Not part of the product library; the product path is the
 // HIP kernel in volume_path_tracer_amd/csrc/vpt_gpu.hip.
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -41,7 +42,16 @@ struct HostEnv {
     return true;
   }
   const double (*logf_table() const)[2] { return vpt::math::kLogfTab; }
-  const float* bb_table(const vpt::DevScene& S) const { return S.bb; }
+  void blackbody(const vpt::DevScene& S, float t, float& X, float& Y, float& Z) const {
+    if (S.bb_lds_ok) {  // the kernel's LDS path: only the first kBbLdsRows rows (NaN beyond, so a
+                        // lookup past them would show in the parity tests)
+      std::vector<float> rows(501 * 3, __builtin_nanf(""));
+      std::copy(S.bb, S.bb + vpt::kBbLdsRows * 3, rows.begin());
+      vpt::blackbody_xyz(S, rows.data(), t, X, Y, Z);
+    } else {
+      vpt::blackbody_xyz(S, S.bb, t, X, Y, Z);
+    }
+  }
   void film_add(const vpt::DevScene& S, const vpt::Lane& ln, int32_t px, int32_t py, int32_t rw) {
     float* f = film + ((int64_t)py * S.W + px) * 4;
     f[3] += 1.0f;
@@ -78,6 +88,8 @@ extern "C" int vpths_render_jobs_order(const vpt_configuration* cfg, const vpt_g
     if ((rc = vpt::build_host_grid(*temperature, false, 0, ht))) return rc;
     S.temperature = ht.dev;
     S.has_temperature = 1;
+    S.bb_lds_ok = vpt::blackbody_rows_suffice(*temperature, cfg->volume_parameters.temperature_scale,
+                                              cfg->volume_parameters.temperature_offset, vpt::kBbLdsRows);
   }
   std::vector<float> bb(501 * 3, 0.0f);
   if (bb500)

@@ -166,7 +166,8 @@ def test_drain_from_nvdb_file_with_tiles_at_every_level(tmp_path):
     path = tmp_path / "sparse.nvdb"
     nvdb.write_nvdb(path, {"density": g}, codec=nvdb.CODEC_ZIP)
     scene = json.loads((SCENE_DIR / "wdas_cloud.json").read_text())
-    scene["camera_parameters"].update(position=[-40.0, -90.0, -700.0], look=[-40.0, -90.0, 10.0], vfov_deg=50.0)
+    scene["camera_parameters"].update(position=[-40.0, -90.0, -700.0], look=[-40.0, -90.0, 10.0], up=[0.0, 1.0, 0.0],
+                                      vfov_deg=50.0)
     cfg_path = tmp_path / "scene.json"
     cfg_path.write_text(json.dumps(scene))
     w, h, waves = 64, 48, 2

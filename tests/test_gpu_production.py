@@ -347,3 +347,20 @@ def test_mapped_grid_production_films_bit_exact(case):
     c = it.counters()
     for k in COUNTERS:
         assert c[k] == tot[k], (k, c[k], tot[k])
+
+
+def test_temperature_kernel_blackbody_from_memory_above_the_lds_rows():
+    """A temperature scale that reaches 20 000 K: the blackbody rows past the kernel's LDS copy
+    (kBbLdsRows) are read from memory; the production films stay bit-exact vs the oracle."""
+    from volume_path_tracer_amd.render import Integrator
+
+    wl = workload("c4", width=40, height=32, spp=2, grid_n=64)
+    wl.cfg.volume_parameters.temperature_scale *= 10.0
+    dens, temp = _grids(wl)
+    it = Integrator(wl.cfg, dens, temp, device=0)
+    od, ot = _oracle_grids(dens, temp)
+    T = wl.cfg.jobs_per_wave()
+    for wave in (1, 2):
+        f_o, _, c_o = O.render_jobs(wl.cfg, od, ot, (wave - 1) * T, T)
+        _assert_bitwise(_prod_film(it, (wave - 1) * T, T), f_o, f"wave {wave}")
+    assert c_o["temp_stencils"] > 0

@@ -146,3 +146,17 @@ def test_mapped_grids_and_walk_padding(case):
         assert c_o[k] == c_h[k], k
     assert c_o["density_evals"] > 500 and c_o["scatters"] > 50, c_o
     assert HS.walk_outside() == 0
+
+
+@pytest.mark.parametrize("scale", [1.0, 10.0])
+def test_blackbody_rows_in_lds_or_memory(scale):
+    """The temperature kernel reads the blackbody table's first kBbLdsRows rows from LDS when the grid's
+    temperatures stay below them (the fire stand-in: T <= 2 020 K), else the whole table from memory
+    (scale 10: T up to 20 200 K).  The host simulator's LDS path sees NaN past those rows, so a wrong
+    bound would show here."""
+    wl = workload("c4", width=32, height=24, spp=2, grid_n=64)
+    wl.cfg.volume_parameters.temperature_scale *= scale
+    jobs = wl.cfg.jobs_per_wave() * 2
+    f_o, r_o, c_o, f_h, r_h, c_h = _run_both(wl, jobs)
+    assert np.array_equal(r_o.view(np.uint32), r_h.view(np.uint32))
+    assert c_o["temp_stencils"] > 100

@@ -57,7 +57,7 @@ __shared__ LaneCold g_lane_cold[kBlockThreads];
 // temperature kernel's 501 x 3 blackbody table): LDS reads instead of vector-memory loads, which
 // would count in vmcnt with the walk's loads.
 __shared__ double g_logf_tab[16][2];
-constexpr int kBbFloats = 501 * 3;
+constexpr int kBbFloats = kBbLdsRows * 3;
 
 
 struct KernelEnv {
@@ -142,9 +142,16 @@ struct KernelEnv {
     e->v[6] = 0.0f;
   }
   __device__ __forceinline__ LaneCold& cold() { return g_lane_cold[threadIdx.x]; }
-  const float* bb_lds;  // the temperature kernel's LDS copy of S.bb
+  const float* bb_lds;  // the temperature kernel's LDS copy of S.bb's first kBbLdsRows rows
   __device__ __forceinline__ const double (*logf_table() const)[2] { return g_logf_tab; }
-  __device__ __forceinline__ const float* bb_table(const DevScene&) const { return bb_lds; }
+  // blackbody_radiation_xyz from the LDS rows when the grid's temperatures stay in them (a uniform
+  // branch, so each path keeps its own address space: ds_read or global loads, no flat pointer)
+  __device__ __forceinline__ void blackbody(const DevScene& S, float t, float& X, float& Y, float& Z) const {
+    if (S.bb_lds_ok)
+      blackbody_xyz(S, bb_lds, t, X, Y, Z);
+    else
+      blackbody_xyz(S, S.bb, t, X, Y, Z);
+  }
 #ifdef VPT_JOB_LOG
   // diagnostic build: per job (tile, fetch time, end time, hardware id) into the records buffer
   __device__ __forceinline__ void job_done(uint32_t job, uint32_t tile, uint32_t t0) {
@@ -695,6 +702,9 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   vpt::scene_finalize(ctx->scene);  // uses only the density map (host copy of the values)
   ctx->scene.temperature = ctx->temperature.dev;
   ctx->scene.has_temperature = temperature ? 1 : 0;
+  ctx->scene.bb_lds_ok = temperature ? vpt::blackbody_rows_suffice(*temperature, cfg->volume_parameters.temperature_scale,
+                                                                    cfg->volume_parameters.temperature_offset, vpt::kBbLdsRows)
+                                     : 0;
 
   std::vector<float> bb(501 * 3, 0.0f);  // row 500 = 0 (reference reads past its table)
   if (blackbody_500x3)

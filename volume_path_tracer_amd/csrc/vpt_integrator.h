@@ -286,6 +286,7 @@ struct DevScene {
   uint32_t tile_area;
   int32_t wave_lanes;   // lanes of each wavefront that take jobs (64; latency-bound launches: 0 = auto)
   const float* bb;      // blackbody table [501][3] (row 500 = 0)
+  int32_t bb_lds_ok;    // every reachable lookup reads rows < kBbLdsRows: the kernel's LDS copy serves it
   const float* cie;     // [471][3] for T >= 49900 K
   float y_integral;
 };
@@ -336,7 +337,12 @@ __host__ __device__ inline float planck_dev(float lambda_m, float t) {
   float e = expf((h * c) / (lambda_m * kb * t));
   return num / (lambda5 * (e - 1));
 }
-// bb: the blackbody table [501][3] (S.bb, or the kernel's LDS copy).
+// Rows of the blackbody table the temperature kernel copies into LDS (T < 6 300 K): a grid whose
+// temperatures stay below that (host check, vpt_gpu_create: the trilinear value is a convex combination
+// of voxel / tile / background values, so max(v) * scale + offset bounds it) looks every row up there;
+// others read the whole table from memory.  64 rows = 768 B per block instead of 6 KB.
+constexpr int kBbLdsRows = 64;
+// bb: the blackbody table [501][3] (S.bb, or the kernel's LDS copy of its first kBbLdsRows rows).
 __host__ __device__ inline void blackbody_xyz(const DevScene& S, const float* bb, float t, float& X, float& Y, float& Z) {
   if (!(t - t == 0.0f)) {  // !isfinite
     X = Y = Z = __builtin_nanf("");
@@ -546,7 +552,14 @@ __host__ __device__ __forceinline__ void hdda_pre_advance(const DevGrid& g, Lane
   uint32_t w = kWalkSlow;
   if (ln.dim == 8) {
     const uint32_t off = walk_index(g, ln.vox) * 4u;
+#if defined(__HIP_DEVICE_COMPILE__) && defined(VPT_EXP_WALK_SC1)
+    // experiment (VERDICT r02 #5a): the walk word loaded sc1 (device scope: served by L2, no L1
+    // allocation) so the 4-byte words stop evicting the stencils' lines from the 32 KB L1
+    w = __hip_atomic_load(reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(g.walk8) + off), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
+#else
     w = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(g.walk8) + off);
+#endif
   }
   ln.pw = w;
 }
@@ -805,7 +818,7 @@ __host__ __device__ __forceinline__ void primary_event(const DevScene& S, const 
     map_inv(S.temperature, cp[0], cp[1], cp[2], tx, ty, tz);
     env.tally(CNT_TEMP_STENCILS, trilinear(S.temperature, ln.temp_cell, tx, ty, tz, tadim) ? 1 : 0);
     float tK = tadim * S.temp_scale + S.temp_offset;
-    blackbody_xyz(S, env.bb_table(S), tK, X, Y, Z);
+    env.blackbody(S, tK, X, Y, Z);
     float sc = p_a * S.le_scale;
     lc.L[0] = lc.L[0] + sc * X;
     lc.L[1] = lc.L[1] + sc * Y;

@@ -51,6 +51,12 @@ float cie_y_integral();
 
 int default_threads();
 
+// 1 when every blackbody lookup of the temperature grid reads rows < rows of the table: the
+// trilinear value is a convex combination of getValue()s (leaf voxels, tile values, background), so
+// T = value * scale + offset (worker.cpp:152-157) lies between the extremes of those; one row of margin
+// covers the rounding of the lerps and of the two float operations.  0 for non-finite values.
+int blackbody_rows_suffice(const vpt_grid_desc& t, float scale, float offset, int rows);
+
 // A vpt_grid_desc that owns its arrays (vpt_synth_grid, vpt_grid_from_nanovdb, vpt_grid_read_nvdb;
 // released by vpt_synth_free / vpt_grid_free).  d must stay the first member.
 struct OwnedGrid {

@@ -3,6 +3,7 @@
 // Everything here runs once per context on the host, with the reference's float formulas and
 // operation order (Eigen fixed-size products/reductions restated as a0*b0 + (a1*b1 + a2*b2)),
 // so the device integrator receives bit-identical constants.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <thread>
@@ -171,6 +172,25 @@ extern "C" int vpt_blackbody_table(float* out) {
   vpt::blackbody_table(out);
   return VPT_OK;
 }
+
+namespace vpt {
+int blackbody_rows_suffice(const vpt_grid_desc& t, float scale, float offset, int rows) {
+  float lo = t.background, hi = t.background;
+  auto take = [&](float v) {
+    lo = std::min(lo, v);
+    hi = std::max(hi, v);
+    return std::isfinite(v);
+  };
+  if (!take(t.background)) return 0;
+  for (uint64_t i = 0; i < t.leaf_count * 512; ++i)
+    if (!take(t.leaf_values[i])) return 0;
+  for (uint64_t i = 0; i < t.tile_count; ++i)
+    if (!take(t.tile_value[i])) return 0;
+  const float tmax = std::max(lo * scale, hi * scale) + offset;
+  // rows dn and dn + 1 with dn <= floor(T / 100) + 1 (the search loops of blackbody_xyz), plus margin
+  return std::isfinite(tmax) && tmax < (float)(rows - 3) * 100.0f ? 1 : 0;
+}
+}  // namespace vpt
 
 extern "C" int vpt_blackbody_xyz(const float* table, float t, float* out) {
   if (!table || !out) return vpt::set_error(VPT_E_INVALID, "vpt_blackbody_xyz: null argument");
