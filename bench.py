@@ -137,6 +137,36 @@ def spawn_ranks(args) -> int:
     return subprocess.run(cmd).returncode
 
 
+def newest_profile(pattern: str, match=lambda j: True):
+    """(json, 'profiles/<name>') of the newest committed profiles/<pattern> that matches, or (None, None)."""
+    for pf in sorted((ROOT / "profiles").glob(pattern), reverse=True):
+        try:
+            j = json.loads(pf.read_text())
+        except Exception:
+            continue
+        if match(j):
+            return j, f"profiles/{pf.name}"
+    return None, None
+
+
+def request_roofline(config: str, samples_per_launch: float, avg_launch_s: float, cus: int) -> dict:
+    """The binding limit of the walk: L1->L2 read requests per second per CU against the
+    measured ceiling of divergent 4-byte per-lane gathers from an L2-resident table
+    (tools/ubench/gather.hip).  Requests per sample come from the newest committed rocprofv3 counter
+    pass of this config (tools/kernel_counters.sh) -- builder measurements, named in the line --
+    times this run's samples per launch over this run's average launch time."""
+    cnt, cnt_src = newest_profile("*_counters.json", lambda j: j.get("config") == config and
+                                  j.get("derived", {}).get("l1_to_l2_requests_per_sample"))
+    ceil, ceil_src = newest_profile("*_gather_ceiling.json")
+    if not cnt or not ceil:
+        return {"request_frac": None}
+    achieved = cnt["derived"]["l1_to_l2_requests_per_sample"] * samples_per_launch / avg_launch_s / cus
+    peak = ceil["ceiling_l1_to_l2_requests_per_s_per_cu"]
+    return {"request_frac": round(achieved / peak, 4),
+            "request_achieved_per_s_per_cu": round(achieved, 1), "request_peak_per_s_per_cu": round(peak, 1),
+            "request_sources": [cnt_src, ceil_src]}
+
+
 def init_rank(args, env=None):
     """(rank, world, device, scalar device) of this process.  One process per GPU: device LOCAL_RANK
     (device 0 for --one-device, the one-GPU multi-process tests).  For world > 1 the process group is
@@ -323,18 +353,12 @@ def main():
         avg_launch_s = sum(kernel_ms) / len(kernel_ms) / 1e3 / launches_per_step
         bytes_per_launch = algorithmic_bytes(counters) / (args.steps * launches_per_step)
         achieved = bytes_per_launch / avg_launch_s / 1e9
-        traffic, traffic_source = None, None
         # PMC-measured HBM bytes of this workload from the newest committed rocprofv3 pass
         # (tools/profile_round.sh): a builder measurement, labelled with its file, not this run's
-        for pf in sorted((ROOT / "profiles").glob("*_pmc.json"), reverse=True):
-            try:
-                pj = json.loads(pf.read_text())
-            except Exception:
-                continue
-            if pj.get("config") == args.config and pj.get("spp") == spp:
-                traffic = pj.get("hbm_bytes_per_launch")
-                traffic_source = f"profiles/{pf.name}"
-                break
+        pj, traffic_source = newest_profile("*_pmc.json", lambda j: j.get("config") == args.config and j.get("spp") == spp)
+        traffic = pj.get("hbm_bytes_per_launch") if pj else None
+        req = request_roofline(args.config, samples_rank / (args.steps * launches_per_step), avg_launch_s,
+                               torch.cuda.get_device_properties(dev).multi_processor_count)
         out = {
             "metric": baseline_metric(),
             "value": round(value, 3),
@@ -362,7 +386,7 @@ def main():
                          "traffic_source": traffic_source,
                          "kernel": "vpt_integrate_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                          "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                         "bytes_per_sample": round(algorithmic_bytes(counters) / samples_rank, 2)},
+                         "bytes_per_sample": round(algorithmic_bytes(counters) / samples_rank, 2), **req},
             # the production kernel counts the events that price algorithmic bytes
             "counters_per_sample": {k: round(counters[k] / samples_rank, 3)
                                     for k in ("dda_steps", "stencils", "temp_stencils")},

@@ -10,6 +10,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CHECK(x)                                                                              \
@@ -22,10 +23,12 @@
   } while (0)
 
 template <int Chains>
-__global__ __launch_bounds__(256) void chase(const uint32_t* __restrict__ t, uint32_t n, int iters, uint32_t* out) {
+__global__ __launch_bounds__(256) void chase(const uint32_t* __restrict__ t, uint32_t n, int iters, uint32_t* out,
+                                             int active) {
   extern __shared__ uint32_t occupancy_lds[];  // only sizes the block (waves per SIMD)
   uint32_t idx[Chains];
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if ((int)(threadIdx.x & 63) >= active) return;  // lanes of a wavefront that load (the rest idle)
 #pragma unroll
   for (int c = 0; c < Chains; ++c) idx[c] = (g * 2654435761u + c * 40503u) % n;
   for (int i = 0; i < iters; ++i) {
@@ -39,7 +42,7 @@ __global__ __launch_bounds__(256) void chase(const uint32_t* __restrict__ t, uin
 }
 
 template <int Chains>
-double run(const uint32_t* t, uint32_t n, int waves, int cus, uint32_t* out, size_t lds_total) {
+double run(const uint32_t* t, uint32_t n, int waves, int cus, uint32_t* out, size_t lds_total, int active = 64) {
   const int blocks = cus * waves;  // 256 threads = 4 waves per block, one per SIMD
   const size_t lds = lds_total / waves - 1024;
   const int iters = 512;
@@ -47,16 +50,16 @@ double run(const uint32_t* t, uint32_t n, int waves, int cus, uint32_t* out, siz
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  hipLaunchKernelGGL(chase<Chains>, dim3(blocks), dim3(256), lds, 0, t, n, iters, out);
+  hipLaunchKernelGGL(chase<Chains>, dim3(blocks), dim3(256), lds, 0, t, n, iters, out, active);
   CHECK(hipEventRecord(e0));
-  hipLaunchKernelGGL(chase<Chains>, dim3(blocks), dim3(256), lds, 0, t, n, iters, out);
+  hipLaunchKernelGGL(chase<Chains>, dim3(blocks), dim3(256), lds, 0, t, n, iters, out, active);
   CHECK(hipEventRecord(e1));
   CHECK(hipEventSynchronize(e1));
   CHECK(hipGetLastError());
   float ms = 0;
   CHECK(hipEventElapsedTime(&ms, e0, e1));
-  const double loads = (double)blocks * 256 * iters * Chains;
-  return loads / (ms * 1e-3) / cus;  // loads per second per CU
+  const double loads = (double)blocks * 4 * active * iters * Chains;
+  return loads / (ms * 1e-3) / cus;  // lane loads per second per CU
 }
 
 int main(int argc, char** argv) {
@@ -65,6 +68,7 @@ int main(int argc, char** argv) {
   const size_t lds_total = 160 * 1024;
   uint32_t* out;
   CHECK(hipMalloc(&out, 4));
+  const bool calib = argc > 1 && std::string(argv[1]) == "calib";  // one config, for a --pmc pass
   const size_t sizes[] = {307200, 1u << 22, 1u << 26};  // 1.2 MiB (L2), 16 MiB (MALL), 256 MiB (HBM)
   std::printf("gather ceiling: %d CUs, divergent 4-B loads, loads/s per CU (G)\n", cus);
   std::printf("%10s %6s %6s %10s\n", "table_MiB", "chains", "waves", "Gload/s/CU");
@@ -80,10 +84,24 @@ int main(int argc, char** argv) {
     uint32_t* t;
     CHECK(hipMalloc(&t, n * 4));
     CHECK(hipMemcpy(t, h.data(), n * 4, hipMemcpyHostToDevice));
+    if (calib) {  // 2 launches of chase<2>, 7 waves, 64 lanes: lane loads per launch below
+      const double r = run<2>(t, (uint32_t)n, 7, cus, out, lds_total);
+      std::printf("calib lane_loads_per_launch %.0f Gload/s/CU %.4f\n", (double)cus * 7 * 256 * 512 * 2, r * 1e-9);
+      return 0;
+    }
     for (int waves : {1, 2, 4, 7, 8}) {
       std::printf("%10.2f %6d %6d %10.4f\n", n * 4.0 / (1 << 20), 1, waves, run<1>(t, (uint32_t)n, waves, cus, out, lds_total) * 1e-9);
       std::printf("%10.2f %6d %6d %10.4f\n", n * 4.0 / (1 << 20), 2, waves, run<2>(t, (uint32_t)n, waves, cus, out, lds_total) * 1e-9);
       std::printf("%10.2f %6d %6d %10.4f\n", n * 4.0 / (1 << 20), 4, waves, run<4>(t, (uint32_t)n, waves, cus, out, lds_total) * 1e-9);
+    }
+    if (n == sizes[0]) {
+      // Partly active wavefronts (a divergent walk keeps ~31 of 64 lanes walking): is the ceiling per
+      // lane (line) or per wave instruction?  Lane loads/s and wave instructions/s per CU.
+      std::printf("%10s %6s %6s %6s %10s %12s\n", "table_MiB", "chains", "waves", "active", "Gload/s/CU", "Ginst/s/CU");
+      for (int act : {64, 48, 32, 16, 8, 1}) {
+        const double r = run<2>(t, (uint32_t)n, 7, cus, out, lds_total, act);
+        std::printf("%10.2f %6d %6d %6d %10.4f %12.4f\n", n * 4.0 / (1 << 20), 2, 7, act, r * 1e-9, r / act * 1e-9);
+      }
     }
     CHECK(hipFree(t));
   }
