@@ -552,14 +552,7 @@ __host__ __device__ __forceinline__ void hdda_pre_advance(const DevGrid& g, Lane
   uint32_t w = kWalkSlow;
   if (ln.dim == 8) {
     const uint32_t off = walk_index(g, ln.vox) * 4u;
-#if defined(__HIP_DEVICE_COMPILE__) && defined(VPT_EXP_WALK_SC1)
-    // experiment (VERDICT r02 #5a): the walk word loaded sc1 (device scope: served by L2, no L1
-    // allocation) so the 4-byte words stop evicting the stencils' lines from the 32 KB L1
-    w = __hip_atomic_load(reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(g.walk8) + off), __ATOMIC_RELAXED,
-                          __HIP_MEMORY_SCOPE_AGENT);
-#else
     w = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(g.walk8) + off);
-#endif
   }
   ln.pw = w;
 }
