@@ -369,7 +369,8 @@ def test_temperature_kernel_blackbody_from_memory_above_the_lds_rows():
 def test_drain_gates_keep_films_bit_exact():
     """The drain-gate kernel variant (vpt_gpu_set_drain_gates): wavefronts switch to their own gates once
     they start draining.  On a 16-block grid, 4 waves of a 160x120 frame (1 200 jobs: above the latency
-    threshold, below 4 items per lane) run the variant; each wave's film is bit-exact vs the oracle."""
+    threshold, below 4 items per lane) run the variant; the film equals the oracle's (counts exactly, XYZ to
+    fp32 atomic-order rounding) and the counters agree."""
     from volume_path_tracer_amd.render import Integrator
 
     wl = workload("c3", width=160, height=120, spp=4, grid_n=64)
