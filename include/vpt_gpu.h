@@ -331,14 +331,6 @@ int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_b
  * gate_eval: <= 0) to keep a value; gate_idle 0 is rejected. */
 int vpt_gpu_set_latency_tuning(vpt_gpu_ctx* ctx, int wave_lanes, int gate_min, int gate_idle, int gate_eval,
                                int gate_walk);
-/* Drain gates: in launches of at most max_items_per_lane work items per resident lane (0 = off, the
- * default), a wavefront that has started to drain (one of its lanes found the job range empty) runs
- * with these gates instead of the launch's (meaning as in vpt_gpu_set_tuning; defaults 1, 65, 1, 1:
- * every block runs as soon as one lane needs it).  For small per-GPU shares of a frame, whose last
- * jobs set the launch time.  Results never depend on them.  Pass <= 0 (gate_idle, gate_walk < 0) to
- * keep a gate; gate_idle 0 is rejected. */
-int vpt_gpu_set_drain_gates(vpt_gpu_ctx* ctx, int max_items_per_lane, int gate_min, int gate_idle, int gate_eval,
-                            int gate_walk);
 /* SIMT-utilisation profile of profiling builds (-DVPT_PROFILE): for each block of the lane state
  * machine, [wave executions, active lanes] as 2*21 uint64 (the last 7: lanes per state at each walk-loop iteration), then the shader cycles the wavefronts
  * spent in each of 10 sections (fetch, pixel, ray, walk-loop control, eval, nee, finish, and the

@@ -365,29 +365,3 @@ def test_temperature_kernel_blackbody_from_memory_above_the_lds_rows():
         _assert_bitwise(_prod_film(it, (wave - 1) * T, T), f_o, f"wave {wave}")
     assert c_o["temp_stencils"] > 0
 
-
-def test_drain_gates_keep_films_bit_exact():
-    """The drain-gate kernel variant (vpt_gpu_set_drain_gates): wavefronts switch to their own gates once
-    they start draining.  On a 16-block grid, 4 waves of a 160x120 frame (1 200 jobs: above the latency
-    threshold, below 4 items per lane) run the variant; the film equals the oracle's (counts exactly, XYZ to
-    fp32 atomic-order rounding) and the counters agree."""
-    from volume_path_tracer_amd.render import Integrator
-
-    wl = workload("c3", width=160, height=120, spp=4, grid_n=64)
-    dens, temp = _grids(wl)
-    it = Integrator(wl.cfg, dens, temp, device=0)
-    it.set_tuning(grid_blocks=16)
-    od, ot = _oracle_grids(dens, temp)
-    T = wl.cfg.jobs_per_wave()
-    for gates in ((4, 1, 65, 1, 1), (4, 2, 16, 8, 2)):
-        it.set_drain_gates(*gates)
-        it.counters(reset=True)
-        f_g = _prod_film(it, 0, 4 * T)
-        f_o, _, c_o = O.render_jobs(wl.cfg, od, ot, 0, 4 * T)
-        np.testing.assert_array_equal(f_g[..., 3], 4.0)
-        np.testing.assert_allclose(f_g[..., :3], f_o[..., :3], rtol=1e-5, atol=1e-6)
-        c = it.counters()
-        for k in COUNTERS:
-            assert c[k] == c_o[k], (gates, k)
-    with pytest.raises(RuntimeError):
-        it.set_drain_gates(4, 1, 0, 1, 1)  # gate_idle 0 could stall a wavefront: rejected

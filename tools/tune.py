@@ -36,9 +36,6 @@ PRESETS = {
     "small-launch": [["--config", "c2", "--spp", "64", "--gates", "6:8:36:4", "--blocks", "512,640,768,1024,1280", "--reps", "2"],
                      ["--config", "c1", "--spp", "4", "--gates", "6:8:36:4", "--blocks", "1792",
                       "--lat", "0:1:65:1:1,0:1:65:2:1,0:1:65:1:2,0:1:65:4:1,0:1:65:1:4,0:2:65:1:1", "--reps", "3"]],
-    # drain gates for small per-GPU shares of a frame (C3 at 32 / 64 / 256 waves: the 8 / 4 / 1-GPU share)
-    "drain": [["--config", "c3", "--spp", str(sp), "--gates", "6:8:36:4", "--reps", "3",
-               "--drain", "0,4:1:65:1:1,4:2:16:8:2,4:6:65:36:4,4:1:65:36:4"] for sp in (32, 64, 256)],
     # the full-occupancy gates of the C3 / C4 frames
     "gates": [["--config", c, "--spp", "32", "--gates", "6:8:36:4,4:8:36:4,8:8:36:4,6:12:36:4,6:8:32:4,6:8:40:4,6:8:36:2,6:8:36:8",
                "--reps", "2"] for c in ("c3", "c4")],
@@ -54,7 +51,6 @@ def parser():
     ap.add_argument("--blocks", default="0")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--lat", default="", help="latency-launch knobs wave_lanes:gate_min:gate_idle:gate_eval:gate_walk, comma-separated")
-    ap.add_argument("--drain", default="", help="drain gates max_items_per_lane:gate_min:gate_idle:gate_eval:gate_walk, comma-separated ('0' = off)")
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--rng-mode", default="reference")
     ap.add_argument("--order", type=int, default=-1, help="job order mode (-1: library default)")
@@ -92,13 +88,10 @@ def sweep(a):
         gm, gi = parts[0], parts[1]
         ge = parts[2] if len(parts) > 2 else 1
         gw = parts[3] if len(parts) > 3 else 0
-        for b, lat, dr in [(b, l, d) for b in map(int, a.blocks.split(",")) for l in (a.lat.split(",") if a.lat else [""])
-                           for d in (a.drain.split(",") if a.drain else [""])]:
+        for b, lat in [(b, l) for b in map(int, a.blocks.split(",")) for l in (a.lat.split(",") if a.lat else [""])]:
             it.set_tuning(gm, gi, b if b > 0 else base_blocks, ge, gw)
             if lat:
                 it.set_latency_tuning(*map(int, lat.split(":")))
-            if dr:
-                it.set_drain_gates(*map(int, dr.split(":")))
             best = 1e9
             for _ in range(a.reps):
                 it.film.zero_()
@@ -110,7 +103,7 @@ def sweep(a):
             if a.profile:
                 print(json.dumps({"gate": g, "profile": it.profile(reset=True)}), flush=True)
             print(json.dumps({"lib": os.environ.get("VPT_LIB", "default"), "config": a.config, "order": a.order, "tail": a.tail,
-                              "gate": g, "lat": lat, "drain": dr, "blocks": b or base_blocks, "spp": a.spp, "ms": round(best * 1e3, 2),
+                              "gate": g, "lat": lat, "blocks": b or base_blocks, "spp": a.spp, "ms": round(best * 1e3, 2),
                               "Msps": round(wl.cfg.width * wl.cfg.height * a.spp / best / 1e6, 2)}), flush=True)
     del it
 

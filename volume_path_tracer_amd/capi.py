@@ -226,7 +226,6 @@ def lib() -> C.CDLL:
     if hasattr(L, "vpt_gpu_set_latency_tuning"):  # (older builds in A/B runs lack it)
         L.vpt_gpu_set_latency_tuning.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
     L.vpt_gpu_launch_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
-    L.vpt_gpu_set_drain_gates.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
     L.vpt_last_error.restype = C.c_char_p
     L.vpt_synth_grid.argtypes = [C.c_int, C.c_int]
     L.vpt_synth_grid.restype = gridp

@@ -63,7 +63,6 @@ constexpr int kBbFloats = kBbLdsRows * 3;
 struct KernelEnv {
   uint64_t jid_begin;
   uint64_t jid_count;
-  const DevScene* drain_scene;  // gates of a draining wavefront (nullptr: the launch's throughout)
   unsigned long long* job_counter;
   float* film;
   float* records;
@@ -208,7 +207,7 @@ struct KernelEnv {
 };
 
 // counters[] order = vpt_counters field order
-template <bool HasTemp, bool Debug, bool Runs, bool Drain = false>
+template <bool HasTemp, bool Debug, bool Runs>
 __global__ __launch_bounds__(kBlockThreads, Debug ? VPT_WAVES_SLOW : (HasTemp ? VPT_WAVES_TEMP : VPT_WAVES_FAST)) void vpt_integrate_kernel(const DevScene* scene, KernelEnv env,
                                                                        unsigned long long* counters) {
   __shared__ unsigned long long wg_counters[kCounterCount];
@@ -233,15 +232,7 @@ __global__ __launch_bounds__(kBlockThreads, Debug ? VPT_WAVES_SLOW : (HasTemp ? 
   lane_init(ln);
   cold_init(env.cold());
   const ScenePtr sp = (ScenePtr)scene;
-  if (Drain) {
-    // Drain gates (vpt_gpu_set_drain_gates; a kernel variant of its own, so the other launches pay
-    // nothing): once a lane of the wavefront has found the job range empty (it left the loop), the
-    // wavefront runs with the drain scene's gates.
-    const ScenePtr dp = (ScenePtr)env.drain_scene;
-    while (ln.state != ST_DONE) lane_iteration<HasTemp, Debug, Runs>(env.count(true) < 64 ? dp : sp, ln, env);
-  } else {
-    while (ln.state != ST_DONE) lane_iteration<HasTemp, Debug, Runs>(sp, ln, env);
-  }
+  while (ln.state != ST_DONE) lane_iteration<HasTemp, Debug, Runs>(sp, ln, env);
   atomicAdd(wg_counters + CNT_DDA_STEPS, (unsigned long long)ln.n_dda);
   __syncthreads();
   if (threadIdx.x < kCounterCount && wg_counters[threadIdx.x])
@@ -437,11 +428,6 @@ struct vpt_gpu_ctx {
   vpt::DevScene* scene_lat_dev = nullptr;
   int lat_gate[4] = {1, 65, 1, 1};   // gate_min, gate_idle, gate_eval, gate_walk
   int lat_wave_lanes = 0;            // 0: spread the items evenly over the grid's wavefronts
-  // Drain gates (vpt_gpu_set_drain_gates): a third copy of the scene whose gates a wavefront uses once
-  // it has started to drain, in launches of at most drain_items work items per resident lane.
-  vpt::DevScene* scene_drain_dev = nullptr;
-  int drain_gate[4] = {1, 65, 1, 1};
-  uint64_t drain_items = 0;
   hipStream_t stream = nullptr;
   bool use_runs = false;             // density-only kernel variant with run skipping (see create)
   int grid_blocks = 0;               // resident capacity (or the set_tuning override)
@@ -480,12 +466,6 @@ int push_scene(vpt_gpu_ctx* ctx) {
   lat.wave_lanes = ctx->lat_wave_lanes;
   VPT_HIP(hipMemcpyAsync(ctx->scene_dev, &ctx->scene, sizeof(vpt::DevScene), hipMemcpyHostToDevice, ctx->stream));
   VPT_HIP(hipMemcpyAsync(ctx->scene_lat_dev, &lat, sizeof(vpt::DevScene), hipMemcpyHostToDevice, ctx->stream));
-  vpt::DevScene drain = ctx->scene;
-  drain.gate_min = ctx->drain_gate[0];
-  drain.gate_idle = ctx->drain_gate[1];
-  drain.gate_eval = ctx->drain_gate[2];
-  drain.gate_walk = ctx->drain_gate[3];
-  VPT_HIP(hipMemcpyAsync(ctx->scene_drain_dev, &drain, sizeof(vpt::DevScene), hipMemcpyHostToDevice, ctx->stream));
   VPT_HIP(hipStreamSynchronize(ctx->stream));
   return VPT_OK;
 }
@@ -542,7 +522,6 @@ void destroy(vpt_gpu_ctx* ctx) {
   (void)hipFree(ctx->prof);
   (void)hipFree(ctx->scene_dev);
   (void)hipFree(ctx->scene_lat_dev);
-  (void)hipFree(ctx->scene_drain_dev);
   (void)hipFree(ctx->order);
   (void)hipFree(ctx->perm);
   for (uint32_t i = 0; i < kLaunchSlots; ++i)
@@ -604,7 +583,6 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   }
   env.film = film ? film : ctx->film;
   env.records = records;
-  env.drain_scene = nullptr;
   env.tile_area = ctx->scene.tw * ctx->scene.th;
   env.prof_buf = ctx->prof;
   env.order = nullptr;
@@ -663,12 +641,6 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
                      : ctx->use_runs
                          ? (dbg ? vpt::vpt_integrate_kernel<false, true, true> : vpt::vpt_integrate_kernel<false, false, true>)
                          : (dbg ? vpt::vpt_integrate_kernel<false, true, false> : vpt::vpt_integrate_kernel<false, false, false>);
-  // drain gates: density-only production launches of at most drain_items work items per resident lane
-  if (!temp && !dbg && !ctx->use_runs && !latency && ctx->drain_items > 0 &&
-      env.jid_count <= ctx->drain_items * (uint64_t)blocks * vpt::kBlockThreads) {
-    env.drain_scene = ctx->scene_drain_dev;
-    kernel = vpt::vpt_integrate_kernel<false, false, false, true>;
-  }
   hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, latency ? ctx->scene_lat_dev : ctx->scene_dev,
                      env, ctx->counters);
   VPT_HIP(hipGetLastError());
@@ -781,7 +753,6 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   ctx->scene.tile_area = (uint32_t)(ctx->scene.tw * ctx->scene.th);
   VPT_HIP(hipMalloc((void**)&ctx->scene_dev, sizeof(vpt::DevScene)));
   VPT_HIP(hipMalloc((void**)&ctx->scene_lat_dev, sizeof(vpt::DevScene)));
-  VPT_HIP(hipMalloc((void**)&ctx->scene_drain_dev, sizeof(vpt::DevScene)));
   if ((rc = push_scene(ctx.get()))) return rc;
   *out = ctx.release();
   return VPT_OK;
@@ -1011,21 +982,6 @@ int vpt_gpu_set_latency_tuning(vpt_gpu_ctx* ctx, int wave_lanes, int gate_min, i
   if (gate_idle >= 0) ctx->lat_gate[1] = gate_idle;
   if (gate_eval > 0) ctx->lat_gate[2] = gate_eval;
   if (gate_walk >= 0) ctx->lat_gate[3] = gate_walk;
-  return push_scene(ctx);
-}
-
-int vpt_gpu_set_drain_gates(vpt_gpu_ctx* ctx, int max_items_per_lane, int gate_min, int gate_idle, int gate_eval,
-                            int gate_walk) {
-  if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
-  if (max_items_per_lane < 0) return vpt::set_error(VPT_E_INVALID, "max_items_per_lane must be >= 0");
-  if (gate_idle == 0) return vpt::set_error(VPT_E_INVALID, "gate_idle must be >= 1 (0 can stall a wavefront)");
-  int rc = ctx_device(ctx);
-  if (rc) return rc;
-  ctx->drain_items = (uint64_t)max_items_per_lane;
-  if (gate_min > 0) ctx->drain_gate[0] = gate_min;
-  if (gate_idle >= 0) ctx->drain_gate[1] = gate_idle;
-  if (gate_eval > 0) ctx->drain_gate[2] = gate_eval;
-  if (gate_walk >= 0) ctx->drain_gate[3] = gate_walk;
   return push_scene(ctx);
 }
 

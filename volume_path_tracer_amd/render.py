@@ -242,13 +242,6 @@ class Integrator:
         capi.check(capi.lib().vpt_gpu_set_latency_tuning(self.h, wave_lanes, gate_min, gate_idle, gate_eval, gate_walk),
                    "vpt_gpu_set_latency_tuning")
 
-    def set_drain_gates(self, max_items_per_lane: int, gate_min: int = 0, gate_idle: int = -1, gate_eval: int = 0,
-                        gate_walk: int = -1):
-        """Gates of draining wavefronts in launches of at most max_items_per_lane items per resident lane
-        (0 = off); see include/vpt_gpu.h."""
-        capi.check(capi.lib().vpt_gpu_set_drain_gates(self.h, max_items_per_lane, gate_min, gate_idle, gate_eval,
-                                                       gate_walk), "vpt_gpu_set_drain_gates")
-
     PROFILE_BLOCKS = ["iter", "fetch", "pixel", "ray", "sample", "need_seg", "step", "draw", "trilinear",
                       "event", "shadow_hit", "none", "nee_done", "finish",
                       "w_walk", "w_eval", "w_nee", "w_finish", "w_ray", "w_pixel", "w_done"]
