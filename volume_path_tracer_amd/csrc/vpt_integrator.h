@@ -809,7 +809,12 @@ __host__ __device__ __forceinline__ void primary_event(const DevScene& S, const 
   if (HasTemp) {
     float tx, ty, tz, tadim, X, Y, Z;
     map_inv(S.temperature, cp[0], cp[1], cp[2], tx, ty, tz);
+#ifdef VPT_EXP_TEMP_NOCACHE
+    StencilCell tc{kNoCell, 0, 0, -1};
+    env.tally(CNT_TEMP_STENCILS, trilinear(S.temperature, tc, tx, ty, tz, tadim) ? 1 : 0);
+#else
     env.tally(CNT_TEMP_STENCILS, trilinear(S.temperature, ln.temp_cell, tx, ty, tz, tadim) ? 1 : 0);
+#endif
     float tK = tadim * S.temp_scale + S.temp_offset;
     env.blackbody(S, tK, X, Y, Z);
     float sc = p_a * S.le_scale;
