@@ -589,12 +589,16 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.perm = nullptr;
   env.order_tail_k0 = 0;
   env.order_tail_n = 0;
-  // Fewer work items than resident lanes (small frames, few waves): a launch lasts as long as its
-  // slowest job, and a job's lane runs faster with fewer waves per SIMD, so the grid is sized to ~2
-  // items per lane in whole blocks per CU (at least one).  C2 (262 144 jobs, r02g sweep,
-  // profiles/r02g_c2_grid_sweep.txt): 1 / 1.5 / 1.75 / 2 / 2.5 / 3 / 4 / 5 blocks per CU 167.7 /
-  // 124.4 / 112.9 / 98.7-99.3 / 104.4 / 104.5-105.3 / 106.7 / 109.9 ms (the r01 rule, ~4/3 items per
-  // lane, gave 3).  Same jobs, same samples.
+  // Partly filled launches (a few work items per resident lane: small frames, few waves, a GPU's share
+  // of a frame dealt over several): a launch lasts as long as its slowest jobs, and a job's lane runs
+  // faster with fewer waves per SIMD, so the grid is sized to round(1 + 1.8 x) blocks per CU (at most
+  // the resident capacity), x = items per resident lane.  Same jobs, same samples.  Measured (r03h,
+  // profiles/r03h_grid_sweep.txt; C3 frames of spp waves, 4 / 5 / 6 / 7 blocks per CU, ms): spp 16
+  // (x 1.1) 54.5 / 55.0 / 55.4 / 57.5 (3: 51.5); spp 24 (x 1.7) 57.3 / 61.0 / 64.7 / 65.7; spp 32
+  // (x 2.3, the 8-GPU share) 70.4 / 66.9 / 67.5 / 71.2; spp 48 (x 3.4) 92.2 / 90.8 / 89.7 / 87.9; from
+  // spp 96 on (and C5's shares) the full grid is best.  C2 (262 144 jobs, x 0.57 -> 2 blocks per CU,
+  // r02g: 1 / 1.5 / 1.75 / 2 / 2.5 / 3 / 4 / 5 blocks per CU 167.7 / 124.4 / 112.9 / 98.7-99.3 / 104.4 /
+  // 104.5-105.3 / 106.7 / 109.9 ms).  (r02's rule, ~2 items per lane, gave 7 blocks from x 1.9 on.)
   uint32_t blocks = (uint32_t)ctx->grid_blocks;
   // Latency-bound launch (at most kSpreadLanes items per wavefront of the grid, e.g. C1's 4 096 jobs):
   // the launch lasts as long as its slowest job, and a job runs fastest on a wavefront with few other
@@ -604,8 +608,10 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   // lanes) -> 20.5 ms (1 792 blocks, one lane per wavefront, gates 1:65:1:1).  Same jobs, same samples.
   const bool latency = env.jid_count <= kSpreadLanes * ((uint64_t)blocks * (vpt::kBlockThreads / 64));
   if (!ctx->grid_user && !latency) {
-    const uint64_t cus = (uint64_t)ctx->cus, per_cu = (env.jid_count + cus * vpt::kBlockThreads) / (2 * cus * vpt::kBlockThreads);
-    blocks = (uint32_t)std::min<uint64_t>(blocks, cus * std::max<uint64_t>(per_cu, 1));
+    const uint64_t cus = (uint64_t)ctx->cus, resident_per_cu = std::max<uint64_t>(1, blocks / cus);
+    const double x = (double)env.jid_count / ((double)blocks * vpt::kBlockThreads);  // items per resident lane
+    const uint64_t per_cu = std::min<uint64_t>(resident_per_cu, (uint64_t)std::max(1.0, std::floor(1.5 + 1.8 * x)));
+    blocks = (uint32_t)std::min<uint64_t>(blocks, cus * per_cu);
   }
   const uint64_t T = ctx->scene.T;
   if (ctx->order_mode != VPT_ORDER_JID && jid_begin % T == 0 && jid_count % T == 0 && jid_count < (1ULL << 32)) {
