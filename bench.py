@@ -283,6 +283,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3")
     ap.add_argument("--spp", type=int, default=None, help="override waves per step (default: the config's)")
+    ap.add_argument("--grid-n", type=int, default=None, help="experiments: override the stand-in grid's size n^3")
     ap.add_argument("--mode", choices=["weak", "strong"], default="weak",
                     help="weak: each rank renders its own spp waves; strong: the spp waves are dealt across ranks")
     ap.add_argument("--strong-configs", default="c3,c5",
@@ -313,7 +314,7 @@ def main():
     from volume_path_tracer_amd.render import Integrator
     from volume_path_tracer_amd.scenes import SynthGrid, workload
 
-    wl = workload(args.config, spp=args.spp)
+    wl = workload(args.config, spp=args.spp, grid_n=args.grid_n)
     t0 = time.time()
     dg = SynthGrid(wl.density_kind, wl.grid_n)
     tg = SynthGrid(2, wl.grid_n) if wl.temperature else None
