@@ -187,10 +187,10 @@ typedef struct vpt_counters {
  * NULL (volume_grids.cpp:61-66).  `blackbody_500x3` may be NULL: the table is then computed
  * with vpt_blackbody_table().  The density grid's leaf maxima are fixed for interpolation
  * here (Volume::Volume, volume.cpp:162-170) — passing already-fixed maxima is harmless.
- * Device memory per grid: 16 KiB per leaf (the stencil-major brick pool: every voxel's 2x2x2 stencil)
+ * Device memory per grid: 9 KiB per leaf (the stencil pool: per voxel row the 2x2 squares of x = 0..8)
  * plus the cell tables (~12 B per 8^3 cell of the lower nodes' bounding box); the host holds the same
  * while building.  A grid that does not fit the device's free memory is VPT_E_NOMEM before any
- * allocation (e.g. 1.5 GB for the 512^3 cloud stand-in's 90 704 leaves). */
+ * allocation (e.g. 0.84 GB for the 512^3 cloud stand-in's 90 704 leaves). */
 int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density,
                    const vpt_grid_desc* temperature, const float* blackbody_500x3, int device,
                    vpt_gpu_ctx** out);

@@ -4,7 +4,7 @@
 // so a wavefront keeps Chains divergent loads in flight; occupancy is set with dynamic LDS.  Reports
 // loads/s per CU for table sizes from L2-resident (1.2 MiB, the C3 walk table) to HBM-resident, and
 // the memory-level parallelism (chains x waves/SIMD) the request rate saturates at.
-//   hipcc -O3 --offload-arch=gfx950 -o gather gather.hip && ./gather
+//   hipcc -O3 --offload-arch=gfx950 -o gather gather.hip && ./gather [calib | width]
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -41,6 +41,97 @@ __global__ __launch_bounds__(256) void chase(const uint32_t* __restrict__ t, uin
   if (r == 0xFFFFFFFFu) out[0] = r + occupancy_lds[0];
 }
 
+// Wide gathers (the `width` mode): each lane loads one W-dword entry per step (W = 1, 2, 4, or 8 as two
+// adjacent dwordx4 loads -- the stencil's 32-B piece), entries W*4-byte aligned; word 0 holds the next
+// entry, the others zero, and the sum keeps every loaded dword live.
+template <int W>
+struct Entry;
+template <>
+struct Entry<1> {
+  static __device__ __forceinline__ uint32_t next(const uint32_t* t, uint32_t i) { return t[i]; }
+};
+template <>
+struct Entry<2> {
+  static __device__ __forceinline__ uint32_t next(const uint32_t* t, uint32_t i) {
+    const uint2 v = reinterpret_cast<const uint2*>(t)[i];
+    return v.x + v.y;
+  }
+};
+template <>
+struct Entry<4> {
+  static __device__ __forceinline__ uint32_t next(const uint32_t* t, uint32_t i) {
+    const uint4 v = reinterpret_cast<const uint4*>(t)[i];
+    return v.x + v.y + v.z + v.w;
+  }
+};
+template <>
+struct Entry<8> {
+  static __device__ __forceinline__ uint32_t next(const uint32_t* t, uint32_t i) {
+    const uint4 a = reinterpret_cast<const uint4*>(t)[2 * i], b = reinterpret_cast<const uint4*>(t)[2 * i + 1];
+    return (a.x + a.y + a.z + a.w) + (b.x + b.y + b.z + b.w);
+  }
+};
+
+template <int Chains, int W>
+__global__ __launch_bounds__(256) void chase_wide(const uint32_t* __restrict__ t, uint32_t n, int iters, uint32_t* out) {
+  extern __shared__ uint32_t occupancy_lds[];
+  uint32_t idx[Chains];
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+#pragma unroll
+  for (int c = 0; c < Chains; ++c) idx[c] = (g * 2654435761u + c * 40503u) % n;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int c = 0; c < Chains; ++c) idx[c] = Entry<W>::next(t, idx[c]);
+  }
+  uint32_t r = 0;
+#pragma unroll
+  for (int c = 0; c < Chains; ++c) r ^= idx[c];
+  if (r == 0xFFFFFFFFu) out[0] = r + occupancy_lds[0];
+}
+
+template <int Chains, int W>
+double run_wide(const uint32_t* t, uint32_t n, int waves, int cus, uint32_t* out, size_t lds_total) {
+  const int blocks = cus * waves;
+  const size_t lds = lds_total / waves - 1024;
+  const int iters = 256;
+  CHECK(hipFuncSetAttribute((const void*)chase_wide<Chains, W>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  hipLaunchKernelGGL((chase_wide<Chains, W>), dim3(blocks), dim3(256), lds, 0, t, n, iters, out);
+  CHECK(hipEventRecord(e0));
+  hipLaunchKernelGGL((chase_wide<Chains, W>), dim3(blocks), dim3(256), lds, 0, t, n, iters, out);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  CHECK(hipGetLastError());
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  return (double)blocks * 256 * iters * Chains / (ms * 1e-3) / cus;  // lane entries per second per CU
+}
+
+template <int W>
+void width_rows(size_t bytes, int cus, uint32_t* out, size_t lds_total) {
+  const size_t n = bytes / (4 * W);
+  std::vector<uint32_t> h(n * W, 0u);
+  uint64_t s = 88172645463325252ull;
+  for (size_t i = 0; i < n; ++i) {
+    s ^= s << 13;
+    s ^= s >> 7;
+    s ^= s << 17;
+    h[i * W] = (uint32_t)(s % n);
+  }
+  uint32_t* t;
+  CHECK(hipMalloc(&t, n * W * 4));
+  CHECK(hipMemcpy(t, h.data(), n * W * 4, hipMemcpyHostToDevice));
+  for (int waves : {4, 7})
+    for (int chains : {1, 2}) {
+      const double r = chains == 1 ? run_wide<1, W>(t, (uint32_t)n, waves, cus, out, lds_total)
+                                   : run_wide<2, W>(t, (uint32_t)n, waves, cus, out, lds_total);
+      std::printf("width %3d %10.2f %6d %6d %10.4f\n", W * 4, bytes / 1048576.0, chains, waves, r * 1e-9);
+    }
+  CHECK(hipFree(t));
+}
+
 template <int Chains>
 double run(const uint32_t* t, uint32_t n, int waves, int cus, uint32_t* out, size_t lds_total, int active = 64) {
   const int blocks = cus * waves;  // 256 threads = 4 waves per block, one per SIMD
@@ -69,6 +160,16 @@ int main(int argc, char** argv) {
   uint32_t* out;
   CHECK(hipMalloc(&out, 4));
   const bool calib = argc > 1 && std::string(argv[1]) == "calib";  // one config, for a --pmc pass
+  if (argc > 1 && std::string(argv[1]) == "width") {  // lane entries/s per CU by entry width and table size
+    std::printf("%5s %5s %10s %6s %6s %10s\n", "", "bytes", "table_MiB", "chains", "waves", "Gentry/s/CU");
+    for (size_t bytes : {size_t(1228800), size_t(16) << 20, size_t(256) << 20, size_t(1536) << 20}) {
+      width_rows<1>(bytes, cus, out, lds_total);
+      width_rows<2>(bytes, cus, out, lds_total);
+      width_rows<4>(bytes, cus, out, lds_total);
+      width_rows<8>(bytes, cus, out, lds_total);
+    }
+    return 0;
+  }
   const size_t sizes[] = {307200, 1u << 22, 1u << 26};  // 1.2 MiB (L2), 16 MiB (MALL), 256 MiB (HBM)
   std::printf("gather ceiling: %d CUs, divergent 4-B loads, loads/s per CU (G)\n", cus);
   std::printf("%10s %6s %6s %10s\n", "table_MiB", "chains", "waves", "Gload/s/CU");

@@ -364,7 +364,7 @@ static int upload(const void* src, size_t n, void** dst, size_t& bytes) {
 static int upload_grid(const HostGrid& h, DeviceGrid& d) {
   d.dev = h.dev;
   int rc;
-  // The stencil-major pool is 16 KiB per leaf (8x the voxels): a large sparse volume can exceed the
+  // The stencil pool is 9 KiB per leaf (4.5x the voxels): a large sparse volume can exceed the
   // device's memory.  Say so before the first allocation instead of failing inside hipMalloc.
   const size_t need = h.cells8.size() * sizeof(int2) + h.runs8.size() + h.walk8.size() * sizeof(uint32_t) +
                       h.cells128.size() * sizeof(int2) + h.root.size() * sizeof(RootTileDev) +
@@ -373,7 +373,7 @@ static int upload_grid(const HostGrid& h, DeviceGrid& d) {
   VPT_HIP(hipMemGetInfo(&free_b, &total_b));
   if (need > free_b)
     return set_error(VPT_E_NOMEM, "grid upload: needs " + std::to_string(need >> 20) + " MiB (" +
-                                      std::to_string(h.dev.leaf_count) + " leaves x 16 KiB stencil pool + tables), " +
+                                      std::to_string(h.dev.leaf_count) + " leaves x 9 KiB stencil pool + tables), " +
                                       std::to_string(free_b >> 20) + " MiB free on the device");
   if ((rc = upload(h.cells8.data(), h.cells8.size() * sizeof(int2), &d.cells8, d.bytes))) return rc;
   if ((rc = upload(h.runs8.data(), h.runs8.size(), &d.runs8, d.bytes))) return rc;

@@ -9,7 +9,8 @@
 //                                          bits for an interior cell, the bits | kWalkEdge for another
 //                                          dim-8 cell, kWalkSlow otherwise; padded by
 //                                          kWalkPad cells of kWalkSlow on every side (w8_n = r8_n + 4)
-//   bricks   float[leaf][8][8][8][8]       per leaf voxel its whole 2x2x2 trilinear stencil (built
+//   bricks   float[leaf][8][8][9][4]       per voxel row (y, z) the 2x2 squares of x = 0..8; a voxel's
+//                                          2x2x2 trilinear stencil is the squares of x and x + 1 (built
 //                                          from 9^3 apron bricks: the leaf's voxels plus the +1
 //                                          neighbours), NanoVDB SampleFromVoxels semantics
 // One 8-byte cells8 load answers getDim, probeLeaf, probeValue and the majorant of
@@ -421,7 +422,7 @@ int build_host_grid(const vpt_grid_desc& d, bool fix, int threads, HostGrid& out
   });
 
   {
-    // expand the apron bricks into per-voxel stencils (corner q = dx<<2 | dy<<1 | dz)
+    // expand the apron bricks into square rows (per row (y, z) the 2x2 squares of x = 0..8)
     std::vector<float> apron;
     apron.swap(out.bricks);
     out.bricks.assign((size_t)nleaf * kBrickVox, 0.0f);
@@ -429,11 +430,11 @@ int build_host_grid(const vpt_grid_desc& d, bool fix, int threads, HostGrid& out
       for (int64_t n = b; n < e; ++n) {
         const float* src = apron.data() + (size_t)n * 729;
         float* dst = out.bricks.data() + (size_t)n * kBrickVox;
-        for (int x = 0; x < 8; ++x)
+        for (int x = 0; x < 9; ++x)
           for (int y = 0; y < 8; ++y)
             for (int z = 0; z < 8; ++z)
-              for (int q = 0; q < 8; ++q)
-                dst[(((x << 6) | (y << 3) | z) << 3) | q] = src[(x + (q >> 2)) * 81 + (y + ((q >> 1) & 1)) * 9 + z + (q & 1)];
+              for (int q = 0; q < 4; ++q)
+                dst[((y * 8 + z) * 9 + x) * 4 + q] = src[x * 81 + (y + (q >> 1)) * 9 + z + (q & 1)];
       }
     });
     G.bricks = out.bricks.data();

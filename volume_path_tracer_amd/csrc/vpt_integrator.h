@@ -48,18 +48,21 @@ struct DevGrid {
   const uint32_t* walk8; // per (padded) cells8 entry: the majorant's bits if the cell is interior, else kWalkSlow
   const int2* cells128;
   const RootTileDev* root;
-  const float* bricks;  // [leaf][8][8][8][8]: per leaf voxel its 2x2x2 trilinear stencil (see brick_index)
+  const float* bricks;  // [leaf][y 8][z 8][x 9][4]: per voxel row the 2x2 squares of its stencils (see brick_index)
 };
 
-// Stencil-major brick pool: per leaf voxel (x, y, z) in 0..7 its whole 2x2x2 trilinear stencil
-// (the voxel and its +x/+y/+z neighbours, crossing into the neighbour leaves at the faces), 8 floats =
-// 32 B, one aligned piece of a 128-B line; corner q = dx<<2 | dy<<1 | dz.  A stencil refresh is two
-// 16-byte loads from one line, where the 9^3 apron brick of round 1 spread it over up to 4 lines
-// (8 loads); the pool is 8x the 8^3 voxels (16 KiB per leaf: 1.5 GB for the 512^3 stand-in; HBM has
-// 288 GB).  Measured (r02, same box): C3 423.3/421.3 -> 417.4/417.7 ms, C4 137.1 -> 134.9 ms.
-constexpr int kBrickVox = 512 * 8;
+// Stencil pool of square rows: per leaf and voxel row (y, z) in 0..7, the 2x2 (dy, dz) squares of
+// x = 0..8 (x = 8 crossing into the +x neighbour, y + 1 / z + 1 into the +y / +z ones), 4 floats =
+// 16 B each, corner order dy<<1 | dz.  The stencil of voxel (x, y, z) is the squares of x and x + 1:
+// 32 contiguous bytes, corner q = dx<<2 | dy<<1 | dz, two 16-byte loads from one 128-B line, or from
+// two when the pair straddles a line boundary (1 pair in 8).  The pool is 4.5x the 8^3 voxels (9 KiB
+// per leaf: 0.84 GB for the 512^3 stand-in).  History: r01's 9^3 apron bricks spread a stencil over up
+// to 4 lines; r02's stencil-major pool (8 floats per voxel, 8x the voxels, 1.49 GB) kept it in one
+// line; the square rows (r03) keep 7 of 8 stencils in one line, store each line's x-neighbours twice as
+// densely and cut the pool by 44 %: C3 359.5 -> 352.6 ms, C4 102.6 -> 99.7 ms (two rounds, one box).
+constexpr int kBrickVox = 576 * 4;
 __host__ __device__ __forceinline__ int64_t brick_index(int32_t code, int32_t i, int32_t j, int32_t k) {
-  return ((int64_t)code * 512 + (((i & 7) << 6) | ((j & 7) << 3) | (k & 7))) * 8;
+  return ((int64_t)code * 576 + ((j & 7) * 8 + (k & 7)) * 9 + (i & 7)) * 4;
 }
 
 struct Cell {
