@@ -99,3 +99,35 @@ MAPPED_CASES = [  # (id, per-axis voxel size, rotation in degrees)
     ("large_voxels", (20.0, 25.0, 18.0), (-15.0, 40.0, 5.0)),
     ("unit_rotated", (1.0, 1.0, 1.0), (30.0, 45.0, 60.0)),
 ]
+
+
+def remapped(grid: capi.Grid, mat, vec) -> capi.Grid:
+    """The same leaves under another index -> world map (mat, vec; float32 as NanoVDB stores them)."""
+    m = np.asarray(mat, np.float64)
+    return capi.Grid(map_mat=m.astype(np.float32), map_inv_mat=np.linalg.inv(m).astype(np.float32),
+                     map_vec=np.asarray(vec, np.float32), background=float(grid.desc.background),
+                     bbox_min=list(grid.desc.index_bbox_min), bbox_max=list(grid.desc.index_bbox_max),
+                     leaf_origin=grid.leaf_origin, leaf_values=grid.leaf_values, leaf_max=grid.leaf_max,
+                     leaf_value_mask=grid.leaf_value_mask)
+
+
+def temperature_pair(kind):
+    """(density, temperature) grids for the temperature sampler: "same" = the fire stand-in (one topology, one map); "shifted" = the temperature
+    grid moved by (3, -5, 2) world units (its corners fall in other 8^3 cells for part of the
+    lookups, and the joint values at the density leaves come from its tiles and background too);
+    "half_voxels" = a 128^3 temperature grid of 0.5-unit voxels over the 64^3 density (mostly the
+    temperature grid's own lookups); "sparse" = the sparse grid of every HDDA level, moved as in
+    "shifted", as temperature over the 128^3 cloud (its lower-node tiles inside the density leaves)."""
+    if kind == "sparse":
+        t = sparse_grid()
+        return SynthGrid(1, 128).grid(copy=True), remapped(t, np.eye(3), np.asarray(t.desc.map_vec, np.float64) + (3.0, -5.0, 2.0))
+    dens = SynthGrid(1, 64).grid(copy=True)
+    if kind == "same":
+        return dens, SynthGrid(2, 64).grid(copy=True)
+    if kind == "shifted":
+        t = SynthGrid(2, 64).grid(copy=True)
+        return dens, remapped(t, np.eye(3), np.asarray(t.desc.map_vec, np.float64) + (3.0, -5.0, 2.0))
+    if kind == "half_voxels":
+        return dens, remapped(SynthGrid(2, 128).grid(copy=True), 0.5 * np.eye(3), (0.0, 0.0, 0.0))
+    raise ValueError(kind)
+

@@ -365,3 +365,30 @@ def test_temperature_kernel_blackbody_from_memory_above_the_lds_rows():
         _assert_bitwise(_prod_film(it, (wave - 1) * T, T), f_o, f"wave {wave}")
     assert c_o["temp_stencils"] > 0
 
+
+
+@pytest.mark.parametrize("kind", ["shifted", "half_voxels", "sparse"])
+def test_temperature_grid_of_another_map_or_topology(kind):
+    """The temperature kernel with a temperature grid whose map / topology differ from the density's
+    (tests/grids.py temperature_pair): production films bit-exact vs the oracle, counters equal."""
+    from grids import look_at, temperature_pair
+    from volume_path_tracer_amd.render import Integrator
+
+    dens, temp = temperature_pair(kind)
+    wl = workload("c4", width=48, height=40, spp=2, grid_n=64)
+    n = 128 if kind == "sparse" else 64
+    look_at(wl.cfg, (0.3 * n, 0.6 * n, -2.2 * n), (0.5 * n, 0.45 * n, 0.5 * n))
+    it = Integrator(wl.cfg, dens, temp, device=0)
+    od, ot = _oracle_grids(dens, temp)
+    T = wl.cfg.jobs_per_wave()
+    it.counters(reset=True)
+    tot = {k: 0 for k in COUNTERS}
+    for wave in (1, 2):
+        f_o, _, c_o = O.render_jobs(wl.cfg, od, ot, (wave - 1) * T, T)
+        _assert_bitwise(_prod_film(it, (wave - 1) * T, T), f_o, f"{kind} wave {wave}")
+        for k in COUNTERS:
+            tot[k] += c_o[k]
+    c = it.counters()
+    for k in COUNTERS:
+        assert c[k] == tot[k], (k, c[k], tot[k])
+    assert tot["temp_stencils"] > 100

@@ -160,3 +160,26 @@ def test_blackbody_rows_in_lds_or_memory(scale):
     f_o, r_o, c_o, f_h, r_h, c_h = _run_both(wl, jobs)
     assert np.array_equal(r_o.view(np.uint32), r_h.view(np.uint32))
     assert c_o["temp_stencils"] > 100
+
+
+@pytest.mark.parametrize("kind", ["same", "shifted", "half_voxels", "sparse"])
+def test_temperature_grid_of_another_map_or_topology(kind):
+    """The temperature sampler on grids whose map and topology differ from the density's (a shifted
+    grid, half-size voxels, every HDDA level's tiles): bit-exact, counters equal.  (These cases were
+    written for the r03 joint-pool experiment, tools/experiments/r03_joint_temperature.patch, whose
+    two lookup paths they exercise; they stay as coverage of the temperature grid's own lookups.)"""
+    from grids import look_at, temperature_pair
+
+    dens, temp = temperature_pair(kind)
+    wl = workload("c4", width=32, height=24, spp=2, grid_n=64)
+    n = 128 if kind == "sparse" else 64
+    look_at(wl.cfg, (0.3 * n, 0.6 * n, -2.2 * n), (0.5 * n, 0.45 * n, 0.5 * n))
+    jobs = wl.cfg.jobs_per_wave() * 2
+    od, ot = O.OracleGrid(dens, fix_majorants=True), O.OracleGrid(temp, fix_majorants=False)
+    f_o, r_o, c_o = O.render_jobs(wl.cfg, od, ot, 0, jobs, records=True)
+    f_h, r_h, c_h = HS.render_jobs(wl.cfg, dens, temp, 0, jobs, records=True)
+    assert np.array_equal(r_o.view(np.uint32), r_h.view(np.uint32)), "per-sample radiance differs"
+    assert np.array_equal(f_o.view(np.uint32), f_h.view(np.uint32))
+    for k in ("temp_stencils", "density_evals", "rng_draws"):
+        assert c_o[k] == c_h[k], k
+    assert c_o["temp_stencils"] > 100, c_o
