@@ -56,6 +56,8 @@ def parser():
     ap.add_argument("--order", type=int, default=-1, help="job order mode (-1: library default)")
     ap.add_argument("--tail", type=int, default=0, help="VPT_ORDER_COST_TAIL tile-major waves (0: auto)")
     ap.add_argument("--tile-costs", default=None, help=".npy of per-tile costs for the job order (vpt_gpu_set_tile_costs)")
+    ap.add_argument("--perm", default="", help="explicit job order: 'same-tile' = each tile's jobs of all waves consecutively, "
+                    "costliest tile first (the lanes of a wavefront trace one tile's pixels at different spp)")
     return ap
 
 
@@ -79,6 +81,11 @@ def sweep(a):
     if a.tile_costs:
         import numpy as np
         it.set_tile_costs(np.load(a.tile_costs))
+    if a.perm == "same-tile":
+        import numpy as np
+        T = wl.cfg.jobs_per_wave()
+        tiles = np.argsort(-it.tile_costs()[0], kind="stable").astype(np.int64)
+        it.set_job_permutation((np.arange(a.spp, dtype=np.int64)[None, :] * T + tiles[:, None]).reshape(-1))
     it.render_waves(1, 1)
     torch.cuda.synchronize()
     if a.profile:
@@ -102,7 +109,7 @@ def sweep(a):
                 best = min(best, time.perf_counter() - t)
             if a.profile:
                 print(json.dumps({"gate": g, "profile": it.profile(reset=True)}), flush=True)
-            print(json.dumps({"lib": os.environ.get("VPT_LIB", "default"), "config": a.config, "order": a.order, "tail": a.tail,
+            print(json.dumps({"lib": os.environ.get("VPT_LIB", "default"), "config": a.config, "order": a.order, "tail": a.tail, "perm": a.perm,
                               "gate": g, "lat": lat, "blocks": b or base_blocks, "spp": a.spp, "ms": round(best * 1e3, 2),
                               "Msps": round(wl.cfg.width * wl.cfg.height * a.spp / best / 1e6, 2)}), flush=True)
     del it
