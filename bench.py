@@ -155,7 +155,7 @@ def request_roofline(config: str, samples_per_launch: float, avg_launch_s: float
     (tools/ubench/gather.hip).  Requests per sample come from the newest committed rocprofv3 counter
     pass of this config (tools/kernel_counters.sh) -- builder measurements, named in the line --
     times this run's samples per launch over this run's average launch time."""
-    cnt, cnt_src = newest_profile("*_counters.json", lambda j: j.get("config") == config and
+    cnt, cnt_src = newest_profile("*_counters.json", lambda j: j.get("config") == config and not j.get("bench_args") and
                                   j.get("derived", {}).get("l1_to_l2_requests_per_sample"))
     ceil, ceil_src = newest_profile("*_gather_ceiling.json")
     if not cnt or not ceil:

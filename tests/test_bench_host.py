@@ -52,3 +52,16 @@ def test_strong_scaling_configs_share_the_cloud():
     """--strong-configs only accepts frames of the 512^3 cloud (the grid is built once)."""
     with pytest.raises(ValueError, match="c4"):
         bench.strong_scaling(["c4"], None, 0, 2, torch.device("cuda", 0), torch.device("cpu"), 1, 0, None)
+
+
+def test_request_roofline_uses_the_configs_own_counter_pass():
+    """Counter passes of other workloads (tools/kernel_counters.sh ... --grid-n N: bench_args set) never
+    feed the bench line's request_frac."""
+    import json
+    from pathlib import Path
+
+    import bench
+
+    r = bench.request_roofline("c3", 5.3e8, 0.35, 256)
+    src = r["request_sources"][0]
+    assert not json.loads((Path(bench.ROOT) / src).read_text()).get("bench_args"), src

@@ -12,6 +12,7 @@ from collections import defaultdict
 from pathlib import Path
 
 d, config = Path(sys.argv[1]), sys.argv[2]
+bench_args = sys.argv[3:]  # extra bench.py arguments of the passes (e.g. --grid-n 384: not the config's workload)
 vals = defaultdict(list)
 ms = []
 samples = None
@@ -64,7 +65,7 @@ if g("SQ_WAVE_CYCLES"):
         der["valu_lane_utilisation"] = g("SQ_THREAD_CYCLES_VALU", 0) / g("SQ_ACTIVE_INST_VALU") / 64
 if g("SQ_INST_LEVEL_VMEM") and g("SQ_INSTS_VMEM_RD"):
     der["vmem_in_flight_per_instruction"] = g("SQ_INST_LEVEL_VMEM") / (g("SQ_INSTS_VMEM_RD") + g("SQ_INSTS_VMEM_WR", 0))
-out = {"config": config, "kernel": "vpt_integrate_kernel", "samples_per_launch": samples,
+out = {"config": config, "bench_args": bench_args, "kernel": "vpt_integrate_kernel", "samples_per_launch": samples,
        "kernel_ms_per_pass": ms, "counters_per_launch": {k: round(v, 1) for k, v in sorted(c.items())},
        "derived": {k: round(v, 6) for k, v in der.items()},
        "method": "rocprofv3 --pmc, one pass per counter group (tools/kernel_counters.sh), one launch of "

@@ -19,4 +19,4 @@ SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_I
 TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE
 TCP_TOTAL_CACHE_ACCESSES_sum TCP_PENDING_STALL_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE
 PASSES
-python3 tools/kernel_counters.py $O $CFG > $O/summary.txt && cat $O/summary.txt | tail -25
+python3 tools/kernel_counters.py $O $CFG "$@" > $O/summary.txt && cat $O/summary.txt | tail -25
