@@ -18,6 +18,9 @@ int set_error(int code, const std::string& msg) {
 }  // namespace vpt
 
 namespace {
+// Runs variant (run skipping) of the density-only path: -1 = the GPU's rule (run_fraction >= 1/4,
+// vpt_gpu.hip), 0 / 1 = forced (vpths_set_runs).
+int g_runs = -1;
 struct HostEnv {
   uint64_t jid_begin, jid_count, next = 0;
   float* film;
@@ -81,7 +84,8 @@ extern "C" int vpths_render_jobs_order(const vpt_configuration* cfg, const vpt_g
   if (rc) return rc;
   vpt::HostGrid hd, ht;
   if ((rc = vpt::build_host_grid(*density, true, 0, hd))) return rc;
-  vpt::compute_runs(hd, 0);  // the density-only path runs the Runs variant (run skipping) here
+  vpt::compute_runs(hd, 0);
+  const bool runs = g_runs < 0 ? hd.run_fraction >= 0.25 : g_runs != 0;
   S.density = hd.dev;
   vpt::scene_finalize(S);
   if (temperature) {
@@ -117,7 +121,12 @@ extern "C" int vpths_render_jobs_order(const vpt_configuration* cfg, const vpt_g
   if (temperature)
     while (ln.state != vpt::ST_DONE) vpt::lane_iteration<true, true, false>(&S, ln, env);
   else
-    while (ln.state != vpt::ST_DONE) vpt::lane_iteration<false, true, true>(&S, ln, env);
+    while (ln.state != vpt::ST_DONE) {
+      if (runs)
+        vpt::lane_iteration<false, true, true>(&S, ln, env);
+      else
+        vpt::lane_iteration<false, true, false>(&S, ln, env);
+    }
   env.cnt[vpt::CNT_DDA_STEPS] += ln.n_dda;
   if (counters) {
     uint64_t* o = reinterpret_cast<uint64_t*>(counters);
@@ -168,18 +177,23 @@ extern "C" int vpths_probe(const vpt_grid_desc* d, const int32_t* ijk, int n, fl
 // (sign bit clear) needs all 27 cells of its neighbourhood at HDDA dim 8 and holds the cell's
 // majorant bits; an edge word (kWalkEdge set) needs the cell itself at dim 8 and holds its majorant
 // bits | kWalkEdge; every dim-8 cell of the r8 table whose majorant has the sign bit clear is one of
-// the two; the padding is kWalkSlow.  counts = {interior, edge, slow, padding}; returns violations.
+// the two (but interior cells whose majorant bits are 1..kZeroRunMax, which are slow); the padding is
+// kWalkSlow.  A +0 interior cell holds its zero-run radius r: r = 0 is checked as an interior +0 cell,
+// r >= 1 by induction -- each of its 26 neighbours holds a zero-run word of radius >= r - 1 (the ball
+// of radius r is the union of the neighbours' balls of radius r - 1).
+// counts = {interior, edge, slow, padding, zero-run words with r >= 1}; returns violations.
 extern "C" int64_t vpths_check_walk(const vpt_grid_desc* d, int64_t* counts) {
   vpt::HostGrid h;
   if (vpt::build_host_grid(*d, true, 0, h)) return -1;
   const vpt::DevGrid& G = h.dev;
   auto bits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
+  auto word = [&](int32_t a, int32_t b, int32_t c) { return h.walk8[((size_t)a * G.w8_n[1] + b) * G.w8_n[2] + c]; };
   int64_t bad = 0;
-  for (int k = 0; k < 4; ++k) counts[k] = 0;
+  for (int k = 0; k < 5; ++k) counts[k] = 0;
   for (int32_t a = 0; a < G.w8_n[0]; ++a)
     for (int32_t b = 0; b < G.w8_n[1]; ++b)
       for (int32_t c = 0; c < G.w8_n[2]; ++c) {
-        const uint32_t w = h.walk8[((size_t)a * G.w8_n[1] + b) * G.w8_n[2] + c];
+        const uint32_t w = word(a, b, c);
         const int32_t o[3] = {G.w8_org[0] + 8 * a, G.w8_org[1] + 8 * b, G.w8_org[2] + 8 * c};
         const bool in_r8 = a >= vpt::kWalkPad && a < vpt::kWalkPad + G.r8_n[0] && b >= vpt::kWalkPad &&
                            b < vpt::kWalkPad + G.r8_n[1] && c >= vpt::kWalkPad && c < vpt::kWalkPad + G.r8_n[2];
@@ -191,9 +205,15 @@ extern "C" int64_t vpths_check_walk(const vpt_grid_desc* d, int64_t* counts) {
         const vpt::Cell C = vpt::cell_at(G, o[0], o[1], o[2]);
         const uint32_t m = bits(vpt::majorant_of(C));
         const bool dim8 = vpt::hdda_dim_of(C) == 8;
+        bool all8 = true;
+        for (int da = -1; da <= 1; ++da)
+          for (int db = -1; db <= 1; ++db)
+            for (int dc = -1; dc <= 1; ++dc)
+              all8 = all8 && vpt::hdda_dim_of(vpt::cell_at(G, o[0] + 8 * da, o[1] + 8 * db, o[2] + 8 * dc)) == 8;
         if (w == vpt::kWalkSlow) {
           ++counts[2];
-          bad += dim8 && !(m & vpt::kWalkEdge) && m != vpt::kWalkSlow;  // a fast cell left slow
+          const bool tiny = all8 && m >= 1u && m <= vpt::kZeroRunMax;
+          bad += dim8 && !(m & vpt::kWalkEdge) && m != vpt::kWalkSlow && !tiny;  // a fast cell left slow
           continue;
         }
         if (w & vpt::kWalkEdge) {
@@ -202,14 +222,30 @@ extern "C" int64_t vpths_check_walk(const vpt_grid_desc* d, int64_t* counts) {
           continue;
         }
         ++counts[0];
-        bool all8 = true;
+        if (w > vpt::kZeroRunMax) {
+          bad += !all8 || w != m;
+          continue;
+        }
+        bad += !all8 || m != 0u;  // a zero-run word: an interior +0 cell
+        if (w == 0) continue;
+        ++counts[4];
         for (int da = -1; da <= 1; ++da)
           for (int db = -1; db <= 1; ++db)
-            for (int dc = -1; dc <= 1; ++dc)
-              all8 = all8 && vpt::hdda_dim_of(vpt::cell_at(G, o[0] + 8 * da, o[1] + 8 * db, o[2] + 8 * dc)) == 8;
-        bad += !all8 || w != m;
+            for (int dc = -1; dc <= 1; ++dc) {
+              const uint32_t nw = word(a + da, b + db, c + dc);  // in the padded table: all8 above
+              bad += !(nw <= vpt::kZeroRunMax && nw + 1u >= w);
+            }
       }
   return bad;
+}
+
+extern "C" void vpths_set_runs(int on) { g_runs = on; }
+
+// Walk-word loads issued and walk words synthesised from zero runs since the last reset.
+extern "C" void vpths_walk_loads(uint64_t* loads, uint64_t* synth, int reset) {
+  *loads = vpt::g_walk_loads;
+  *synth = vpt::g_walk_synth;
+  if (reset) vpt::g_walk_loads = vpt::g_walk_synth = 0;
 }
 
 // Run radii (vpt::compute_runs) checked by brute force: every cell within Chebyshev distance r of a

@@ -108,12 +108,14 @@ def test_walk_table_words(which):
     import grids
     g = {"cloud128": lambda: SynthGrid(1, 128).grid(), "constant": lambda: SynthGrid(0, 128).grid(),
          "sparse": grids.sparse_grid, "tiles_only": grids.tiles_only_grid, "signed": grids.signed_grid}[which]()
-    counts = np.zeros(4, np.int64)
+    counts = np.zeros(5, np.int64)
     bad = HS.lib().vpths_check_walk(C.byref(g.desc), counts.ctypes.data_as(C.POINTER(C.c_int64)))
     assert bad == 0
-    interior, edge, slow, pad = counts.tolist()
+    interior, edge, slow, pad, zero_runs = counts.tolist()
     assert pad > 0
     if which in ("cloud128", "constant", "sparse"):
         assert interior > 0 and edge > 0
+    if which == "cloud128":
+        assert zero_runs > 0  # empty space inside the cloud's lower nodes: zero-run words
     if which == "signed":
         assert slow > 0 and edge > 0  # negative majorants and the -0.0 tile stay slow

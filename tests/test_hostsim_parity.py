@@ -183,3 +183,28 @@ def test_temperature_grid_of_another_map_or_topology(kind):
     for k in ("temp_stencils", "density_evals", "rng_draws"):
         assert c_o[k] == c_h[k], k
     assert c_o["temp_stencils"] > 100, c_o
+
+
+@pytest.mark.parametrize("runs", [0, 1])
+def test_zero_run_walk_words_bit_exact(runs):
+    """Zero-run walk words (kZeroRunMax): a step in empty space hands the next cell's word over
+    without loading it.  With the Runs variant off (the cloud's production kernel) the walk must
+    synthesise words, and the samples stay the oracle's bit for bit, in both variants."""
+    import ctypes as C
+    L = HS.lib()
+    L.vpths_walk_loads.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_int]
+    L.vpths_set_runs.argtypes = [C.c_int]
+    wl = workload("c3", width=48, height=40, spp=2, grid_n=256)
+    jobs = wl.cfg.jobs_per_wave() * 2
+    loads, synth = C.c_uint64(), C.c_uint64()
+    L.vpths_walk_loads(C.byref(loads), C.byref(synth), 1)
+    L.vpths_set_runs(runs)
+    try:
+        f_o, r_o, c_o, f_h, r_h, c_h = _run_both(wl, jobs)
+    finally:
+        L.vpths_set_runs(-1)
+    L.vpths_walk_loads(C.byref(loads), C.byref(synth), 1)
+    assert np.array_equal(r_o.view(np.uint32), r_h.view(np.uint32)), "per-sample radiance differs"
+    assert c_o["dda_steps"] == c_h["dda_steps"] and c_o["segments"] == c_h["segments"]
+    if runs == 0:
+        assert synth.value > 0.01 * (loads.value + synth.value), (loads.value, synth.value)

@@ -6,7 +6,8 @@
 //   cells128 int2[...]                     one entry per 128^3 cell over every upper node
 //   root     RootTileDev[]                 value tiles at the root (outside every upper node)
 //   walk8    uint32[w8_n.x][w8_n.y][w8_n.z] the HDDA fast path's word per cells8 entry: the majorant's
-//                                          bits for an interior cell, the bits | kWalkEdge for another
+//                                          bits for an interior cell (for a +0 majorant: its zero-run
+//                                          radius, see kZeroRunMax), the bits | kWalkEdge for another
 //                                          dim-8 cell, kWalkSlow otherwise; padded by
 //                                          kWalkPad cells of kWalkSlow on every side (w8_n = r8_n + 4)
 //   bricks   float[leaf][8][8][9][4]       per voxel row (y, z) the 2x2 squares of x = 0..8; a voxel's
@@ -165,6 +166,67 @@ void compute_runs(HostGrid& h, int threads) {
   h.run_fraction = interior ? (double)long_runs / (double)interior : 0.0;
 }
 
+std::vector<uint8_t> zero_run_radii(const HostGrid& h, int threads) {
+  if (threads <= 0) threads = default_threads();
+  const DevGrid& G = h.dev;
+  const int32_t nx = G.r8_n[0], ny = G.r8_n[1], nz = G.r8_n[2];
+  const size_t n = h.cells8.size();
+  std::vector<uint8_t> out(n, 0);
+  if (n == 0) return out;
+  auto idx = [&](int64_t a, int32_t b, int32_t c) { return ((size_t)a * ny + b) * nz + c; };
+  // r = -1: not an interior +0 cell; else the radius reached so far
+  std::vector<int16_t> r(n);
+  parallel_for(nx, threads, [&](int64_t b0, int64_t e0) {
+    for (size_t q = idx(b0, 0, 0); q < idx(e0, 0, 0); ++q) {
+      const int32_t x = h.cells8[q].x;
+      const float m = majorant_of(Cell{cell8_code(x), math::as_f32((uint32_t)h.cells8[q].y)});
+      r[q] = (cell8_interior(x) && math::as_u32(m) == 0u) ? 0 : -1;
+    }
+  });
+  // erosion pass k: a cell reaches radius k when its whole 3x3x3 block (inside the table) has
+  // radius >= k - 1 (separable over z, y, x)
+  std::vector<uint8_t> ez(n), ey(n), grow(n);
+  for (int32_t k = 1; k <= (int32_t)kZeroRunMax; ++k) {
+    auto ok = [&](size_t q) { return r[q] >= k - 1; };
+    parallel_for(nx, threads, [&](int64_t b0, int64_t e0) {
+      for (int64_t a = b0; a < e0; ++a)
+        for (int32_t b = 0; b < ny; ++b)
+          for (int32_t c = 0; c < nz; ++c) {
+            const size_t q = idx(a, b, c);
+            ez[q] = c > 0 && c + 1 < nz && ok(q - 1) && ok(q) && ok(q + 1);
+          }
+    });
+    parallel_for(nx, threads, [&](int64_t b0, int64_t e0) {
+      for (int64_t a = b0; a < e0; ++a)
+        for (int32_t b = 0; b < ny; ++b)
+          for (int32_t c = 0; c < nz; ++c) {
+            const size_t q = idx(a, b, c), s = (size_t)nz;
+            ey[q] = b > 0 && b + 1 < ny && ez[q - s] && ez[q] && ez[q + s];
+          }
+    });
+    std::vector<int64_t> grown_by(nx, 0);
+    parallel_for(nx, threads, [&](int64_t b0, int64_t e0) {
+      for (int64_t a = b0; a < e0; ++a)
+        for (int32_t b = 0; b < ny; ++b)
+          for (int32_t c = 0; c < nz; ++c) {
+            const size_t q = idx(a, b, c), s = (size_t)ny * nz;
+            const bool g = a > 0 && a + 1 < nx && ey[q - s] && ey[q] && ey[q + s];
+            grow[q] = g;
+            grown_by[a] += g;
+          }
+    });
+    int64_t grown = 0;
+    for (int64_t v : grown_by) grown += v;
+    if (!grown) break;
+    parallel_for(nx, threads, [&](int64_t b0, int64_t e0) {
+      for (size_t q = idx(b0, 0, 0); q < idx(e0, 0, 0); ++q)
+        if (grow[q]) r[q] = (int16_t)k;
+    });
+  }
+  for (size_t q = 0; q < n; ++q) out[q] = r[q] > 0 ? (uint8_t)r[q] : 0;
+  return out;
+}
+
 void build_walk_table(HostGrid& h, int threads) {
   DevGrid& G = h.dev;
   const int32_t nx = G.r8_n[0], ny = G.r8_n[1], nz = G.r8_n[2];
@@ -175,6 +237,7 @@ void build_walk_table(HostGrid& h, int threads) {
   const size_t n = (size_t)G.w8_n[0] * G.w8_n[1] * G.w8_n[2];
   G.w8_max = (uint32_t)(n - 1);
   h.walk8.assign(n, kWalkSlow);
+  const std::vector<uint8_t> zr = VPT_ZERO_RUNS ? zero_run_radii(h, threads) : std::vector<uint8_t>(h.cells8.size(), 0);
   parallel_for((int64_t)nx, threads, [&](int64_t b0, int64_t e0) {
     for (int64_t a = b0; a < e0; ++a)
       for (int32_t b = 0; b < ny; ++b)
@@ -185,8 +248,12 @@ void build_walk_table(HostGrid& h, int threads) {
           if (!cell8_dim8(code)) continue;
           const uint32_t m = math::as_u32(majorant_of(Cell{code, math::as_f32((uint32_t)h.cells8[q].y)}));
           if (m & kWalkEdge) continue;  // a majorant with the sign bit set: general path (same result)
-          h.walk8[((size_t)(a + kWalkPad) * G.w8_n[1] + (b + kWalkPad)) * G.w8_n[2] + (c + kWalkPad)] =
-              cell8_interior(x) ? m : (m | kWalkEdge);
+          uint32_t w = m | kWalkEdge;
+          if (cell8_interior(x)) {
+            if (VPT_ZERO_RUNS && m >= 1u && m <= kZeroRunMax) continue;  // bits that read as a zero run: general path
+            w = (VPT_ZERO_RUNS && m == 0u) ? (uint32_t)zr[q] : m;        // +0: the zero-run radius (0 = none)
+          }
+          h.walk8[((size_t)(a + kWalkPad) * G.w8_n[1] + (b + kWalkPad)) * G.w8_n[2] + (c + kWalkPad)] = w;
         }
   });
   h.dev.walk8 = h.walk8.data();

@@ -110,6 +110,21 @@ constexpr uint32_t kWalkSlow = 0xFFFFFFFFu;
 // whose lookahead point lies in the cell itself.  Majorants with the sign bit set are stored as
 // kWalkSlow.
 constexpr uint32_t kWalkEdge = 0x80000000u;
+// Zero runs (empty-space skipping without changing a step): an interior cell with majorant +0 stores
+// its zero-run radius r (the bits 0..kZeroRunMax) -- every cell within Chebyshev distance r is interior
+// with majorant +0 as well.  The HDDA's next cell is face-adjacent, so its word is known to be a zero
+// run of radius >= r - 1: hdda_pre_advance writes r - 1 instead of loading it, and a ray crossing empty
+// space loads one walk word per ~r cells.  Every step still runs (same times, same float operations);
+// only its load goes.  Interior majorants whose bits are 1..kZeroRunMax (tiny denormals) are stored
+// as kWalkSlow.
+constexpr uint32_t kZeroRunMax = 63;
+#ifndef VPT_ZERO_RUNS
+#define VPT_ZERO_RUNS 1
+#endif
+#if !defined(__HIP_DEVICE_COMPILE__)
+// Host builds only (the CPU simulator): walk-word loads issued and walk words synthesised from a zero run.
+inline uint64_t g_walk_loads = 0, g_walk_synth = 0;
+#endif
 // Cells of kWalkSlow padding around the walk table.  The HDDA prefetches the walk word of the cell
 // it is about to enter whenever it walks at dim 8; that cell is at most 2 cells outside the r8 table
 // (see hdda_pre_advance), so the prefetch needs no bounds test.
@@ -550,14 +565,22 @@ __host__ __device__ __forceinline__ uint32_t walk_index(const DevGrid& g, const 
 // Padding argument (kWalkPad = 2): at dim 8 the current cell is within one cell of the r8 table (it
 // was reached from an interior cell, or its lookahead cell -- within ~1 voxel -- has dim 8 and so
 // lies in the table), and the next cell is adjacent to it.
-__host__ __device__ __forceinline__ void hdda_pre_advance(const DevGrid& g, Lane& ln) {
+// synth: the step took the fast path on a zero-run word r >= 1 (still in ln.pw): the next cell's word
+// is r - 1, without a load (kZeroRunMax).  The word is decremented in place by a select before the
+// (masked) load, so the load writes the register the next step reads and no VALU write follows it
+// (either would make the wavefront wait for the load here instead of at the next step).
+__host__ __device__ __forceinline__ void hdda_pre_advance(const DevGrid& g, Lane& ln, bool synth = false) {
   ln.Tn = hdda_advance(ln);
-  uint32_t w = kWalkSlow;
-  if (ln.dim == 8) {
+  synth = VPT_ZERO_RUNS && synth;
+  ln.pw = synth ? ln.pw - 1u : kWalkSlow;
+  if (!synth && ln.dim == 8) {
     const uint32_t off = walk_index(g, ln.vox) * 4u;
-    w = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(g.walk8) + off);
+    ln.pw = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(g.walk8) + off);
   }
-  ln.pw = w;
+#if !defined(__HIP_DEVICE_COMPILE__)
+  if (synth) ++g_walk_synth;
+  else if (ln.dim == 8) ++g_walk_loads;
+#endif
 }
 
 // Volume::intersect (volume.cpp:78-88) + RayMajorantIterator ctor (volume.cpp:90-98).
@@ -636,15 +659,18 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
   // in a dim-8 cell, so getDim answers 8 == dim and HDDA::update is a no-op; the prefetched walk word
   // answers both "interior?" and the majorant.
   const uint32_t w = ln.pw;
+  bool synth = false;  // a zero run r >= 1: the pre-advance derives the next word (kZeroRunMax)
   if ((int32_t)w >= 0) {
-    const float m = math::as_f32(w);
+    const float m = (VPT_ZERO_RUNS && w <= kZeroRunMax) ? 0.0f : math::as_f32(w);
     ln.maj = m;
+    synth = w - 1u < kZeroRunMax;
     if (Runs && m == ln.s_dmaj) {
       // an interior cell lies in the r8 table: its run radius from the unpadded index
       const uint32_t a = (uint32_t)((ln.vox[0] - g.r8_org[0]) >> 3), b = (uint32_t)((ln.vox[1] - g.r8_org[1]) >> 3),
                      c = (uint32_t)((ln.vox[2] - g.r8_org[2]) >> 3);
       for (int32_t r = (int32_t)g.runs8[math::mul24(math::mul24(a, (uint32_t)g.r8_n[1]) + b, (uint32_t)g.r8_n[2]) + c]; r > 0;
            --r) {
+        synth = false;  // the HDDA has left the cell w describes
         ++ln.n_dda;
         const float t = hdda_advance(ln);
         if (!(t <= ln.T1)) {
@@ -694,7 +720,7 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
       ln.maj = majorant_of((dx & ~(nd - 1)) == 0 ? la : cell_at(g, ln.vox[0], ln.vox[1], ln.vox[2]));
     }
   }
-  hdda_pre_advance(g, ln);  // the next step's advance, and its cell's walk word in flight
+  hdda_pre_advance(g, ln, synth);  // the next step's advance, and its cell's walk word in flight
   if (ln.maj == ln.s_dmaj) return false;
   ln.s_t1 = tk;
   return true;

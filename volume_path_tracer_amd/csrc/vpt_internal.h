@@ -31,8 +31,13 @@ struct HostGrid {
 void compute_runs(HostGrid& h, int threads);
 
 // The HDDA fast-path table of the cells8 entries (DevGrid::walk8): the majorant's bits for interior
-// cells, kWalkSlow for the others.  Sets h.walk8 and h.dev.walk8 (build_host_grid calls it).
+// cells (a +0 majorant: the zero-run radius), kWalkSlow for the others.  Sets h.walk8 and h.dev.walk8
+// (build_host_grid calls it).
 void build_walk_table(HostGrid& h, int threads);
+
+// Zero-run radius per cells8 entry: the largest r <= kZeroRunMax such that every cell within
+// Chebyshev distance r lies in the table, is interior and has majorant +0 (0 for other cells).
+std::vector<uint8_t> zero_run_radii(const HostGrid& h, int threads);
 
 // Builds the leaf-slot tables, the walk table and the stencil brick pool; fixes the majorants
 // (fix_majorants_for_interpolation, volume.cpp:104-160) when fix == true.
