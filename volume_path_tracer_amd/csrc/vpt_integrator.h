@@ -477,7 +477,7 @@ struct Lane {
   float Tn, T1;     // Tn: HDDA time of the pending cell (the one the HDDA has been advanced into)
   uint32_t pw;      // walk word of the pending cell (prefetched; kWalkSlow when not at dim 8)
   float nxt[3];
-  int32_t vox[3];
+  int32_t vox[3];   // HDDA voxel, relative to the walk table's origin (DevGrid::w8_org): vox_rel
   float finc[3];    // HDDA: dim * delta[axis] (the float product NanoVDB adds at every step)
   int32_t vinc[3];  // HDDA: dim * step[axis]
   // current majorant segment
@@ -543,18 +543,30 @@ __host__ __device__ __forceinline__ float hdda_advance(Lane& ln) {
 inline uint64_t g_walk_outside = 0;
 #endif
 
-// Walk-table index of the 8^3 cell holding voxel v (padded table).  The min() only guarantees a
-// memory-safe address; hdda_pre_advance never asks for a cell beyond the padding.  The padding is in
-// index space, and so is the HDDA's lookahead (1.0001 along the index-space ray, whose direction
-// Ray::worldToIndexF normalises): the argument holds for every voxel size and any affine map.
+// Walk-table index of the 8^3 cell holding voxel v, given relative to the table's origin (Lane::vox).
+// The min() only guarantees a memory-safe address; hdda_pre_advance never asks for a cell beyond the
+// padding.  The padding is in index space, and so is the HDDA's lookahead (1.0001 along the index-space
+// ray, whose direction Ray::worldToIndexF normalises): the argument holds for every voxel size and any
+// affine map.
 __host__ __device__ __forceinline__ uint32_t walk_index(const DevGrid& g, const int32_t v[3]) {
-  const uint32_t a = (uint32_t)((v[0] - g.w8_org[0]) >> 3), b = (uint32_t)((v[1] - g.w8_org[1]) >> 3),
-                 c = (uint32_t)((v[2] - g.w8_org[2]) >> 3);
-#if !defined(__HIP_DEVICE_COMPILE__)
-  if (a >= (uint32_t)g.w8_n[0] || b >= (uint32_t)g.w8_n[1] || c >= (uint32_t)g.w8_n[2]) ++g_walk_outside;
-#endif
+  const uint32_t a = (uint32_t)(v[0] >> 3), b = (uint32_t)(v[1] >> 3), c = (uint32_t)(v[2] >> 3);
   const uint32_t idx = math::mul24(math::mul24(a, (uint32_t)g.w8_n[1]) + b, (uint32_t)g.w8_n[2]) + c;
   return idx < g.w8_max ? idx : g.w8_max;
+}
+
+// Host builds: count a walk-word load of the cell holding v (and whether it lies outside the table).
+__host__ __device__ __forceinline__ void note_walk_load(const DevGrid& g, const int32_t v[3]) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t a = (uint32_t)(v[0] >> 3), b = (uint32_t)(v[1] >> 3), c = (uint32_t)(v[2] >> 3);
+  if (a >= (uint32_t)g.w8_n[0] || b >= (uint32_t)g.w8_n[1] || c >= (uint32_t)g.w8_n[2]) ++g_walk_outside;
+  ++g_walk_loads;
+#else
+  (void)g;
+  (void)v;
+#endif
+}
+__host__ __device__ __forceinline__ uint32_t load_walk_word(const DevGrid& g, uint32_t idx) {
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(g.walk8) + idx * 4u);
 }
 
 // The HDDA runs one step ahead of the segment logic: after a step has examined its cell (or at
@@ -574,12 +586,11 @@ __host__ __device__ __forceinline__ void hdda_pre_advance(const DevGrid& g, Lane
   synth = VPT_ZERO_RUNS && synth;
   ln.pw = synth ? ln.pw - 1u : kWalkSlow;
   if (!synth && ln.dim == 8) {
-    const uint32_t off = walk_index(g, ln.vox) * 4u;
-    ln.pw = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(g.walk8) + off);
+    ln.pw = load_walk_word(g, walk_index(g, ln.vox));
+    note_walk_load(g, ln.vox);
   }
 #if !defined(__HIP_DEVICE_COMPILE__)
   if (synth) ++g_walk_synth;
-  else if (ln.dim == 8) ++g_walk_loads;
 #endif
 }
 
@@ -630,7 +641,7 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
   const float P[3] = {px, py, pz}, D[3] = {dx, dy, dz};
   for (int a = 0; a < 3; ++a) {
     int32_t v = ((int32_t)floorf(P[a])) & (~(dim - 1));
-    ln.vox[a] = v;
+    ln.vox[a] = v - g.w8_org[a];  // relative (the walk index needs no subtraction per step)
     ln.finc[a] = (float)dim * fabsf(I[a]);
     ln.vinc[a] = dim * hdda_stp(D[a], I[a]);
     // HDDA::init: the next boundary at v + dim (I > 0) or v; none for D == 0 (selects, not branches)
@@ -642,9 +653,66 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
   return true;
 }
 
+// The general HDDA step (volume.cpp:63-70) on the pending cell at time tk, whose walk word w is not an
+// interior one: new_dim = max(8, getDim(floor(ray(time + 1.0001f)))), HDDA::update, and the majorant.
+__host__ __device__ __forceinline__ bool hdda_general(const DevGrid& g, Lane& ln, uint32_t w, float tk,
+                                                      const int32_t vc[3]) {
+  float tl = tk + 1.0001f;
+  const int32_t lx = (int32_t)floorf(ln.e[0] + ln.d[0] * tl), ly = (int32_t)floorf(ln.e[1] + ln.d[1] * tl),
+                lz = (int32_t)floorf(ln.e[2] + ln.d[2] * tl);
+  const int32_t vx = vc[0] + g.w8_org[0], vy = vc[1] + g.w8_org[1], vz = vc[2] + g.w8_org[2];  // absolute
+  const int32_t dl = (vx ^ lx) | (vy ^ ly) | (vz ^ lz);
+  if (w != kWalkSlow && dl >= 0 && dl < 8) {
+    // An edge cell (dim 8, not interior) whose lookahead point lies in the cell itself: getDim
+    // answers the cell's dim, 8 == dim, and update_current_majorant the cell's majorant.
+    ln.maj = math::as_f32(w & ~kWalkEdge);
+    return false;
+  }
+  Cell la = cell_at(g, lx, ly, lz);
+  int32_t nd = hdda_dim_of(la);
+  int32_t ax = vx, ay = vy, az = vz;
+  const bool changed = nd != ln.dim;
+  // HDDA::update(ray, dim): recomputes the voxel and the boundaries from the ray at tk
+  if (changed) {
+    ln.dim = nd;
+    const float P[3] = {ln.e[0] + ln.d[0] * tk, ln.e[1] + ln.d[1] * tk, ln.e[2] + ln.d[2] * tk};
+    int32_t V[3];
+    for (int b = 0; b < 3; ++b) {
+      V[b] = ((int32_t)floorf(P[b])) & (~(nd - 1));
+      ln.vox[b] = V[b] - g.w8_org[b];
+    }
+    ax = V[0];
+    ay = V[1];
+    az = V[2];
+    for (int b = 0; b < 3; ++b) {
+      // local_value: the direction is loop-invariant in the walk, and the compiler would compute
+      // invDir and the step signs before the loop and hold them in registers for this rare block.
+      const float db = local_value(ln.d[b]);
+      const float inv = math::rcp_rn(db);  // == the ray's invDir (begin_ray / scene_finalize)
+      const int32_t st = hdda_stp(db, inv);
+      ln.finc[b] = (float)nd * fabsf(inv);
+      ln.vinc[b] = nd * st;
+      if (st == 0) continue;
+      float n = tk + ((float)V[b] - P[b]) * inv;
+      if (st > 0) n += (float)nd * inv;
+      ln.nxt[b] = n;
+    }
+  }
+  // update_current_majorant at the (new) voxel: the lookahead cell answers it when both points lie
+  // in the same nd^3 block, saving a dependent load.  nd = 8: every query is a function of the
+  // 8^3 cell; nd = 128 / 4096: the lookahead's cell is an upper-node tile / root tile /
+  // background, which covers its whole nd^3 block.  (Here ln.dim == nd.)
+  const int32_t dx = (ax ^ lx) | (ay ^ ly) | (az ^ lz);
+  ln.maj = majorant_of((dx & ~(nd - 1)) == 0 ? la : cell_at(g, ax, ay, az));
+  return changed;
+}
+
 // One iteration of the do-while in RayMajorantIterator::next (volume.cpp:53-71), on the pending
 // cell (the HDDA was advanced into it by the previous step or by begin_ray, see hdda_pre_advance).
 // Returns true when the segment [s_t0, s_t1) with majorant s_dmaj is complete.
+// Fast path: at dim 8 in an interior cell the lookahead point (within ~1 voxel of the cell) lies in a
+// dim-8 cell, so getDim answers 8 == dim and HDDA::update is a no-op; the prefetched walk word answers
+// both "interior?" and the majorant.
 // Runs: the grid's run radii (runs8) let an interior step that keeps the majorant take the next r
 // HDDA steps without loading their cells (grids with large equal-majorant regions, e.g. C2).
 template <bool Runs = false>
@@ -655,9 +723,6 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
     ln.s_t1 = ln.T1;
     return true;
   }
-  // Fast path: at dim 8 in an interior cell the lookahead point (within ~1 voxel of the cell) lies
-  // in a dim-8 cell, so getDim answers 8 == dim and HDDA::update is a no-op; the prefetched walk word
-  // answers both "interior?" and the majorant.
   const uint32_t w = ln.pw;
   bool synth = false;  // a zero run r >= 1: the pre-advance derives the next word (kZeroRunMax)
   if ((int32_t)w >= 0) {
@@ -666,10 +731,11 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
     synth = w - 1u < kZeroRunMax;
     if (Runs && m == ln.s_dmaj) {
       // an interior cell lies in the r8 table: its run radius from the unpadded index
-      const uint32_t a = (uint32_t)((ln.vox[0] - g.r8_org[0]) >> 3), b = (uint32_t)((ln.vox[1] - g.r8_org[1]) >> 3),
-                     c = (uint32_t)((ln.vox[2] - g.r8_org[2]) >> 3);
-      for (int32_t r = (int32_t)g.runs8[math::mul24(math::mul24(a, (uint32_t)g.r8_n[1]) + b, (uint32_t)g.r8_n[2]) + c]; r > 0;
-           --r) {
+      // r8_org = w8_org + 8 kWalkPad
+      const uint32_t a = (uint32_t)((ln.vox[0] >> 3) - kWalkPad), b = (uint32_t)((ln.vox[1] >> 3) - kWalkPad),
+                     c = (uint32_t)((ln.vox[2] >> 3) - kWalkPad);
+      for (int32_t r = (int32_t)g.runs8[math::mul24(math::mul24(a, (uint32_t)g.r8_n[1]) + b, (uint32_t)g.r8_n[2]) + c];
+           r > 0; --r) {
         synth = false;  // the HDDA has left the cell w describes
         ++ln.n_dda;
         const float t = hdda_advance(ln);
@@ -681,44 +747,7 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
       }
     }
   } else {
-    // new_dim = max(8, getDim(floor(ray(time + 1.0001f))))
-    float tl = tk + 1.0001f;
-    const int32_t lx = (int32_t)floorf(ln.e[0] + ln.d[0] * tl), ly = (int32_t)floorf(ln.e[1] + ln.d[1] * tl),
-                  lz = (int32_t)floorf(ln.e[2] + ln.d[2] * tl);
-    const int32_t dl = (ln.vox[0] ^ lx) | (ln.vox[1] ^ ly) | (ln.vox[2] ^ lz);
-    if (w != kWalkSlow && dl >= 0 && dl < 8) {
-      // An edge cell (dim 8, not interior) whose lookahead point lies in the cell itself: getDim
-      // answers the cell's dim, 8 == dim, and update_current_majorant the cell's majorant.
-      ln.maj = math::as_f32(w & ~kWalkEdge);
-    } else {
-      Cell la = cell_at(g, lx, ly, lz);
-      int32_t nd = hdda_dim_of(la);
-      // HDDA::update(ray, dim)
-      if (nd != ln.dim) {
-        ln.dim = nd;
-        const float P[3] = {ln.e[0] + ln.d[0] * tk, ln.e[1] + ln.d[1] * tk, ln.e[2] + ln.d[2] * tk};
-        for (int b = 0; b < 3; ++b) ln.vox[b] = ((int32_t)floorf(P[b])) & (~(nd - 1));
-        for (int b = 0; b < 3; ++b) {
-          // local_value: the direction is loop-invariant in the walk, and the compiler would compute
-          // invDir and the step signs before the loop and hold them in registers for this rare block.
-          const float db = local_value(ln.d[b]);
-          const float inv = math::rcp_rn(db);  // == the ray's invDir (begin_ray / scene_finalize)
-          const int32_t st = hdda_stp(db, inv);
-          ln.finc[b] = (float)nd * fabsf(inv);
-          ln.vinc[b] = nd * st;
-          if (st == 0) continue;
-          float n = tk + ((float)ln.vox[b] - P[b]) * inv;
-          if (st > 0) n += (float)nd * inv;
-          ln.nxt[b] = n;
-        }
-      }
-      // update_current_majorant at the (new) voxel: the lookahead cell answers it when both points lie
-      // in the same nd^3 block, saving a dependent load.  nd = 8: every query is a function of the
-      // 8^3 cell; nd = 128 / 4096: the lookahead's cell is an upper-node tile / root tile /
-      // background, which covers its whole nd^3 block.  (Here ln.dim == nd.)
-      const int32_t dx = (ln.vox[0] ^ lx) | (ln.vox[1] ^ ly) | (ln.vox[2] ^ lz);
-      ln.maj = majorant_of((dx & ~(nd - 1)) == 0 ? la : cell_at(g, ln.vox[0], ln.vox[1], ln.vox[2]));
-    }
+    hdda_general(g, ln, w, tk, ln.vox);
   }
   hdda_pre_advance(g, ln, synth);  // the next step's advance, and its cell's walk word in flight
   if (ln.maj == ln.s_dmaj) return false;
