@@ -274,7 +274,7 @@ __global__ void vpt_majorant_trace_kernel(const DevScene* scene, float ox, float
   int n = 0;
   if (begin_ray(G, ln, o, ray_dir_setup(G, d))) {
     while (ln.s_t1 < ln.T1) {  // RayMajorantIterator::next: segments until the HDDA leaves [t0, t1]
-      ln.s_t0 = ln.s_t1;
+      begin_segment(ln);
       while (!hdda_step(G, ln)) {
       }
       if (n < max_rows) {
@@ -326,7 +326,7 @@ __global__ void vpt_tile_cost_kernel(const DevScene* scene, float* cost) {
     int steps = 0;
     float tau = 0.0f;
     while (ln.s_t1 < ln.T1 && steps < (1 << 16)) {
-      ln.s_t0 = ln.s_t1;
+      begin_segment(ln);
       bool done;
       do {
         ++steps;

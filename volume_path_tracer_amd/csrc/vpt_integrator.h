@@ -477,9 +477,9 @@ struct Lane {
   float Tn, T1;     // Tn: HDDA time of the pending cell (the one the HDDA has been advanced into)
   uint32_t pw;      // walk word of the pending cell (prefetched; kWalkSlow when not at dim 8)
   float nxt[3];
-  int32_t vox[3];   // HDDA voxel, relative to the walk table's origin (DevGrid::w8_org): vox_rel
+  int32_t vox[3];   // HDDA voxel in 8^3-cell units relative to the walk table's origin: (voxel - w8_org) / 8
   float finc[3];    // HDDA: dim * delta[axis] (the float product NanoVDB adds at every step)
-  int32_t vinc[3];  // HDDA: dim * step[axis]
+  int32_t vinc[3];  // HDDA: dim * step[axis] / 8 (cell units; every HDDA dim is a multiple of 8)
   // current majorant segment
   float s_t0, s_t1, s_dmaj;
   StencilCell temp_cell;
@@ -543,13 +543,13 @@ __host__ __device__ __forceinline__ float hdda_advance(Lane& ln) {
 inline uint64_t g_walk_outside = 0;
 #endif
 
-// Walk-table index of the 8^3 cell holding voxel v, given relative to the table's origin (Lane::vox).
+// Walk-table index of the 8^3 cell v, in cell units relative to the table's origin (Lane::vox).
 // The min() only guarantees a memory-safe address; hdda_pre_advance never asks for a cell beyond the
 // padding.  The padding is in index space, and so is the HDDA's lookahead (1.0001 along the index-space
 // ray, whose direction Ray::worldToIndexF normalises): the argument holds for every voxel size and any
 // affine map.
 __host__ __device__ __forceinline__ uint32_t walk_index(const DevGrid& g, const int32_t v[3]) {
-  const uint32_t a = (uint32_t)(v[0] >> 3), b = (uint32_t)(v[1] >> 3), c = (uint32_t)(v[2] >> 3);
+  const uint32_t a = (uint32_t)v[0], b = (uint32_t)v[1], c = (uint32_t)v[2];
   const uint32_t idx = math::mul24(math::mul24(a, (uint32_t)g.w8_n[1]) + b, (uint32_t)g.w8_n[2]) + c;
   return idx < g.w8_max ? idx : g.w8_max;
 }
@@ -557,7 +557,7 @@ __host__ __device__ __forceinline__ uint32_t walk_index(const DevGrid& g, const 
 // Host builds: count a walk-word load of the cell holding v (and whether it lies outside the table).
 __host__ __device__ __forceinline__ void note_walk_load(const DevGrid& g, const int32_t v[3]) {
 #if !defined(__HIP_DEVICE_COMPILE__)
-  const uint32_t a = (uint32_t)(v[0] >> 3), b = (uint32_t)(v[1] >> 3), c = (uint32_t)(v[2] >> 3);
+  const uint32_t a = (uint32_t)v[0], b = (uint32_t)v[1], c = (uint32_t)v[2];
   if (a >= (uint32_t)g.w8_n[0] || b >= (uint32_t)g.w8_n[1] || c >= (uint32_t)g.w8_n[2]) ++g_walk_outside;
   ++g_walk_loads;
 #else
@@ -641,9 +641,11 @@ __host__ __device__ __forceinline__ bool begin_ray(const DevGrid& g, Lane& ln, c
   const float P[3] = {px, py, pz}, D[3] = {dx, dy, dz};
   for (int a = 0; a < 3; ++a) {
     int32_t v = ((int32_t)floorf(P[a])) & (~(dim - 1));
-    ln.vox[a] = v - g.w8_org[a];  // relative (the walk index needs no subtraction per step)
+    // cell units relative to the table (v and w8_org are multiples of 8): the walk index needs no
+    // subtraction or shift per step
+    ln.vox[a] = (v - g.w8_org[a]) >> 3;
     ln.finc[a] = (float)dim * fabsf(I[a]);
-    ln.vinc[a] = dim * hdda_stp(D[a], I[a]);
+    ln.vinc[a] = (dim >> 3) * hdda_stp(D[a], I[a]);
     // HDDA::init: the next boundary at v + dim (I > 0) or v; none for D == 0 (selects, not branches)
     const float n = t0 + ((float)(I[a] > 0 ? v + dim : v) - P[a]) * I[a];
     ln.nxt[a] = D[a] == 0.0f ? 3.40282347e+38f : n;
@@ -660,7 +662,8 @@ __host__ __device__ __forceinline__ bool hdda_general(const DevGrid& g, Lane& ln
   float tl = tk + 1.0001f;
   const int32_t lx = (int32_t)floorf(ln.e[0] + ln.d[0] * tl), ly = (int32_t)floorf(ln.e[1] + ln.d[1] * tl),
                 lz = (int32_t)floorf(ln.e[2] + ln.d[2] * tl);
-  const int32_t vx = vc[0] + g.w8_org[0], vy = vc[1] + g.w8_org[1], vz = vc[2] + g.w8_org[2];  // absolute
+  // the pending cell's voxel, absolute (vc in cell units relative to the walk table)
+  const int32_t vx = (vc[0] << 3) + g.w8_org[0], vy = (vc[1] << 3) + g.w8_org[1], vz = (vc[2] << 3) + g.w8_org[2];
   const int32_t dl = (vx ^ lx) | (vy ^ ly) | (vz ^ lz);
   if (w != kWalkSlow && dl >= 0 && dl < 8) {
     // An edge cell (dim 8, not interior) whose lookahead point lies in the cell itself: getDim
@@ -679,7 +682,7 @@ __host__ __device__ __forceinline__ bool hdda_general(const DevGrid& g, Lane& ln
     int32_t V[3];
     for (int b = 0; b < 3; ++b) {
       V[b] = ((int32_t)floorf(P[b])) & (~(nd - 1));
-      ln.vox[b] = V[b] - g.w8_org[b];
+      ln.vox[b] = (V[b] - g.w8_org[b]) >> 3;
     }
     ax = V[0];
     ay = V[1];
@@ -691,7 +694,7 @@ __host__ __device__ __forceinline__ bool hdda_general(const DevGrid& g, Lane& ln
       const float inv = math::rcp_rn(db);  // == the ray's invDir (begin_ray / scene_finalize)
       const int32_t st = hdda_stp(db, inv);
       ln.finc[b] = (float)nd * fabsf(inv);
-      ln.vinc[b] = nd * st;
+      ln.vinc[b] = (nd >> 3) * st;
       if (st == 0) continue;
       float n = tk + ((float)V[b] - P[b]) * inv;
       if (st > 0) n += (float)nd * inv;
@@ -707,6 +710,14 @@ __host__ __device__ __forceinline__ bool hdda_general(const DevGrid& g, Lane& ln
   return changed;
 }
 
+// RayMajorantIterator::next's prologue for a segment that starts at the previous one's end (or the
+// clip entry): d_maj = maj (volume.cpp:54) once per segment -- the steps compare their cells against it,
+// and only set maj.
+__host__ __device__ __forceinline__ void begin_segment(Lane& ln) {
+  ln.s_t0 = ln.s_t1;
+  ln.s_dmaj = ln.maj;
+}
+
 // One iteration of the do-while in RayMajorantIterator::next (volume.cpp:53-71), on the pending
 // cell (the HDDA was advanced into it by the previous step or by begin_ray, see hdda_pre_advance).
 // Returns true when the segment [s_t0, s_t1) with majorant s_dmaj is complete.
@@ -717,12 +728,14 @@ __host__ __device__ __forceinline__ bool hdda_general(const DevGrid& g, Lane& ln
 // HDDA steps without loading their cells (grids with large equal-majorant regions, e.g. C2).
 template <bool Runs = false>
 __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
-  ln.s_dmaj = ln.maj;
   const float tk = ln.Tn;  // the step's time (HDDA::step's mT0)
   if (!(tk <= ln.T1)) {
     ln.s_t1 = ln.T1;
     return true;
   }
+  // The segment's end if this step ends it: nothing reads s_t1 while a segment grows (NEED_SEG has
+  // taken it), and tk's register is free for the pre-advance's Tn.
+  ln.s_t1 = tk;
   const uint32_t w = ln.pw;
   bool synth = false;  // a zero run r >= 1: the pre-advance derives the next word (kZeroRunMax)
   if ((int32_t)w >= 0) {
@@ -732,8 +745,8 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
     if (Runs && m == ln.s_dmaj) {
       // an interior cell lies in the r8 table: its run radius from the unpadded index
       // r8_org = w8_org + 8 kWalkPad
-      const uint32_t a = (uint32_t)((ln.vox[0] >> 3) - kWalkPad), b = (uint32_t)((ln.vox[1] >> 3) - kWalkPad),
-                     c = (uint32_t)((ln.vox[2] >> 3) - kWalkPad);
+      const uint32_t a = (uint32_t)(ln.vox[0] - kWalkPad), b = (uint32_t)(ln.vox[1] - kWalkPad),
+                     c = (uint32_t)(ln.vox[2] - kWalkPad);
       for (int32_t r = (int32_t)g.runs8[math::mul24(math::mul24(a, (uint32_t)g.r8_n[1]) + b, (uint32_t)g.r8_n[2]) + c];
            r > 0; --r) {
         synth = false;  // the HDDA has left the cell w describes
@@ -750,9 +763,7 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
     hdda_general(g, ln, w, tk, ln.vox);
   }
   hdda_pre_advance(g, ln, synth);  // the next step's advance, and its cell's walk word in flight
-  if (ln.maj == ln.s_dmaj) return false;
-  ln.s_t1 = tk;
-  return true;
+  return ln.maj != ln.s_dmaj;  // (a NaN majorant ends its segment, as the reference's ==)
 }
 
 // Walk-loop iterations between two checks of its exit condition (the ballots).  The extra
@@ -1312,7 +1323,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
           ln.sm = SM_NONE;
           env.prof(PB_NONE);
         } else {
-          ln.s_t0 = ln.s_t1;
+          begin_segment(ln);
           ln.sm = SM_STEP;
         }
       }
