@@ -293,6 +293,7 @@ struct DevScene {
   // float values the reference recomputes at every call.
   float hg_g2, hg_1pg2, hg_1mg2, hg_1pg, hg_2g, hg_inv2g, hg_num;
   float sigma_a, sigma_s, sigma_t, g_hg, le_scale, temp_scale, temp_offset;
+  float sigt_c;  // RN(sigma_t * kOvershootC): the free-flight overshoot pre-test's constant factor (SM_DRAW)
   // Wave gating of the rare states: a rare block runs when at least gate_min lanes of the wavefront
   // wait for it, or when fewer than gate_idle lanes are sampling (1/64 = always run).
   int32_t gate_min, gate_idle;
@@ -860,6 +861,7 @@ __host__ __device__ inline void scene_finalize(DevScene& S) {
   S.hg_inv2g = 1.0f / (2.0f * g);
   const float inv_4_pi = (float)(0.318309886183790671537767526745028724 / 4.0);  // float(inv_pi / 4.0)
   S.hg_num = inv_4_pi * (1.0f - g * g);
+  S.sigt_c = S.sigma_t * kOvershootC;
 }
 
 // A primary ray's real-or-null collision (worker.cpp:148-188) at the index point pi with density
@@ -1344,11 +1346,12 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         // draw only proves the overshoot with the hardware log2: a = -v_log_f32(1 - u) satisfies
         // a*ln2 <= X*(1 + 2.71*2^-24) for X = -logf(1 - u) as the exact path computes it, over every
         // 1 - u (tools/proofs/log2_bound.hip).  With kOvershootC = log2(e)*(1 + 2^-16) rounded, a >
-        // thr = ((s_t1 - s_t0)*sigma_maj*m_scale)*kOvershootC then implies RN(s_t0 + RN(RN(X/sigma_maj)
-        // /m_scale)) >= s_t1 (every rounding is covered by the 2^-16 margin; the guards keep the
-        // intermediate results normal: m_scale in [2^-26, 2^26) via rscale, s_t1 - s_t0 >= 2^-96).
+        // thr = (s_t1 - s_t0)*sigma_maj*m_scale*kOvershootC then implies RN(s_t0 + RN(RN(X/sigma_maj)
+        // /m_scale)) >= s_t1 (every rounding is covered by the 2^-16 margin, whatever the order of the
+        // four products: thr is computed as ((s_t1 - s_t0)*RN(d_maj*RN(sigma_t*kOvershootC)))*m_scale, three
+        // roundings of 2^-24 each against 2^-16; the guards keep the intermediate results normal:
+        // m_scale in [2^-26, 2^26) via rscale, s_t1 - s_t0 >= 2^-96).
         // Anything else parks in SM_EVAL, which computes the exact distance first (eval_collision).
-        const float sigma_maj = ln.s_dmaj * S.sigma_t;
         const float u = rng_uniform(ln.rng);
         if (Debug) {
           env.tally(CNT_DRAWS, 1);
@@ -1356,7 +1359,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         }
         const float y = 1 - u;
         const float D = ln.s_t1 - ln.s_t0;
-        const float thr = ((D * sigma_maj) * ln.scale) * kOvershootC;
+        const float thr = (D * (ln.s_dmaj * S.sigt_c)) * ln.scale;
         if (math::neg_log2_hw(y) > thr && D >= 0x1p-96f && ln.rscale == ln.rscale) {
           ln.sm = SM_NEED_SEG;
         } else {
