@@ -129,6 +129,11 @@ inline uint64_t g_walk_loads = 0, g_walk_synth = 0;
 // it is about to enter whenever it walks at dim 8; that cell is at most 2 cells outside the r8 table
 // (see hdda_pre_advance), so the prefetch needs no bounds test.
 constexpr int32_t kWalkPad = 2;
+// r03 step trim: the fast path's pre-advance without the dim test, s_t1 by one min, the free-flight
+// draw's 1 - u by one fma and a max (rng_one_minus_uniform).  0 = the r03v code (A/B builds).
+#ifndef VPT_STEP_TRIM
+#define VPT_STEP_TRIM 1
+#endif
 // A cells8 code whose cell has HDDA dim 8: a leaf (code >= 0) or a lower-node tile (-16 / -17).
 __host__ __device__ __forceinline__ bool cell8_dim8(int32_t code) { return code >= 0 || code == -16 || code == -17; }
 __host__ __device__ __forceinline__ int32_t cell8_code(int32_t x) {
@@ -332,15 +337,35 @@ constexpr int32_t kOnePixel = 1 << 30;
 constexpr int32_t kPixelTaken = 1 << 29;
 constexpr int32_t kPixelMask = kPixelTaken - 1;
 
-__host__ __device__ __forceinline__ float rng_uniform(uint64_t& state) {
-  uint64_t old = state;
-  state = state * 6364136223846793005ULL;
-  uint32_t rshift = (uint32_t)(old >> 61);
+// pcg32_fast's output (pcg_random.hpp xsh_rs): (uint32)((old ^ (old >> 22)) >> (22 + (old >> 61))).  On
+// the device the shifts by 22..29 take the low word of a 64-bit pair with v_alignbit_b32 (32-bit
+// funnel shifts) instead of two 64-bit shifts.
+__host__ __device__ __forceinline__ uint32_t pcg32_output(uint64_t old) {
+#if defined(__HIP_DEVICE_COMPILE__) && VPT_STEP_TRIM
+  const uint32_t lo = (uint32_t)old, hi = (uint32_t)(old >> 32);
+  const uint32_t xlo = lo ^ __builtin_amdgcn_alignbit(hi, lo, 22u), xhi = hi ^ (hi >> 22);
+  return __builtin_amdgcn_alignbit(xhi, xlo, 22u + (hi >> 29));
+#else
+  const uint32_t rshift = (uint32_t)(old >> 61);
   old ^= old >> 22;
-  uint32_t r = (uint32_t)(old >> (22 + rshift));
+  return (uint32_t)(old >> (22 + rshift));
+#endif
+}
+__host__ __device__ __forceinline__ float rng_uniform(uint64_t& state) {
+  const uint32_t r = pcg32_output(state);
+  state = state * 6364136223846793005ULL;
   float v = (float)r * 0x1p-32f;
   const float one_minus_eps = 0x1.fffffep-1f;
   return (v < one_minus_eps) ? v : one_minus_eps;  // std::min<float>(1-eps, v)
+}
+// 1 - rng_uniform(state), as the free-flight draw uses it (random.hpp:20-22: -log(1 - u)).  With
+// v = r * 2^-32 (exact), RN(1 - min(v, 1 - 2^-24)) == max(RN(1 - v), 2^-24): below 1 - 2^-24 the min is
+// v and 1 - v > 2^-24, so its rounding is >= 2^-24; at or above it both sides are 2^-24 (v may round
+// up to 1).  RN(1 - v) is one fma of the exact product.
+__host__ __device__ __forceinline__ float rng_one_minus_uniform(uint64_t& state) {
+  const uint32_t r = pcg32_output(state);
+  state = state * 6364136223846793005ULL;
+  return fmaxf(__builtin_fmaf(-(float)r, 0x1p-32f, 1.0f), 0x1p-24f);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -730,6 +755,13 @@ __host__ __device__ __forceinline__ void begin_segment(Lane& ln) {
 template <bool Runs = false>
 __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
   const float tk = ln.Tn;  // the step's time (HDDA::step's mT0)
+#if VPT_STEP_TRIM
+  // The segment's end if this step ends it (tk), or T1 when the HDDA has left [t0, t1]: one select
+  // instead of a copy on each path.  Nothing reads s_t1 while a segment grows (NEED_SEG has taken it).
+  const bool in = tk <= ln.T1;
+  ln.s_t1 = in ? tk : ln.T1;
+  if (!in) return true;
+#else
   if (!(tk <= ln.T1)) {
     ln.s_t1 = ln.T1;
     return true;
@@ -737,6 +769,7 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
   // The segment's end if this step ends it: nothing reads s_t1 while a segment grows (NEED_SEG has
   // taken it), and tk's register is free for the pre-advance's Tn.
   ln.s_t1 = tk;
+#endif
   const uint32_t w = ln.pw;
   bool synth = false;  // a zero run r >= 1: the pre-advance derives the next word (kZeroRunMax)
   if ((int32_t)w >= 0) {
@@ -763,7 +796,8 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
   } else {
     hdda_general(g, ln, w, tk, ln.vox);
   }
-  hdda_pre_advance(g, ln, synth);  // the next step's advance, and its cell's walk word in flight
+  // the next step's advance, and its cell's walk word in flight
+  hdda_pre_advance(g, ln, synth);
   return ln.maj != ln.s_dmaj;  // (a NaN majorant ends its segment, as the reference's ==)
 }
 
@@ -1352,12 +1386,15 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         // roundings of 2^-24 each against 2^-16; the guards keep the intermediate results normal:
         // m_scale in [2^-26, 2^26) via rscale, s_t1 - s_t0 >= 2^-96).
         // Anything else parks in SM_EVAL, which computes the exact distance first (eval_collision).
-        const float u = rng_uniform(ln.rng);
+#if VPT_STEP_TRIM
+        const float y = rng_one_minus_uniform(ln.rng);
+#else
+        const float y = 1 - rng_uniform(ln.rng);
+#endif
         if (Debug) {
           env.tally(CNT_DRAWS, 1);
           env.tally(CNT_RNG_DRAWS, 1);
         }
-        const float y = 1 - u;
         const float D = ln.s_t1 - ln.s_t0;
         const float thr = (D * (ln.s_dmaj * S.sigt_c)) * ln.scale;
         if (math::neg_log2_hw(y) > thr && D >= 0x1p-96f && ln.rscale == ln.rscale) {
