@@ -167,6 +167,47 @@ def request_roofline(config: str, samples_per_launch: float, avg_launch_s: float
             "request_sources": [cnt_src, ceil_src]}
 
 
+POOL_BYTES_PER_LEAF = 9216  # the stencil pool: per leaf 8 x 8 voxel rows of 9 2x2 squares (include/vpt_gpu.h)
+STRADDLE = 1.125            # L1->L2 requests per stencil piece: 1 pair in 8 straddles a 128-B line
+
+
+def interp_loglog(points, x):
+    """Log-log interpolation of [(x, y)] at x (clamped to the measured range)."""
+    import math
+
+    pts = sorted(points)
+    if x <= pts[0][0]:
+        return pts[0][1]
+    if x >= pts[-1][0]:
+        return pts[-1][1]
+    for (x0, y0), (x1, y1) in zip(pts, pts[1:]):
+        if x0 <= x <= x1:
+            f = (math.log(x) - math.log(x0)) / (math.log(x1) - math.log(x0))
+            return math.exp(math.log(y0) + f * (math.log(y1) - math.log(y0)))
+    return pts[-1][1]
+
+
+def pipe_roofline(config: str, samples_per_s_per_cu: float, stencil_entries_per_sample: float, pool_mib: float) -> dict:
+    """The vector-memory pipeline as two request classes: stencil pieces gathered from the
+    stencil pool (L2 misses: ~every one) at the measured rate of random 32-B gathers from a table of the
+    pool's size (tools/ubench/gather pool), and every other L1->L2 request (walk words, cell entries: L2
+    hits) at the measured L2-resident 4-B gather ceiling.  pipe_frac = the sum of the two classes' shares
+    of the pipeline's time, from this run's rate and stencil count, the newest committed counter pass's
+    requests per sample and the two ceiling files (all named in pipe_sources)."""
+    cnt, cnt_src = newest_profile("*_counters.json", lambda j: j.get("config") == config and not j.get("bench_args") and
+                                  j.get("derived", {}).get("l1_to_l2_requests_per_sample"))
+    ceil, ceil_src = newest_profile("*_gather_ceiling.json")
+    pool, pool_src = newest_profile("*_pool_ceiling.json")
+    if not cnt or not ceil or not pool:
+        return {"pipe_frac": None}
+    stencil_ceiling = interp_loglog([(p["table_mib"], p["entries_per_s_per_cu"]) for p in pool["points"]], pool_mib)
+    other = max(0.0, cnt["derived"]["l1_to_l2_requests_per_sample"] - STRADDLE * stencil_entries_per_sample)
+    st = stencil_entries_per_sample * samples_per_s_per_cu / stencil_ceiling
+    ot = other * samples_per_s_per_cu / ceil["ceiling_l1_to_l2_requests_per_s_per_cu"]
+    return {"pipe_frac": round(st + ot, 4), "pipe_stencil_share": round(st, 4), "pipe_other_share": round(ot, 4),
+            "pipe_pool_mib": round(pool_mib, 1), "pipe_sources": [cnt_src, ceil_src, pool_src]}
+
+
 def init_rank(args, env=None):
     """(rank, world, device, scalar device) of this process.  One process per GPU: device LOCAL_RANK
     (device 0 for --one-device, the one-GPU multi-process tests).  For world > 1 the process group is
@@ -358,8 +399,11 @@ def main():
         # (tools/profile_round.sh): a builder measurement, labelled with its file, not this run's
         pj, traffic_source = newest_profile("*_pmc.json", lambda j: j.get("config") == args.config and j.get("spp") == spp)
         traffic = pj.get("hbm_bytes_per_launch") if pj else None
-        req = request_roofline(args.config, samples_rank / (args.steps * launches_per_step), avg_launch_s,
-                               torch.cuda.get_device_properties(dev).multi_processor_count)
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        req = request_roofline(args.config, samples_rank / (args.steps * launches_per_step), avg_launch_s, cus)
+        pool_mib = (dens.leaf_count + (temp.leaf_count if temp is not None else 0)) * POOL_BYTES_PER_LEAF / 2**20
+        req.update(pipe_roofline(args.config, samples_rank / args.steps / launches_per_step / avg_launch_s / cus,
+                                 (counters["stencils"] + counters["temp_stencils"]) / samples_rank, pool_mib))
         out = {
             "metric": baseline_metric(),
             "value": round(value, 3),

@@ -65,3 +65,16 @@ def test_request_roofline_uses_the_configs_own_counter_pass():
     r = bench.request_roofline("c3", 5.3e8, 0.35, 256)
     src = r["request_sources"][0]
     assert not json.loads((Path(bench.ROOT) / src).read_text()).get("bench_args"), src
+
+
+def test_pipe_roofline_two_request_classes():
+    """pipe_frac: stencil pieces at the pool-size gather ceiling plus the other requests at the L2 ceiling,
+    from the committed counter / ceiling files; log-log interpolation between measured pool sizes."""
+    pts = [(200.0, 4.0e8), (800.0, 2.0e8)]
+    assert bench.interp_loglog(pts, 400.0) == pytest.approx(2.0e8 * 2 ** 0.5)
+    assert bench.interp_loglog(pts, 100.0) == 4.0e8 and bench.interp_loglog(pts, 1600.0) == 2.0e8
+    r = bench.pipe_roofline("c3", 5.95e6, 11.857, 797.2)
+    assert r["pipe_frac"] is not None and 0.3 < r["pipe_frac"] < 1.2, r
+    assert r["pipe_frac"] == pytest.approx(r["pipe_stencil_share"] + r["pipe_other_share"], abs=2e-4)
+    assert all(src and src.startswith("profiles/") for src in r["pipe_sources"])
+    assert bench.pipe_roofline("no-such-config", 5.95e6, 11.857, 797.2) == {"pipe_frac": None}

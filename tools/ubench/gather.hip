@@ -4,7 +4,7 @@
 // so a wavefront keeps Chains divergent loads in flight; occupancy is set with dynamic LDS.  Reports
 // loads/s per CU for table sizes from L2-resident (1.2 MiB, the C3 walk table) to HBM-resident, and
 // the memory-level parallelism (chains x waves/SIMD) the request rate saturates at.
-//   hipcc -O3 --offload-arch=gfx950 -o gather gather.hip && ./gather [calib | width]
+//   hipcc -O3 --offload-arch=gfx950 -o gather gather.hip && ./gather [calib | width | pool MiB...]
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -168,6 +168,11 @@ int main(int argc, char** argv) {
       width_rows<4>(bytes, cus, out, lds_total);
       width_rows<8>(bytes, cus, out, lds_total);
     }
+    return 0;
+  }
+  if (argc > 2 && std::string(argv[1]) == "pool") {  // 32-B entries (a stencil's piece) from tables of the given MiB
+    std::printf("%5s %5s %10s %6s %6s %10s\n", "", "bytes", "table_MiB", "chains", "waves", "Gentry/s/CU");
+    for (int a = 2; a < argc; ++a) width_rows<8>((size_t)(std::atof(argv[a]) * 1048576.0) & ~size_t(31), cus, out, lds_total);
     return 0;
   }
   const size_t sizes[] = {307200, 1u << 22, 1u << 26};  // 1.2 MiB (L2), 16 MiB (MALL), 256 MiB (HBM)
