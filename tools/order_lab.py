@@ -11,6 +11,8 @@ ap.add_argument("--config", default="c3")
 ap.add_argument("--costs", default=None)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--only", default=None)
+ap.add_argument("--regions", default=None, help="region-major orders with these region sizes (tiles), e.g. 1024,4096")
+ap.add_argument("--tails", default=None, help="with --regions: region-major curve orders ending in the cost tail of these wave counts")
 a = ap.parse_args()
 import torch
 from volume_path_tracer_amd.render import Integrator
@@ -48,6 +50,60 @@ for K in (128, 512, 2048):
     orders[f"front_top{K}_tail"] = np.concatenate([front, base[keep]])
 for tl in (auto_tail // 2, auto_tail * 2):
     orders[f"tail{tl}"] = cost_tail(rank, W, min(W, tl))
+
+
+def morton(tx, ty):
+    """Interleaved bits of (tx, ty): a Z-order curve over the tile grid."""
+    code = np.zeros_like(tx, dtype=np.int64)
+    for b in range(12):
+        code |= ((tx >> b) & 1) << (2 * b) | ((ty >> b) & 1) << (2 * b + 1)
+    return code
+
+
+def region_major(G, group_order="cost"):
+    """Regions of G tiles compact in the image (consecutive along a Z-order curve): every wave of a region
+    before the next region, so the lanes in flight trace one region's frustum through the volume and the
+    stencil pool lines they touch are reused from L2 / MALL; within a region and wave the tiles costliest
+    first (64 consecutive items = 64 different tiles: no film-atomic conflicts).  Regions costliest first
+    (group_order "cost") so the launch drains on cheap regions, or along the curve ("curve")."""
+    ntx = int(np.ceil(wl.cfg.width / wl.cfg.tile_size[0]))
+    tiles = np.arange(T)
+    z = np.argsort(morton(tiles % ntx, tiles // ntx), kind="stable")
+    groups = [z[i:i + G] for i in range(0, T, G)]
+    if group_order == "cost":
+        groups.sort(key=lambda g: -cost[g].sum() / len(g))
+    parts = []
+    for g in groups:
+        g = g[np.argsort(-cost[g], kind="stable")]
+        parts.append((np.arange(W)[:, None] * T + g[None, :]).ravel())
+    return np.concatenate(parts)
+
+
+def region_then_tail(G, tail):
+    """region_major along the curve for the first W - tail waves, then the built-in cost tail (the last `tail`
+    waves over all tiles, costliest first in groups of 64) so the launch drains on cheap jobs."""
+    ntx = int(np.ceil(wl.cfg.width / wl.cfg.tile_size[0]))
+    tiles = np.arange(T)
+    z = np.argsort(morton(tiles % ntx, tiles // ntx), kind="stable")
+    parts = []
+    for i in range(0, T, G):
+        g = z[i:i + G]
+        g = g[np.argsort(-cost[g], kind="stable")]
+        parts.append((np.arange(W - tail)[:, None] * T + g[None, :]).ravel())
+    tl = cost_tail(rank, W, tail, waves0=W - tail)
+    return np.concatenate(parts + [tl])
+
+
+if a.regions:
+    orders = {"builtin": None}
+    for G in map(int, a.regions.split(",")):
+        if a.tails:
+            for t in map(int, a.tails.split(",")):
+                orders[f"region{G}_curve_tail{t}"] = region_then_tail(G, t)
+        else:
+            orders[f"region{G}_cost"] = region_major(G, "cost")
+            orders[f"region{G}_curve"] = region_major(G, "curve")
+    orders["builtin_again"] = None
 res = {}
 for name, perm in orders.items():
     if a.only and name not in a.only.split(","):
