@@ -12,6 +12,7 @@ ap.add_argument("--costs", default=None)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--only", default=None)
 ap.add_argument("--regions", default=None, help="region-major orders with these region sizes (tiles), e.g. 1024,4096")
+ap.add_argument("--blocks", default=None, help="cost-tail orders over b x b blocks of adjacent tiles, e.g. 4,8")
 ap.add_argument("--tails", default=None, help="with --regions: region-major curve orders ending in the cost tail of these wave counts")
 a = ap.parse_args()
 import torch
@@ -94,6 +95,25 @@ def region_then_tail(G, tail):
     return np.concatenate(parts + [tl])
 
 
+def block_rank(b):
+    """Tiles grouped into b x b blocks of adjacent tiles (64 = one wavefront's fetch for b = 8), blocks by
+    descending mean estimated cost, tiles raster order within a block: a rank list for cost_tail whose
+    consecutive items are neighbouring tiles, so the lanes that fetch together trace nearby primary rays."""
+    ntx = int(np.ceil(wl.cfg.width / wl.cfg.tile_size[0]))
+    tiles = np.arange(T)
+    bx, by = (tiles % ntx) // b, (tiles // ntx) // b
+    key = by * (ntx // b + 1) + bx
+    order = np.argsort(key, kind="stable")
+    blocks = np.split(order, np.flatnonzero(np.diff(key[order])) + 1)
+    blocks.sort(key=lambda g: -cost[g].mean())
+    return np.concatenate(blocks).astype(np.int64)
+
+
+if a.blocks:
+    orders = {"builtin": None}
+    for b in map(int, a.blocks.split(",")):
+        orders[f"blocks{b}_cost_tail"] = cost_tail(block_rank(b), W, auto_tail)
+    orders["builtin_again"] = None
 if a.regions:
     orders = {"builtin": None}
     for G in map(int, a.regions.split(",")):
