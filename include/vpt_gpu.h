@@ -275,6 +275,11 @@ int vpt_gpu_majorant_trace(vpt_gpu_ctx* ctx, const float origin[3], const float 
  * the reference only in expectation and is never used for parity. */
 enum { VPT_RNG_REFERENCE = 0, VPT_RNG_PIXEL = 1 };
 int vpt_gpu_set_rng_mode(vpt_gpu_ctx* ctx, int mode);
+/* Throughput mode's work granularity: pixels of one job per work item (a lane traces them in order, each
+ * with its own stream, so the samples do not depend on it).  0 (default): the largest power of two
+ * dividing the tile area that leaves >= 32 work items per resident lane; else a power of two dividing
+ * the tile area (VPT_E_INVALID otherwise).  Applies from the next render call. */
+int vpt_gpu_set_pixel_chunk(vpt_gpu_ctx* ctx, int chunk);
 
 /* Kernel variant of density-only scenes.  The run-skipping variant takes, from an interior cell whose
  * majorant equals the segment's, the next r HDDA steps without loading their cells (r = the cell's

@@ -21,11 +21,14 @@ namespace {
 // Runs variant (run skipping) of the density-only path: -1 = the GPU's rule (run_fraction >= 1/4,
 // vpt_gpu.hip), 0 / 1 = forced (vpths_set_runs).
 int g_runs = -1;
+// Throughput mode's pixels per work item (vpt_gpu_set_pixel_chunk; vpths_set_pixel_chunk).
+uint32_t g_pixel_chunk = 1;
 struct HostEnv {
   uint64_t jid_begin, jid_count, next = 0;
   float* film;
   float* records;
   int32_t tile_area;
+  uint32_t pixel_chunk = 1;
   const uint32_t* order = nullptr;  // job order (see vpt_integrator.h ST_FETCH)
   const uint32_t* perm = nullptr;   // explicit job order (vpt_gpu_set_job_permutation)
   uint32_t order_tail_k0 = 0;
@@ -108,7 +111,9 @@ extern "C" int vpths_render_jobs_order(const vpt_configuration* cfg, const vpt_g
   S.gate_walk = 1;  // exercise the inner walk loop
   S.pixel_mode = rng_mode == VPT_RNG_PIXEL ? 1 : 0;
   S.tile_area = (uint32_t)(S.tw * S.th);
-  HostEnv env{jid_begin, S.pixel_mode ? jid_count * S.tile_area : jid_count, 0, film, records, S.tw * S.th};
+  if (S.pixel_mode && S.tile_area % g_pixel_chunk != 0) return VPT_E_INVALID;
+  HostEnv env{jid_begin, S.pixel_mode ? jid_count * S.tile_area / g_pixel_chunk : jid_count, 0, film, records, S.tw * S.th,
+              S.pixel_mode ? g_pixel_chunk : 1u};
   if (order) {
     env.order = order;
     env.order_tail_n = (uint32_t)tail_waves;
@@ -240,6 +245,7 @@ extern "C" int64_t vpths_check_walk(const vpt_grid_desc* d, int64_t* counts) {
 }
 
 extern "C" void vpths_set_runs(int on) { g_runs = on; }
+extern "C" void vpths_set_pixel_chunk(int chunk) { g_pixel_chunk = (uint32_t)chunk; }
 
 // Walk-word loads issued and walk words synthesised from zero runs since the last reset.
 extern "C" void vpths_walk_loads(uint64_t* loads, uint64_t* synth, int reset) {

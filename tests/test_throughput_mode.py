@@ -46,9 +46,32 @@ def test_device_state_machine_pixel_mode_on_host():
     np.testing.assert_allclose(f_h[..., :3], f_o[..., :3], rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("chunk", [2, 16, 64])
+def test_pixel_chunks_keep_every_pixels_stream_on_host(chunk):
+    """Work items of `chunk` pixels (vpt_gpu_set_pixel_chunk) trace the same samples as one pixel per item:
+    each pixel seeds its own stream when it starts; clipped tiles end their chunks early."""
+    import ctypes as C
+
+    import hostsim_lib as HS
+
+    wl = workload("c3", width=37, height=29, spp=2, grid_n=64)
+    dens = SynthGrid(wl.density_kind, wl.grid_n).grid()
+    jobs = wl.cfg.jobs_per_wave() * 2
+    _, r_1, c_1 = HS.render_jobs(wl.cfg, dens, None, 0, jobs, records=True, rng_mode=capi.VPT_RNG_PIXEL)
+    L = HS.lib()
+    L.vpths_set_pixel_chunk.argtypes = [C.c_int]
+    L.vpths_set_pixel_chunk(chunk)
+    try:
+        _, r_k, c_k = HS.render_jobs(wl.cfg, dens, None, 0, jobs, records=True, rng_mode=capi.VPT_RNG_PIXEL)
+    finally:
+        L.vpths_set_pixel_chunk(1)
+    assert r_k.tobytes() == r_1.tobytes()
+    assert c_k == c_1
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,n", [("c3", 64), ("c4", 64)])
-def test_gpu_pixel_mode_bit_exact(name, n):
+@pytest.mark.parametrize("name,n,chunk", [("c3", 64, 0), ("c4", 64, 0), ("c3", 64, 8), ("c4", 64, 64)])
+def test_gpu_pixel_mode_bit_exact(name, n, chunk):
     import torch
 
     from volume_path_tracer_amd.render import Integrator
@@ -58,6 +81,7 @@ def test_gpu_pixel_mode_bit_exact(name, n):
     temp = SynthGrid(2, wl.grid_n).grid() if wl.temperature else None
     it = Integrator(wl.cfg, dens, temp, device=0)
     it.set_rng_mode(capi.VPT_RNG_PIXEL)
+    it.set_pixel_chunk(chunk)
     jobs = wl.cfg.jobs_per_wave() * 2
     area = int(wl.cfg.tile_size[0] * wl.cfg.tile_size[1])
     rec = torch.full((jobs * area, 3), float("nan"), dtype=torch.float32, device=it.dev)

@@ -238,6 +238,8 @@ def lib() -> C.CDLL:
     L.vpt_gpu_majorant_trace.argtypes = [vp, fp, fp, fp, C.c_int, C.POINTER(C.c_int)]
     L.vpt_dda_trace.argtypes = [C.POINTER(GridDesc), fp, fp, vp, C.c_int, C.POINTER(C.c_int)]
     L.vpt_gpu_set_rng_mode.argtypes = [vp, C.c_int]
+    if hasattr(L, "vpt_gpu_set_pixel_chunk"):  # (A/B builds of older sources lack it; tests check the exports)
+        L.vpt_gpu_set_pixel_chunk.argtypes = [vp, C.c_int]
     L.vpt_gpu_set_run_skipping.argtypes = [vp, C.c_int]
     L.vpt_gpu_kernel_variant.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.vpt_gpu_set_job_order.argtypes = [vp, C.c_int]

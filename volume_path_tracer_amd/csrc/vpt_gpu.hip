@@ -67,6 +67,7 @@ struct KernelEnv {
   float* film;
   float* records;
   int32_t tile_area;
+  uint32_t pixel_chunk;  // throughput mode: pixels per work item (a power of two dividing tile_area; else 1)
   unsigned long long* prof_buf;  // [PB_COUNT][2] wave executions, active lanes; then [PT_COUNT] cycles
   unsigned long long* lds_prof;  // this workgroup's section cycles (LDS, VPT_PROFILE builds)
   unsigned long long* lds_counters;  // this workgroup's event counters (LDS)
@@ -430,6 +431,7 @@ struct vpt_gpu_ctx {
   int lat_wave_lanes = 0;            // 0: spread the items evenly over the grid's wavefronts
   hipStream_t stream = nullptr;
   bool use_runs = false;             // density-only kernel variant with run skipping (see create)
+  int pixel_chunk = 0;               // throughput mode: pixels per work item (0 = auto, see render)
   int grid_blocks = 0;               // resident capacity (or the set_tuning override)
   int cus = 1;                       // compute units of the device
   bool grid_user = false;            // grid_blocks set by vpt_gpu_set_tuning: use it as is
@@ -577,9 +579,26 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   vpt::KernelEnv env;
   env.jid_begin = jid_begin;
   env.jid_count = jid_count;
-  if (ctx->scene.pixel_mode) {  // work items are pixels
-    if (jid_count > UINT64_MAX / ctx->scene.tile_area) return vpt::set_error(VPT_E_INVALID, "render: job range too large");
-    env.jid_count = jid_count * ctx->scene.tile_area;
+  env.pixel_chunk = 1;
+  if (ctx->scene.pixel_mode) {  // work items are chunks of pixel_chunk pixels of one job
+    const uint64_t area = ctx->scene.tile_area;
+    if (jid_count > UINT64_MAX / area) return vpt::set_error(VPT_E_INVALID, "render: job range too large");
+    const uint64_t items = jid_count * area;
+    // One work item per pixel makes every pixel a device-wide atomic on the launch's job counter, and a
+    // wavefront's fetches then serialise there (C3: 530 M pixels, 546 ms vs 348 in the reference mode,
+    // r03zf).  Pixels are taken pixel_chunk at a time: the largest power of two dividing the tile area that
+    // still leaves >= 32 chunks per resident lane (C3 / C5: 32 pixels; C2, C1: 1 -- C2 ran 41.6 ms with 1
+    // pixel per item, 43.7 with 4, r03zg), or the vpt_gpu_set_pixel_chunk value.  Every pixel keeps its own
+    // stream: samples do not depend on it.
+    uint64_t K = 1;
+    if (ctx->pixel_chunk > 0) {
+      K = (uint64_t)ctx->pixel_chunk;
+    } else {
+      const uint64_t lanes = (uint64_t)ctx->grid_blocks * vpt::kBlockThreads;
+      while (area % (2 * K) == 0 && items / (2 * K) >= 32 * lanes) K *= 2;
+    }
+    env.pixel_chunk = (uint32_t)K;
+    env.jid_count = items / K;
   }
   env.film = film ? film : ctx->film;
   env.records = records;
@@ -838,6 +857,13 @@ int vpt_gpu_set_rng_mode(vpt_gpu_ctx* ctx, int mode) {
   ctx->scene.pixel_mode = mode == VPT_RNG_PIXEL ? 1 : 0;
   ctx->scene.tile_area = (uint32_t)(ctx->scene.tw * ctx->scene.th);
   return push_scene(ctx);
+}
+
+int vpt_gpu_set_pixel_chunk(vpt_gpu_ctx* ctx, int chunk) {
+  if (!ctx || chunk < 0 || (chunk & (chunk - 1)) != 0 || (chunk > 0 && ctx->scene.tile_area % (uint32_t)chunk != 0))
+    return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_pixel_chunk: 0 or a power of two dividing the tile area");
+  ctx->pixel_chunk = chunk;  // read by the next render's host code only: no wait
+  return VPT_OK;
 }
 
 int vpt_gpu_set_run_skipping(vpt_gpu_ctx* ctx, int mode) {

@@ -484,6 +484,7 @@ struct LaneCold {
   StencilCell dens_cell;  // the density sampler's last stencil cell (collision evaluation only)
   float Tr;               // shadow-ray transmittance (< 0: sample_Ld returns zero)
   float y_draw;           // 1 - u of a free-flight draw whose exact distance is pending (SM_EVAL)
+  uint32_t item_lo, item_hi;  // throughput mode: jid * tile_area of the lane's job (its pixels' streams)
 #ifdef VPT_JOB_LOG
   uint32_t t_start;       // diagnostic build: s_memrealtime at the job's fetch
   uint32_t job;           // and the job's index in the launch
@@ -1196,7 +1197,8 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         return;
       }
       uint32_t p = 0;
-      if (S.pixel_mode) {  // throughput mode: item = job * tile_area + pixel
+      if (S.pixel_mode) {  // throughput mode: item = job * tile_area + pixel, taken pixel_chunk at a time
+        j *= env.pixel_chunk;
         p = (uint32_t)(j % S.tile_area);
         j /= S.tile_area;
       }
@@ -1213,7 +1215,13 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       lc.t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
       uint64_t jid = env.jid_begin + j;
-      ln.rng = job_seed(S.seed, S.pixel_mode ? jid * S.tile_area + p : jid);
+      if (S.pixel_mode) {  // each pixel's stream is seeded when the pixel starts (ST_PIXEL)
+        const uint64_t base = jid * S.tile_area;
+        lc.item_lo = (uint32_t)base;
+        lc.item_hi = (uint32_t)(base >> 32);
+      } else {
+        ln.rng = job_seed(S.seed, jid);
+      }
       uint64_t tile = jid % S.T;
       lc.x0 = (int32_t)(tile % S.ntx) * S.tw;  // TileProvider::compute_tile_rect
       lc.y0 = (int32_t)(tile / S.ntx) * S.th;
@@ -1239,7 +1247,11 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       int32_t px, py;
       const int32_t one = lc.pix & kOnePixel;
       int32_t q = lc.pix & kPixelMask;
-      const int32_t end = one ? ((lc.pix & kPixelTaken) ? 0 : min(q + 1, rw * rh)) : rw * rh;
+      // Throughput mode: the lane's chunk of pixel_chunk pixels (a power of two dividing the tile area; chunk
+      // starts are multiples of it) ends at the next multiple once a pixel of it has been taken.
+      const int32_t K = (int32_t)env.pixel_chunk;
+      const int32_t end = one ? (((lc.pix & kPixelTaken) && (q & (K - 1)) == 0) ? 0 : min((q & ~(K - 1)) + K, rw * rh))
+                              : rw * rh;
       while (true) {
         if (q >= end) {
 #ifdef VPT_JOB_LOG
@@ -1255,6 +1267,8 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         lc.pix = q | (one ? (kOnePixel | kPixelTaken) : 0);
         if (!S.single_pixel_enabled || (px == S.sp_x && py == S.sp_y)) break;
       }
+      if (one)  // throughput mode: the pixel's own stream, hash(seed, jid * tile_area + pixel)
+        ln.rng = job_seed(S.seed, (((uint64_t)lc.item_hi << 32) | lc.item_lo) + (uint64_t)(q - 1));
       float jx = rng_uniform(ln.rng);
       float jy = rng_uniform(ln.rng);
       if (Debug) env.tally(CNT_RNG_DRAWS, 2);

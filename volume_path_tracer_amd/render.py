@@ -183,6 +183,11 @@ class Integrator:
         (throughput mode: one stream per pixel; matches the reference only in expectation)."""
         capi.check(capi.lib().vpt_gpu_set_rng_mode(self.h, int(mode)), "vpt_gpu_set_rng_mode")
 
+    def set_pixel_chunk(self, chunk: int) -> None:
+        """Throughput mode: pixels per work item (0 = auto; else a power of two dividing the tile area).
+        Samples never depend on it."""
+        capi.check(capi.lib().vpt_gpu_set_pixel_chunk(self.h, int(chunk)), "vpt_gpu_set_pixel_chunk")
+
     def set_run_skipping(self, mode: int) -> None:
         """-1: the creation-time choice; 0 / 1: force the run-skipping kernel variant off / on."""
         capi.check(capi.lib().vpt_gpu_set_run_skipping(self.h, int(mode)), "vpt_gpu_set_run_skipping")
