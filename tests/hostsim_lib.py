@@ -18,6 +18,9 @@ def lib():
     global _L
     if _L is None:
         subprocess.run(["make", "-s", "-C", str(NATIVE)], check=True)
+        # hipcc links the host simulator against libamdhip64: torch's HIP runtime must be the process's
+        # one (see volume_path_tracer_amd/capi.py lib())
+        import torch  # noqa: F401
         L = C.CDLL(str(LIB))
         cfgp, gp, fp = C.POINTER(Configuration), C.POINTER(GridDesc), C.POINTER(C.c_float)
         L.vpths_render_jobs.argtypes = [cfgp, gp, gp, fp, C.c_uint64, C.c_uint64, fp, fp, C.POINTER(Counters)]

@@ -180,3 +180,31 @@ def test_drain_from_nvdb_file_with_tiles_at_every_level(tmp_path):
     f_o, _, c = O.render_jobs(wl.cfg, O.OracleGrid(g, fix_majorants=True), None, 0, wl.cfg.jobs_per_wave() * waves)
     assert c["density_evals"] > 1000
     np.testing.assert_allclose(film[..., :3], f_o[..., :3], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.spawns
+def test_library_before_torch_keeps_one_hip_runtime():
+    """A process that reaches the C ABI (capi.lib()) before it imports torch still ends up with a single HIP
+    runtime -- torch's -- and torch sees the GPU (r03zl: /opt/rocm's runtime loaded first made torch's second
+    ROCr find no GPU on some boxes).  Run in a child process, the way a user script starts."""
+    import subprocess
+    import sys
+
+    code = ("import sys; sys.path.insert(0, '.')\n"
+            "from volume_path_tracer_amd.scenes import SynthGrid, workload\n"
+            "wl = workload('c3', width=16, height=16, spp=1, grid_n=32)\n"
+            "dens = SynthGrid(wl.density_kind, wl.grid_n).grid()\n"
+            "import torch\n"
+            "from volume_path_tracer_amd.render import Integrator\n"
+            "it = Integrator(wl.cfg, dens, None, device=0)\n"
+            "it.render_jobs(0, wl.cfg.jobs_per_wave())\n"
+            "torch.cuda.synchronize()\n"
+            "libs = {l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}\n"
+            "print('runtimes', len(libs), 'samples', it.counters()['samples'])\n")
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "runtimes 1 samples 256" in r.stdout, r.stdout

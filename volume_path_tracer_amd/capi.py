@@ -203,6 +203,12 @@ def lib() -> C.CDLL:
         return _lib
     if not LIB_PATH.exists():
         raise RuntimeError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc, gfx950)")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 / libhsa-runtime64.  Loaded first,
+    # they also serve this library (same sonames), and the device memory torch allocates is the memory the
+    # kernels see.  Loaded after /opt/rocm's (this library's link-time runtime), torch's ROCr opens the GPU a
+    # second time and, on some boxes, finds none ("No HIP GPUs are available"; r03zl,
+    # tools/probe_hip_init2.py).  So torch is imported before the library, whatever the caller imported.
+    import torch  # noqa: F401
     L = C.CDLL(str(LIB_PATH))
     cfgp, gridp = C.POINTER(Configuration), C.POINTER(GridDesc)
     fp, vp = C.POINTER(C.c_float), C.c_void_p
