@@ -16,7 +16,8 @@ WORLD_SIZE is unset, by starting torch.distributed.run itself before anything to
   * for N > 1 the line also carries `scaling_strong`: the C3 frame (256 waves) and the C5 frame
     (BASELINE.json configs[4], 3840x2160 at 1024 spp) each dealt across the N ranks and timed the same
     way (barrier + synchronize, max over ranks, film all-reduce inside the step): the strong scaling
-    that north_star's ">= 6x at 8 GPUs" asks about (`--strong-configs`, '' to skip);
+    that north_star's ">= 6x at 8 GPUs" asks about (`--strong-configs`, '' to skip); and the C3 frame in
+    the throughput mode ("c3:pixel": per-pixel streams, reported separately, never the headline);
   * `--config c5 --mode strong --gpus 8` makes the C5 frame the main measurement.
 
 The JSON line also carries:
@@ -299,18 +300,26 @@ def strong_scaling(configs, dens, rank, world, dev, sdev, steps, warmup, stream)
     from volume_path_tracer_amd.render import Integrator
     from volume_path_tracer_amd.scenes import workload
 
+    from volume_path_tracer_amd import capi
+
     out = {}
     for name in configs:
-        wl = workload(name)
+        base, _, mode = name.partition(":")  # "c3:pixel" = the throughput mode's per-pixel streams
+        if mode not in ("", "pixel"):
+            raise ValueError(f"--strong-configs: unknown mode in {name}")
+        wl = workload(base)
         if wl.temperature or wl.density_kind != 1 or wl.grid_n != 512:
             raise ValueError(f"--strong-configs: {name} does not share the 512^3 cloud stand-in")
         it = Integrator(wl.cfg, dens, None, device=dev.index)
+        if mode == "pixel":
+            it.set_rng_mode(capi.VPT_RNG_PIXEL)
         elapsed = max_over_ranks(timed_frames(it, rank, world, wl.spp, "strong", steps, warmup, stream), world, sdev)
         samples = sum_over_ranks(it.counters()["samples"], world, sdev)
         film = it.film_host()
         assert (film[..., 3] == D.total_samples_per_pixel(world, wl.spp, "strong")).all(), "sample-count channel mismatch"
         assert samples == wl.cfg.width * wl.cfg.height * wl.spp * steps, samples
-        out[name] = {"workload": f"{name}: {wl.cfg.width}x{wl.cfg.height}, {wl.spp} spp per image, dealt over {world} GPUs",
+        out[name] = {"workload": f"{base}: {wl.cfg.width}x{wl.cfg.height}, {wl.spp} spp per image, dealt over {world} GPUs"
+                                 + (" (throughput mode: per-pixel streams, not the reference's samples)" if mode else ""),
                      "ms_per_step": round(elapsed / steps * 1e3, 3), "value": round(samples / elapsed / 1e6, 3),
                      "unit": "Msamples/s", "steps": steps, "warmup": warmup}
         del it
@@ -327,8 +336,9 @@ def main():
     ap.add_argument("--grid-n", type=int, default=None, help="experiments: override the stand-in grid's size n^3")
     ap.add_argument("--mode", choices=["weak", "strong"], default="weak",
                     help="weak: each rank renders its own spp waves; strong: the spp waves are dealt across ranks")
-    ap.add_argument("--strong-configs", default="c3,c5",
-                    help="N > 1: configs whose whole frame is also timed dealt across the ranks ('' = none)")
+    ap.add_argument("--strong-configs", default="c3,c5,c3:pixel",
+                    help="N > 1: configs whose whole frame is also timed dealt across the ranks ('' = none; "
+                         "':pixel' = in the throughput mode)")
     ap.add_argument("--rng-mode", choices=["reference", "pixel"], default="reference",
                     help="pixel = throughput mode (per-pixel streams; not the reference's samples)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

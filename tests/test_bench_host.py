@@ -52,6 +52,8 @@ def test_strong_scaling_configs_share_the_cloud():
     """--strong-configs only accepts frames of the 512^3 cloud (the grid is built once)."""
     with pytest.raises(ValueError, match="c4"):
         bench.strong_scaling(["c4"], None, 0, 2, torch.device("cuda", 0), torch.device("cpu"), 1, 0, None)
+    with pytest.raises(ValueError, match="unknown mode"):
+        bench.strong_scaling(["c3:fast"], None, 0, 2, torch.device("cuda", 0), torch.device("cpu"), 1, 0, None)
 
 
 def test_request_roofline_uses_the_configs_own_counter_pass():

@@ -81,7 +81,7 @@ def test_bench_gpus2_spawns_two_ranks(tmp_path):
     assert_hip_untouched()
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
-                        "--spp", "2", "--no-cpu-baseline", "--backend", "gloo", "--one-device", "--strong-configs", "c3"],
+                        "--spp", "2", "--no-cpu-baseline", "--backend", "gloo", "--one-device", "--strong-configs", "c3,c3:pixel"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
@@ -89,6 +89,8 @@ def test_bench_gpus2_spawns_two_ranks(tmp_path):
     # and the strong-scaling record: the whole C3 frame dealt over the 2 ranks, timed the same way
     s = line["scaling_strong"]["c3"]
     assert s["value"] > 0 and s["ms_per_step"] > 0 and "1920x1080, 256 spp" in s["workload"]
+    p = line["scaling_strong"]["c3:pixel"]  # the same frame in the throughput mode, labelled as such
+    assert p["value"] > 0 and "throughput mode" in p["workload"]
     # WORLD_SIZE that disagrees with --gpus is an error
     env2 = dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r2 = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1"], cwd=ROOT, env=env2,
