@@ -1,3 +1,6 @@
+# r03zg record: parity of the chunked throughput mode, reference-mode A/B against the previous build
+# (libvpt_prev.so = the sources before the change, built with `python -m volume_path_tracer_amd.build --name=libvpt_prev.so`
+# from a checkout of them), and throughput-mode frames of C1 / C2 / C3.
 set -o pipefail
 O=gpurun_out/r03zg; mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_throughput_mode.py tests/test_gpu_production.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -20 $O/pytest.log; exit 1; }
