@@ -13,6 +13,16 @@
 
 #include "vpt_oracle.h"
 
+// Mutation builds (test infrastructure for the scattering anchor, tests/test_analytic_scatter.py,
+// which must reject each; `make mutants` builds build/libvpt_oracle_mut<N>.so):
+//   1  NEE phase with pbrt's sign (den = 1 + g^2 - 2g w.wi instead of utils.hpp:62's + with the forward w)
+//   2  HG sampling about -w (pbrt's minus sign restored, random.hpp:64)
+//   3  one depth increment per scatter (worker.cpp:169's depth++ dropped)
+//   4  environment light only on escape (not on the depth-bound exit, worker.cpp:130,198-200)
+#ifndef VPTO_MUTANT
+#define VPTO_MUTANT 0
+#endif
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -569,6 +579,7 @@ V3 sample_henyey_greenstein(V3 w, float u0, float u1, float g) {  // random.hpp:
     cos_theta = 1 - 2 * u0;
   else
     cos_theta = 1.0f / (2.0f * g) * (1.0f + g2 - std::pow((1.0f - g2) / (1.0f + g - 2.0f * g * u0), 2.0f));
+  if (VPTO_MUTANT == 2) cos_theta = -cos_theta;
   float sin_theta = std::sqrt(std::max(0.0f, 1.0f - std::pow(cos_theta, 2.0f)));
   float phi = 2.0f * 3.14159274f * u1;  // 2.0f * float(pi) * u
   float sc = std::clamp(sin_theta, -1.0f, 1.0f);
@@ -758,7 +769,7 @@ V3 sample_Ld(const Scene& S, Rng& rng, V3 pos, V3 w, vpt_counters* cnt) {  // wo
       if (T_ray <= 0.0f) return v3(0, 0, 0);
     }
   }
-  float p = henyey_greenstein(eigen_dot(w, wi), VP.henyey_greenstein_g);
+  float p = henyey_greenstein(VPTO_MUTANT == 1 ? -eigen_dot(w, wi) : eigen_dot(w, wi), VP.henyey_greenstein_g);
   return v3(p * T_ray * Li.x, p * T_ray * Li.y, p * T_ray * Li.z);
 }
 
@@ -829,10 +840,14 @@ void run_job(const Scene& S, uint64_t jid, float* film, float* records, uint64_t
       if (log) log->log(jid, pix, VPT_EV_NEW_RAY, &r_o, &r_d, 0.0f);
       V3 L = v3(0, 0, 0);
       bool terminated = false;
+      bool escaped = false;  // mutant 4 only
       for (unsigned int depth = 0; depth < P.max_depth; ++depth) {
         bool scattered = false;
         NRay ir(v3(0, 0, 0), v3(1, 0, 0));
-        if (!volume_intersect(*S.density, r_o, r_d, ir)) break;
+        if (!volume_intersect(*S.density, r_o, r_d, ir)) {
+          escaped = true;
+          break;
+        }
         RayMajorantIterator it(ir, S.density);
         MajorantTransmittanceSampler sampler(it, rng, S.density, sigma_t, cnt);
         MediumProperties props;
@@ -856,7 +871,7 @@ void run_job(const Scene& S, uint64_t jid, float* film, float* records, uint64_t
             if (log) log->log(jid, pix, VPT_EV_NULL, nullptr, nullptr, 0.0f);
             continue;
           } else if (ev == ScatterEvent::Scatter) {
-            if (depth++ >= P.max_depth) {
+            if ((VPTO_MUTANT == 3 ? depth : depth++) >= P.max_depth) {
               if (log) log->log(jid, pix, VPT_EV_SCATTER_TERMINATED, nullptr, nullptr, 0.0f);
               terminated = true;
               break;
@@ -878,9 +893,12 @@ void run_job(const Scene& S, uint64_t jid, float* film, float* records, uint64_t
             break;
           }
         }
-        if (!scattered) break;
+        if (!scattered) {
+          escaped = !terminated;
+          break;
+        }
       }
-      if (!terminated) {
+      if (!terminated && (VPTO_MUTANT != 4 || escaped)) {
         L = add(L, v3(P.infinite_light_xyz[0] * P.infinite_light_multiplier,
                       P.infinite_light_xyz[1] * P.infinite_light_multiplier,
                       P.infinite_light_xyz[2] * P.infinite_light_multiplier));

@@ -233,3 +233,106 @@ def optical_depth_chunk(o, d):
         p = o + (mid + half * x)[..., None] * d[:, None, :]
         tau += (w * half * ind * trilinear(p)).sum(axis=1)
     return tau
+
+
+# ---- the constant cube and the single-scatter expectation ----------------------------
+# Density 1 on index voxels [0, 127]^3, background 0, world = index - 64, voxel size 1.  NanoVDB's
+# trilinear field inside the clip box [0, 128]^3 (CoordBBox max + 1, volume.cpp:83) is
+# prod_axes clip(128 - p, 0, 1): 1 up to 127, the half-voxel ramp to 0 at the max + 1 face.
+CUBE_HI = 128.0
+GL3 = (np.array([-np.sqrt(0.6), 0.0, np.sqrt(0.6)]), np.array([5.0, 8.0, 5.0]) / 9.0)
+
+
+def cube_density(p):
+    return np.clip(CUBE_HI - p, 0.0, 1.0).prod(axis=-1)
+
+
+def cube_chord(o, d):
+    """Ray::clip against [0, 128]^3 (slab test): (t_enter, t_exit) per row; t_exit < t_enter = miss."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        inv = 1.0 / d
+        ta, tb = (0.0 - o) * inv, (CUBE_HI - o) * inv
+        t0 = np.nanmax(np.minimum(ta, tb), axis=-1)
+        t1 = np.nanmin(np.maximum(ta, tb), axis=-1)
+    return t0, t1
+
+
+def cube_od(o, d, ta, tb):
+    """Integral of the cube's density along o + t d for t in [ta, tb] (clipped to the box), exact: the
+    integrand is a polynomial of degree <= 3 between the ramp entries (an axis crossing 127), so
+    3-point Gauss-Legendre per piece is exact.  o, d: [n, 3] (or broadcastable); ta, tb: [n]."""
+    o, d = np.broadcast_arrays(np.asarray(o, np.float64), np.asarray(d, np.float64))
+    c0, c1 = cube_chord(o, d)
+    a = np.maximum(ta, c0)
+    b = np.maximum(np.minimum(tb, c1), a)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        br = (CUBE_HI - 1.0 - o) / d
+    br = np.where(np.isfinite(br), br, a[:, None])
+    pts = np.sort(np.concatenate([a[:, None], np.clip(br, a[:, None], b[:, None]), b[:, None]], axis=1), axis=1)
+    tau = np.zeros(o.shape[0])
+    for k in range(pts.shape[1] - 1):
+        lo, hi = pts[:, k], pts[:, k + 1]
+        half, mid = 0.5 * (hi - lo), 0.5 * (hi + lo)
+        for x, w in zip(*GL3):
+            tau += w * half * cube_density(o + (mid + half * x)[:, None] * d)
+    return tau
+
+
+def hg_reference(cos_wwi, g):
+    """henyey_greenstein(w.dot(wi), g) as the reference evaluates it in NEE: den = 1 + g^2 + 2 g c with
+    the FORWARD ray direction w (utils.hpp:61-66, worker.cpp:88) -- pbrt's phase with the sign mirrored."""
+    den = 1.0 + g * g + 2.0 * g * cos_wwi
+    return (1.0 - g * g) / (4.0 * np.pi * den * np.sqrt(den))
+
+
+def hg_cos_cdf(mu, g):
+    """CDF of cos(theta) between the incoming direction w and the sampled one under
+    sample_henyey_greenstein (random.hpp:56-84): local z = w and cos = (1 + g^2 - ((1 - g^2) /
+    (1 + g - 2 g u))^2) / (2 g), i.e. p(mu) = (1 - g^2) / (2 (1 + g^2 - 2 g mu)^1.5), forward-peaked
+    (mean g) for g > 0."""
+    mu = np.asarray(mu, np.float64)
+    return (1.0 - g * g) / (2.0 * g) * (1.0 / np.sqrt(1.0 + g * g - 2.0 * g * mu) - 1.0 / (1.0 + g))
+
+
+def single_scatter(o, w, wi, sigma_s, sub=48, npts=8, t_shadow0=1e-5):
+    """For camera rays o + t w (index space, |w| = 1) through the cube with sigma_a = 0:
+    (I, tau) with tau the chord's optical depth / sigma_s and
+
+        I = integral over the chord of sigma_s rho(t) exp(-sigma_s tau(t0, t)) exp(-sigma_s tau_sh(x(t))) dt,
+
+    the probability-weighted shadow transmittance of the first real collision (delta tracking's
+    first-scatter density, the shadow ray's expected ratio-tracking-with-RR weight, worker.cpp:52-90).
+    tau_sh(x) is the optical depth from x along wi (from t = 1e-5, volume.cpp:79-80) to the box exit.
+    The chord is split at the ramp entries and each piece into `sub` intervals of `npts`-point
+    Gauss-Legendre (the integrand is smooth there up to the kinks of tau_sh, which are second order)."""
+    o = np.asarray(o, np.float64)
+    w = np.asarray(w, np.float64)
+    n = w.shape[0]
+    t0, t1 = cube_chord(np.broadcast_to(o, w.shape), w)
+    t0 = np.maximum(t0, 0.0)
+    hit = t1 > t0
+    t1 = np.where(hit, t1, t0)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        br = (CUBE_HI - 1.0 - o) / w
+    br = np.where(np.isfinite(br), br, t0[:, None])
+    edges = np.sort(np.concatenate([t0[:, None], np.clip(br, t0[:, None], t1[:, None]), t1[:, None]], axis=1), axis=1)
+    gx, gw = np.polynomial.legendre.leggauss(npts)
+    # nodes: [n, pieces, sub, npts]
+    lo, hi = edges[:, :-1], edges[:, 1:]
+    s = np.arange(sub)
+    a = lo[..., None] + (hi - lo)[..., None] * s / sub
+    h = ((hi - lo) / sub)[..., None]
+    t = (a + 0.5 * h)[..., None] + (0.5 * h)[..., None] * gx
+    wt = np.broadcast_to((0.5 * h)[..., None] * gw, t.shape)
+    t, wt = t.reshape(n, -1), wt.reshape(n, -1)
+    m = t.shape[1]
+    x = o + t[..., None] * w[:, None, :]                                   # [n, m, 3]
+    rho = cube_density(x)
+    tau_cam = cube_od(np.broadcast_to(o, (n * m, 3)), np.repeat(w, m, axis=0), np.repeat(t0, m),
+                      t.reshape(-1)).reshape(n, m)
+    wi = np.asarray(wi, np.float64)
+    tau_sh = cube_od(x.reshape(-1, 3), np.broadcast_to(wi, (n * m, 3)), np.full(n * m, t_shadow0),
+                     np.full(n * m, np.inf)).reshape(n, m)
+    I = (wt * sigma_s * rho * np.exp(-sigma_s * (tau_cam + tau_sh))).sum(axis=1)
+    tau = cube_od(np.broadcast_to(o, (n, 3)), w, t0, t1)
+    return np.where(hit, I, 0.0), np.where(hit, tau, 0.0)

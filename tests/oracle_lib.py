@@ -17,19 +17,32 @@ ORACLE_DIR = ROOT / "oracle"
 ORACLE_LIB = ORACLE_DIR / "build" / "libvpt_oracle.so"
 
 _L = None
+_MUT: dict = {}
 
 
 def build_oracle() -> None:
     subprocess.run(["make", "-s", "-C", str(ORACLE_DIR), "build/libvpt_oracle.so"], check=True)
 
 
-def lib() -> C.CDLL:
+def lib(mutant: int = 0) -> C.CDLL:
+    """The oracle library; `mutant` 1-4 loads a mutation build (oracle/vpt_oracle.cpp's VPTO_MUTANT),
+    used only to show that the scattering anchor rejects each mutation."""
     global _L
+    if mutant:
+        if mutant not in _MUT:
+            path = ORACLE_DIR / "build" / f"libvpt_oracle_mut{mutant}.so"
+            subprocess.run(["make", "-s", "-C", str(ORACLE_DIR), f"build/{path.name}"], check=True)
+            _MUT[mutant] = _bind(C.CDLL(str(path)))
+        return _MUT[mutant]
     if _L is not None:
         return _L
     if not ORACLE_LIB.exists():
         build_oracle()
-    L = C.CDLL(str(ORACLE_LIB))
+    _L = _bind(C.CDLL(str(ORACLE_LIB)))
+    return _L
+
+
+def _bind(L: C.CDLL) -> C.CDLL:
     fp, u32p = C.POINTER(C.c_float), C.POINTER(C.c_uint32)
     cfgp, gridp, vp = C.POINTER(Configuration), C.POINTER(GridDesc), C.c_void_p
     L.vpto_hash.argtypes = [C.c_uint64, C.c_uint64]
@@ -71,7 +84,6 @@ def lib() -> C.CDLL:
     L.vpto_majorant_trace.restype = C.c_int
     L.vpto_dda_trace.argtypes = [vp, fp, fp, vp, C.c_int]
     L.vpto_dda_trace.restype = C.c_int
-    _L = L
     return L
 
 
@@ -82,11 +94,12 @@ def fptr(a):
 class OracleGrid:
     """NanoVDB-semantics tree inside the oracle, built from a Grid/GridDesc."""
 
-    def __init__(self, grid: Grid, fix_majorants: bool = True):
+    def __init__(self, grid: Grid, fix_majorants: bool = True, L: C.CDLL | None = None):
         self.grid = grid
-        self.h = lib().vpto_grid_create(C.byref(grid.desc))
+        self.L = L or lib()
+        self.h = self.L.vpto_grid_create(C.byref(grid.desc))
         if fix_majorants:
-            lib().vpto_grid_fix_majorants(self.h)
+            self.L.vpto_grid_fix_majorants(self.h)
 
     def leaf_max(self) -> np.ndarray:
         out = np.zeros(self.grid.leaf_count, np.float32)
@@ -104,7 +117,7 @@ class OracleGrid:
 
     def __del__(self):
         try:
-            lib().vpto_grid_destroy(self.h)
+            self.L.vpto_grid_destroy(self.h)
         except Exception:
             pass
 
@@ -128,6 +141,8 @@ def blackbody_table(cie=None, yint=None) -> np.ndarray:
 
 def render_jobs(cfg: Configuration, density: OracleGrid, temperature: OracleGrid | None, jid_begin: int,
                 jid_count: int, records: bool = False, bb=None):
+    """Serial oracle render of jobs [jid_begin, jid_begin + jid_count), with the library `density`
+    was built by (a mutation build's grids render through that build)."""
     cie, yint = load_cie()
     if bb is None:
         bb = blackbody_table(cie, yint)
@@ -136,7 +151,7 @@ def render_jobs(cfg: Configuration, density: OracleGrid, temperature: OracleGrid
     tile_area = int(cfg.tile_size[0] * cfg.tile_size[1])
     rec = np.full((jid_count * tile_area, 3), np.nan, np.float32) if records else None
     cnt = Counters()
-    rc = lib().vpto_render_jobs(C.byref(cfg), density.h, temperature.h if temperature else None, fptr(bb),
+    rc = density.L.vpto_render_jobs(C.byref(cfg), density.h, temperature.h if temperature else None, fptr(bb),
                                 fptr(cie), C.c_float(yint), jid_begin, jid_count, fptr(film),
                                 fptr(rec) if rec is not None else None, C.byref(cnt))
     assert rc == 0
@@ -176,7 +191,7 @@ def render_jobs_events(cfg: Configuration, density: OracleGrid, temperature: Ora
     film = np.zeros((cfg.height, cfg.width, 4), np.float32)
     ev = np.zeros(capacity, EVENT_DTYPE)
     n = C.c_uint64()
-    rc = lib().vpto_render_jobs_events(C.byref(cfg), density.h, temperature.h if temperature else None, fptr(bb),
+    rc = density.L.vpto_render_jobs_events(C.byref(cfg), density.h, temperature.h if temperature else None, fptr(bb),
                                        fptr(cie), C.c_float(yint), jid_begin, jid_count, fptr(film),
                                        ev.ctypes.data_as(C.c_void_p), capacity, C.byref(n))
     assert rc == 0 and n.value <= capacity, (rc, n.value)
