@@ -255,11 +255,12 @@ def sum_over_ranks(x: int, world: int, sdev) -> int:
     return int(t.item())
 
 
-def timed_frames(it, rank, world, spp, mode, steps, warmup, stream, launch_ms=None):
+def timed_frames(it, rank, world, spp, mode, steps, warmup, stream, launch_ms=None, reduce=True):
     """`warmup` untimed then `steps` timed frames (this rank's share of the spp waves, then the film
-    all-reduce), bracketed by a barrier and torch.cuda.synchronize() on both sides; returns the MAX
-    over ranks of the timed region (seconds).  launch_ms collects HIP-event pairs around each frame's
-    kernel launches (on the launch stream)."""
+    all-reduce), bracketed by a barrier and torch.cuda.synchronize() on both sides; returns this rank's
+    timed region (seconds; the caller takes the MAX over ranks).  launch_ms collects HIP-event pairs
+    around each frame's kernel launches (on the launch stream).  world = 1 with reduce=False times one
+    rank alone (no collective: the other ranks are not in the step)."""
     import torch
     import torch.distributed as dist
 
@@ -274,7 +275,8 @@ def timed_frames(it, rank, world, spp, mode, steps, warmup, stream, launch_ms=No
         ev1.record(stream)
         if timed and launch_ms is not None:
             launch_ms.append((ev0, ev1))
-        D.reduce_film(it.film)
+        if reduce:
+            D.reduce_film(it.film)
 
     for _ in range(warmup):
         step(False)
@@ -292,15 +294,22 @@ def timed_frames(it, rank, world, spp, mode, steps, warmup, stream, launch_ms=No
     return time.perf_counter() - t_start
 
 
+ALONE_BIG_SAMPLES = 1e9  # frames this large (C5: 8.5e9 samples, ~5 s on one GPU) are timed alone at 1 + 1 frames
+
+
 def strong_scaling(configs, dens, rank, world, dev, sdev, steps, warmup, stream):
     """For N > 1: each config's whole frame (its spp waves) dealt across the N ranks (distributed
     "strong" ranges), timed like the main loop -- the work the north_star's "scaling at 8 GPUs" means
-    (C3: the headline frame; C5: BASELINE's 8-GPU configuration, 3840x2160 at 1024 spp)."""
+    (C3: the headline frame; C5: BASELINE's 8-GPU configuration, 3840x2160 at 1024 spp, on which the
+    ">= 6x at 8 GPUs" target is judged).  Then the same whole frame on rank 0's GPU alone, timed the same
+    way while the other ranks wait at a barrier (1 warmup + 1 step for frames of >= 1e9 samples), so the
+    record carries its own speedup_vs_1gpu = t(1 GPU) / t(N GPUs) and efficiency = speedup / N."""
+    import torch.distributed as dist
+
+    from volume_path_tracer_amd import capi
     from volume_path_tracer_amd import distributed as D
     from volume_path_tracer_amd.render import Integrator
     from volume_path_tracer_amd.scenes import workload
-
-    from volume_path_tracer_amd import capi
 
     out = {}
     for name in configs:
@@ -318,10 +327,24 @@ def strong_scaling(configs, dens, rank, world, dev, sdev, steps, warmup, stream)
         film = it.film_host()
         assert (film[..., 3] == D.total_samples_per_pixel(world, wl.spp, "strong")).all(), "sample-count channel mismatch"
         assert samples == wl.cfg.width * wl.cfg.height * wl.spp * steps, samples
-        out[name] = {"workload": f"{base}: {wl.cfg.width}x{wl.cfg.height}, {wl.spp} spp per image, dealt over {world} GPUs"
-                                 + (" (throughput mode: per-pixel streams, not the reference's samples)" if mode else ""),
-                     "ms_per_step": round(elapsed / steps * 1e3, 3), "value": round(samples / elapsed / 1e6, 3),
-                     "unit": "Msamples/s", "steps": steps, "warmup": warmup}
+        frame = wl.cfg.width * wl.cfg.height * wl.spp
+        s1, w1 = (1, 1) if frame >= ALONE_BIG_SAMPLES else (steps, warmup)
+        dist.barrier()
+        alone = None
+        if rank == 0:
+            alone = timed_frames(it, 0, 1, wl.spp, "strong", s1, w1, stream, reduce=False)
+            film = it.film_host()
+            assert (film[..., 3] == wl.spp).all(), "sample-count channel mismatch (1-GPU frame)"
+        dist.barrier()
+        rec = {"workload": f"{base}: {wl.cfg.width}x{wl.cfg.height}, {wl.spp} spp per image, dealt over {world} GPUs"
+                           + (" (throughput mode: per-pixel streams, not the reference's samples)" if mode else ""),
+               "ms_per_step": round(elapsed / steps * 1e3, 3), "value": round(samples / elapsed / 1e6, 3),
+               "unit": "Msamples/s", "steps": steps, "warmup": warmup}
+        if alone is not None:
+            t1, tn = alone / s1, elapsed / steps
+            rec.update(one_gpu_ms_per_step=round(t1 * 1e3, 3), one_gpu_steps=s1, one_gpu_warmup=w1,
+                       speedup_vs_1gpu=round(t1 / tn, 3), efficiency=round(t1 / tn / world, 4))
+        out[name] = rec
         del it
     return out
 
@@ -341,6 +364,9 @@ def main():
                          "':pixel' = in the throughput mode)")
     ap.add_argument("--rng-mode", choices=["reference", "pixel"], default="reference",
                     help="pixel = throughput mode (per-pixel streams; not the reference's samples)")
+    ap.add_argument("--latency-kernel", choices=["auto", "off", "on"], default="auto",
+                    help="the latency kernel (cold lane state in VGPRs): auto = for launches that fill at most its "
+                         "resident grid (C1, C2, small shares); off / on force it (A/B runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work (3 runs)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
@@ -374,8 +400,10 @@ def main():
     if args.rng_mode == "pixel":
         from volume_path_tracer_amd import capi
         it.set_rng_mode(capi.VPT_RNG_PIXEL)
+    lat_mode = {"auto": -1, "off": 0, "on": 1}[args.latency_kernel]
+    it.set_latency_kernel(lat_mode)
     log(f"[rank {rank}] grids ready in {time.time() - t0:.1f}s: {dens.leaf_count} leaves, "
-        f"launch {it.launch_info()}")
+        f"launch {it.launch_info()}, latency kernel {it.latency_kernel_info()}")
 
     spp = wl.spp
     ranges = D.rank_job_ranges(rank, world, spp, it.jobs_per_wave, args.mode)
@@ -435,7 +463,7 @@ def main():
                        "width": wl.cfg.width, "height": wl.cfg.height, "spp": spp,
                        "jobs_per_step_per_gpu": jobs_rank, "volume": f"synthetic {wl.grid_n}^3 kind {wl.density_kind}",
                        "parallelism": f"wave-sharded x{world} ({args.mode}), RCCL film all-reduce" if world > 1 else "1 GPU",
-                       "rng_mode": args.rng_mode},
+                       "rng_mode": args.rng_mode, "latency_kernel": args.latency_kernel},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_source": traffic_source,

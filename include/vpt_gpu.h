@@ -210,8 +210,9 @@ int vpt_gpu_job_space(const vpt_gpu_ctx* ctx, uint64_t* jobs_per_wave, uint64_t*
  * launch that last held it has completed (the new launch's stream waits on an event), so any number
  * of launches is safe.  Launches that share a film add into it atomically.  The calls that change
  * context state read by running kernels (vpt_gpu_set_tuning, vpt_gpu_set_rng_mode) and
- * vpt_gpu_film_clear first wait for all work on the device.  One context is driven by one host
- * thread at a time (as the reference's `run` owns its RandomNumberGenerator). */
+ * vpt_gpu_film_clear first wait for this context's launches.  One context is driven by one host
+ * thread at a time (as the reference's `run` owns its RandomNumberGenerator): a state-changing call
+ * made from a second thread while the first is inside vpt_gpu_render_jobs is not supported. */
 int vpt_gpu_render_jobs(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count,
                         float* film_device, void* hip_stream);
 
@@ -315,6 +316,26 @@ int vpt_gpu_set_tile_costs(vpt_gpu_ctx* ctx, const float* cost_T);
 int vpt_gpu_set_job_permutation(vpt_gpu_ctx* ctx, const uint32_t* perm, uint64_t n);
 
 int vpt_gpu_sync(vpt_gpu_ctx* ctx);
+
+/* ---- pipelining and progressive films (the drop-in's drain, include/vpt_run.hpp) ------------ */
+
+/* A HIP stream on the context's device (non-blocking w.r.t. the null stream), for launches that overlap:
+ * a launch lasts as long as its longest job (a tile's pixels in one RNG stream), so back-to-back launches
+ * on one stream would each pay that drain; launches on two streams fill it with the next one's jobs. */
+int vpt_gpu_stream_create(vpt_gpu_ctx* ctx, void** hip_stream);
+int vpt_gpu_stream_destroy(vpt_gpu_ctx* ctx, void* hip_stream);
+/* Waits for the work enqueued on hip_stream so far. */
+int vpt_gpu_stream_sync(vpt_gpu_ctx* ctx, void* hip_stream);
+/* An extra device film (float[H][W][4], zeroed) of the context's size, e.g. the second buffer of a
+ * progressive film; release it with vpt_gpu_film_free before vpt_gpu_destroy. */
+int vpt_gpu_film_alloc(vpt_gpu_ctx* ctx, float** film_device);
+int vpt_gpu_film_free(vpt_gpu_ctx* ctx, float* film_device);
+/* film_host[i] += film_device[i], then film_device = 0 (film_device NULL = the context's own film).
+ * Synchronous.  The caller must have waited for every launch that renders into film_device (this call
+ * does not know their streams); launches into other films may keep running.  Uses a pinned staging
+ * buffer owned by the context. */
+int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* ctx, float* film_device, float* film_host_hxwx4);
+
 /* Zero the context's own film. */
 int vpt_gpu_film_clear(vpt_gpu_ctx* ctx);
 /* Device pointer of the context's own film (for an RCCL reduce), and its element count H*W*4. */
@@ -340,6 +361,16 @@ int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_b
  * gate_eval: <= 0) to keep a value; gate_idle 0 is rejected. */
 int vpt_gpu_set_latency_tuning(vpt_gpu_ctx* ctx, int wave_lanes, int gate_min, int gate_idle, int gate_eval,
                                int gate_walk);
+/* The latency kernel: the same state machine with the lane's cold state in VGPRs instead of LDS and a
+ * larger register budget (4 waves per SIMD instead of 7), for launches that occupy at most that many
+ * anyway -- latency-bound launches (C1) and partly filled ones (C2: 2 blocks per CU; a GPU's small share
+ * of a frame).  mode -1 (default): used where the grid rule gives <= its resident blocks per CU; 0: never;
+ * 1: always (tests).  ungated 1 (default): its partly filled launches use the latency gates (every block
+ * runs for one waiting lane, vpt_gpu_set_latency_tuning); 0: the context's gates; -1: keep.  Samples never
+ * depend on it.  Takes effect at the next launch. */
+int vpt_gpu_set_latency_kernel(vpt_gpu_ctx* ctx, int mode, int ungated);
+/* The mode and the latency kernel's resident blocks per CU. */
+int vpt_gpu_latency_kernel_info(const vpt_gpu_ctx* ctx, int* mode, int* resident_blocks_per_cu);
 /* SIMT-utilisation profile of profiling builds (-DVPT_PROFILE): for each block of the lane state
  * machine, [wave executions, active lanes] as 2*21 uint64 (the last 7: lanes per state at each walk-loop iteration), then the shader cycles the wavefronts
  * spent in each of 10 sections (fetch, pixel, ray, walk-loop control, eval, nee, finish, and the

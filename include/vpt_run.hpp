@@ -36,6 +36,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -50,11 +51,10 @@
 
 namespace vpt_gpu {
 
-// Renders every job `tp` hands out on `ctx` (asynchronously on `hip_stream`, batch_jobs job ids per
-// round of token taking, launches overlapping the next round), then adds the context's film into the
-// caller's reference-layout film (float[H][W][4], Image<float,4>).  Returns VPT_OK or the first error
-// code (vpt_last_error() has the message).  Several threads may call it with one `tp` and one
-// `film_host`, each with its own context.
+// Renders every job `tp` hands out on `ctx` and adds it into the caller's reference-layout film
+// (float[H][W][4], Image<float,4>) as it goes.  Returns VPT_OK or the first error code
+// (vpt_last_error() has the message).  Several threads may call it with one `tp` and one `film_host`,
+// each with its own context.
 //
 // TileProvider::next() blocks until the same tile's previous wave has been released
 // (src/tile_provider.cpp:40-60), so a thread that holds a token while calling next() deadlocks on
@@ -62,7 +62,25 @@ namespace vpt_gpu {
 // taking jobs, can happen at any batch size.  drain() therefore holds no token across next(): each
 // token is released as soon as its job id is recorded.  Every recorded job is rendered (no token is
 // dropped), and the GPU film needs no tile exclusivity: its adds are fp32 atomics.
+//
+// What the caller sees while it runs (main.cpp:101-132 shows the film at 5 FPS with progress() and
+// eta()):
+//   * token run-ahead is bounded: jobs are taken in rounds of batch_jobs, each round launched at once on
+//     one of `rounds_in_flight` streams, and a round's tokens are taken only after the round that last
+//     used its stream has completed -- so the provider's job counter (progress(), eta()) runs ahead of
+//     the rendered work by at most rounds_in_flight rounds, and stop_at_next_wave() stops within them;
+//   * the film is progressive: rounds render into one of two device films; every flush_seconds the
+//     current one is retired (later rounds go to the other), and once its rounds have completed it is
+//     added into film_host (under a mutex shared by all callers) and zeroed.  Sample counts in film_host
+//     therefore rise during the run, a whole job at a time, and the final film is the same sum.
+// Rounds on alternating streams overlap: a launch lasts as long as its longest job, and the next
+// round's jobs fill that drain instead of waiting behind it.
 using JobRuns = std::vector<std::pair<uint64_t, uint64_t>>;  // contiguous (jid_begin, count) runs
+
+struct DrainOptions {
+  unsigned rounds_in_flight = 2;  // token run-ahead bound, in rounds of batch_jobs
+  double flush_seconds = 0.2;     // progressive film period (main.cpp's window draws at 5 FPS)
+};
 
 // Takes up to max_jobs tokens; on_token(token&) sees each before it is released.  Returns the count.
 template <class Provider, class OnToken>
@@ -83,25 +101,106 @@ uint64_t take_jobs(Provider& tp, uint64_t max_jobs, JobRuns& runs, OnToken&& on_
   return taken;
 }
 
-inline int render_runs(vpt_gpu_ctx* ctx, const JobRuns& runs, void* hip_stream) {
+inline int render_runs(vpt_gpu_ctx* ctx, const JobRuns& runs, float* film_device, void* hip_stream) {
   for (const auto& r : runs)
-    if (int rc = vpt_gpu_render_jobs(ctx, r.first, r.second, nullptr, hip_stream)) return rc;
+    if (int rc = vpt_gpu_render_jobs(ctx, r.first, r.second, film_device, hip_stream)) return rc;
   return VPT_OK;
 }
 
-inline int finish(vpt_gpu_ctx* ctx, float* film_host) {
-  static std::mutex film_mu;  // the host film is shared by every caller
-  if (int rc = vpt_gpu_sync(ctx)) return rc;
-  std::lock_guard<std::mutex> lock(film_mu);
-  return vpt_gpu_film_add_to_host(ctx, film_host);
+inline std::mutex& film_mutex() {  // the host film is shared by every caller
+  static std::mutex mu;
+  return mu;
 }
 
+// The streams and the second device film of one drain() call.
+class DrainPipeline {
+ public:
+  DrainPipeline(vpt_gpu_ctx* ctx, unsigned rounds) : ctx_(ctx), streams_(rounds, nullptr), round_film_(rounds, -1) {}
+  ~DrainPipeline() {
+    for (void* s : streams_)
+      if (s) {
+        (void)vpt_gpu_stream_sync(ctx_, s);
+        (void)vpt_gpu_stream_destroy(ctx_, s);
+      }
+    if (films_[1]) (void)vpt_gpu_film_free(ctx_, films_[1]);
+  }
+  int init() {
+    for (void*& s : streams_)
+      if (int rc = vpt_gpu_stream_create(ctx_, &s)) return rc;
+    return vpt_gpu_film_alloc(ctx_, &films_[1]);
+  }
+  // Round k goes to stream k % rounds: wait for the round that last used it, then flush the retired film
+  // if its last round has completed.
+  int begin_round(uint64_t k, float* film_host) {
+    const size_t i = (size_t)(k % streams_.size());
+    if (round_film_[i] >= 0) {
+      if (int rc = vpt_gpu_stream_sync(ctx_, streams_[i])) return rc;
+      --inflight_[round_film_[i]];
+      round_film_[i] = -1;
+    }
+    return retired_ >= 0 && inflight_[retired_] == 0 ? flush(retired_, film_host) : VPT_OK;
+  }
+  // Retire the current film when the period is up (and the other film is free).
+  void maybe_retire(double flush_seconds) {
+    const auto now = std::chrono::steady_clock::now();
+    if (retired_ < 0 && std::chrono::duration<double>(now - last_retire_).count() >= flush_seconds) {
+      retired_ = current_;
+      current_ ^= 1;
+      last_retire_ = now;
+    }
+  }
+  int launch(uint64_t k, const JobRuns& runs) {
+    const size_t i = (size_t)(k % streams_.size());
+    round_film_[i] = current_;
+    ++inflight_[current_];
+    return render_runs(ctx_, runs, films_[current_], streams_[i]);
+  }
+  int finish(float* film_host) {
+    for (size_t i = 0; i < streams_.size(); ++i)
+      if (round_film_[i] >= 0) {
+        if (int rc = vpt_gpu_stream_sync(ctx_, streams_[i])) return rc;
+        --inflight_[round_film_[i]];
+        round_film_[i] = -1;
+      }
+    for (int f = 0; f < 2; ++f)
+      if (int rc = flush(f, film_host)) return rc;
+    return VPT_OK;
+  }
+
+ private:
+  int flush(int f, float* film_host) {
+    std::lock_guard<std::mutex> lock(film_mutex());
+    if (int rc = vpt_gpu_film_flush_to_host(ctx_, films_[f], film_host)) return rc;
+    if (retired_ == f) retired_ = -1;
+    return VPT_OK;
+  }
+  vpt_gpu_ctx* ctx_;
+  std::vector<void*> streams_;
+  std::vector<int> round_film_;   // film of the round last launched on each stream (-1: none / done)
+  float* films_[2] = {nullptr, nullptr};  // [0]: the context's own film (NULL), [1]: allocated
+  int inflight_[2] = {0, 0};      // rounds launched into each film and not known to be complete
+  int current_ = 0, retired_ = -1;
+  std::chrono::steady_clock::time_point last_retire_ = std::chrono::steady_clock::now();
+};
+
+// `first`: job runs already taken by the caller (launched as round 0).
 template <class Provider>
-int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs, void* hip_stream = nullptr) {
+int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs, const DrainOptions& opt = {},
+          const JobRuns* first = nullptr) {
+  DrainPipeline pipe(ctx, std::max(1u, opt.rounds_in_flight));
+  if (int rc = pipe.init()) return rc;
   JobRuns runs;
-  while (take_jobs(tp, batch_jobs, runs, [](auto&) {}))
-    if (int rc = render_runs(ctx, runs, hip_stream)) return rc;
-  return finish(ctx, film_host);
+  for (uint64_t k = 0;; ++k) {
+    if (int rc = pipe.begin_round(k, film_host)) return rc;
+    if (k == 0 && first) {
+      runs = *first;
+    } else if (!take_jobs(tp, std::max<uint64_t>(1, batch_jobs), runs, [](auto&) {})) {
+      break;
+    }
+    pipe.maybe_retire(opt.flush_seconds);
+    if (int rc = pipe.launch(k, runs)) return rc;
+  }
+  return pipe.finish(film_host);
 }
 
 namespace detail {
@@ -308,9 +407,8 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
     ~Ctx() { vpt_gpu_destroy(c); }
   } guard{ctx};
   float* film_host = reinterpret_cast<float*>(film.data().data());  // H x W x (X, Y, Z, W)
-  if (int rc = render_runs(ctx, runs, nullptr)) return rc;
-  // later rounds: 8 waves of jobs per round of token taking
-  return drain(ctx, tp, film_host, 8 * T, nullptr);
+  // the first batch is round 0; later rounds: 8 waves of jobs each
+  return drain(ctx, tp, film_host, 8 * T, DrainOptions{}, &runs);
 }
 
 template <class WorkerParameters, class Volume, class Camera, class TileProvider, class Image, class RNG>

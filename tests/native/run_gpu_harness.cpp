@@ -5,7 +5,7 @@
 //
 //   run_gpu_harness config=<scene.json> out=<film.f32> [mode=drain|run w= h= waves= threads= batch=
 //                   grid_n= dist= temperature=0|1 stop_after=<jobs> nvdb=<file.nvdb> gridbuf=<file>
-//                   tempbuf=<file>]
+//                   tempbuf=<file> rounds= flush_ms= grid_blocks= sample_ms=]
 //
 // mode=drain (default): each thread owns a context made with vpt_gpu_create and calls
 //   vpt_gpu::drain(ctx, tp, film, batch).  The volume is nvdb= (vpt_grid_read_nvdb: "density", and
@@ -17,12 +17,18 @@
 //   to the RandomNumberGenerator.
 // The camera looks at the volume from (0, 0, -dist) unless dist=0 (then the scene file's camera).
 // stop_after: after that many jobs thread 0 calls tp.stop_at_next_wave() (tile_provider.cpp:107-110).
+// rounds / flush_ms: vpt_gpu::DrainOptions of mode=drain; grid_blocks: vpt_gpu_set_tuning's grid override.
+// sample_ms: a thread samples, every sample_ms, the jobs handed out and the samples in the host film (what
+// main.cpp's 5-FPS window shows: film_to_image(film) and provider.progress(), main.cpp:101-132) and prints
+// them as "sample <ms> <waves handed out> <waves in the film>".  The render time is printed as render_ms.
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iterator>
+#include <array>
 #include <map>
 #include <string>
 #include <thread>
@@ -98,6 +104,23 @@ int main(int argc, char** argv) {
   vpt_headless::Image<float, 4> film(cfg.output_size[0], cfg.output_size[1]);
   std::vector<int> rc(threads, 0);
 
+  // the 5-FPS window of main.cpp:101-132, headless: what a viewer would see while the GPU renders
+  const long long sample_ms = num("sample_ms", 0);
+  std::atomic<bool> rendering{true};
+  std::vector<std::array<double, 3>> samples;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto sampler = [&] {
+    const double T = (double)tp.num_tiles(), px = (double)cfg.output_size[0] * (double)cfg.output_size[1];
+    while (rendering.load()) {
+      double w = 0.0;
+      for (size_t i = 3; i < film.px.size() * 4; i += 4) w += (double)reinterpret_cast<const float*>(film.px.data())[i];
+      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      samples.push_back({ms, (double)sp.handed.load() / T, w / px});
+      std::this_thread::sleep_for(std::chrono::milliseconds(sample_ms));
+    }
+  };
+  std::thread sampler_thread;
+
   if (mode == "seed") {  // the drop-in's seed recovery (no GPU): the RNG's seed is private
     vpt_headless::RandomNumberGenerator rng(cfg.seed);
     uint32_t seed = 0;
@@ -134,6 +157,7 @@ int main(int argc, char** argv) {
     const vpt_camera_params& c = cfg.camera_parameters;
     vpt_headless::Camera camera{{v3(c.position), v3(c.look), v3(c.up), c.vfov_deg, c.imaging_ratio}};
     std::vector<std::thread> pool;
+    if (sample_ms > 0) sampler_thread = std::thread(sampler);
     for (int i = 0; i < threads; ++i)
       pool.emplace_back([&, i] {
         vpt_headless::RandomNumberGenerator rng(cfg.seed);
@@ -157,10 +181,22 @@ int main(int argc, char** argv) {
     for (int i = 0; i < threads; ++i)
       if (vpt_gpu_create(&cfg, dens, temp, nullptr, i % ndev, &ctx[i])) return fail("vpt_gpu_create");
     float* fh = reinterpret_cast<float*>(film.data().data());
+    vpt_gpu::DrainOptions opt;
+    opt.rounds_in_flight = (unsigned)num("rounds", opt.rounds_in_flight);
+    opt.flush_seconds = (double)num("flush_ms", (long long)(opt.flush_seconds * 1000)) / 1000.0;
+    if (num("grid_blocks", 0) > 0)
+      for (auto* c : ctx)
+        if (vpt_gpu_set_tuning(c, 0, -1, (int)num("grid_blocks", 0), 0, -1)) return fail("vpt_gpu_set_tuning");
+    for (auto* c : ctx)  // the context's one-time tile-cost pass, outside the timed render
+      if (vpt_gpu_tile_costs(c, nullptr, nullptr) || vpt_gpu_sync(c)) return fail("warm-up");
     {
+      const auto r0 = std::chrono::steady_clock::now();
+      if (sample_ms > 0) sampler_thread = std::thread(sampler);
       std::vector<std::thread> pool;
-      for (int i = 0; i < threads; ++i) pool.emplace_back([&, i] { rc[i] = vpt_gpu::drain(ctx[i], sp, fh, batch); });
+      for (int i = 0; i < threads; ++i) pool.emplace_back([&, i] { rc[i] = vpt_gpu::drain(ctx[i], sp, fh, batch, opt); });
       for (auto& t : pool) t.join();
+      std::printf("run_gpu_harness: render_ms %.1f\n",
+                  std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count());
     }
     for (int i = 0; i < threads; ++i)
       if (rc[i]) return fail("vpt_gpu::drain");
@@ -168,6 +204,10 @@ int main(int argc, char** argv) {
     vpt_grid_free(dens);
     if (temp) vpt_grid_free(temp);
   }
+
+  rendering.store(false);
+  if (sampler_thread.joinable()) sampler_thread.join();
+  for (const auto& e : samples) std::printf("sample %.1f %.3f %.3f\n", e[0], e[1], e[2]);
 
   FILE* f = std::fopen(a["out"].c_str(), "wb");
   const size_t n = film.px.size() * 4;

@@ -89,6 +89,10 @@ def test_bench_gpus2_spawns_two_ranks(tmp_path):
     # and the strong-scaling record: the whole C3 frame dealt over the 2 ranks, timed the same way
     s = line["scaling_strong"]["c3"]
     assert s["value"] > 0 and s["ms_per_step"] > 0 and "1920x1080, 256 spp" in s["workload"]
+    # ... with its own 1-GPU time of the same frame (rank 0 alone) and the speedup / efficiency from it
+    assert s["one_gpu_ms_per_step"] > 0
+    assert s["speedup_vs_1gpu"] == pytest.approx(s["one_gpu_ms_per_step"] / s["ms_per_step"], rel=2e-3)
+    assert s["efficiency"] == pytest.approx(s["speedup_vs_1gpu"] / 2, rel=2e-3)
     p = line["scaling_strong"]["c3:pixel"]  # the same frame in the throughput mode, labelled as such
     assert p["value"] > 0 and "throughput mode" in p["workload"]
     # WORLD_SIZE that disagrees with --gpus is an error

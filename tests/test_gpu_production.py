@@ -9,6 +9,8 @@ therefore gives a bit-exact comparison with the oracle's per-sample records, for
   <HasTemp=false, Runs=true>   run skipping (chosen automatically for C2's constant cube; forced here
                                on the 128^3 cube and on a 64^3 cloud)
   <HasTemp=true,  Runs=false>  C4 (fire: blackbody emission from the temperature grid)
+each as the throughput kernel and as the latency kernel (Lat: the lane's cold state in VGPRs; C1, C2 and
+small shares of a frame select it), forced with vpt_gpu_set_latency_kernel.
 
 The production kernel's own event counters (samples, HDDA steps, density and temperature stencil
 refreshes -- the terms of the algorithmic bytes) must equal the oracle's.
@@ -85,13 +87,17 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("lat", [0, 1])
 @pytest.mark.parametrize("name,w,h,n,runs", CASES)
-def test_production_kernel_single_wave_films_bit_exact(name, w, h, n, runs):
+def test_production_kernel_single_wave_films_bit_exact(name, w, h, n, runs, lat):
+    """lat 0: the throughput kernels (7 / 6 waves per SIMD, cold state in LDS); lat 1: the latency kernels
+    (cold state in VGPRs), which C1 / C2 select automatically."""
     from volume_path_tracer_amd.render import Integrator
 
     wl = workload(name, width=w, height=h, spp=3, grid_n=n)
     dens, temp = _grids(wl)
     it = Integrator(wl.cfg, dens, temp, device=0)
+    it.set_latency_kernel(lat)
     if runs >= 0:
         it.set_run_skipping(runs)
     kv = it.kernel_variant()
@@ -161,29 +167,34 @@ def test_c1_full_workload_vs_oracle():
     it.render_jobs(0, jobs, film=torch.zeros_like(it.film), records=rec)
     torch.cuda.synchronize()
     assert rec.cpu().numpy().tobytes() == r_o.tobytes()
-    it.counters(reset=True)
-    for wave in range(4):
-        f_g = _prod_film(it, wave * T, T)
-        _assert_bitwise(f_g, records_film(wl.cfg, wave * T, T, r_o[wave * T * 64:(wave + 1) * T * 64]), f"wave {wave + 1}")
-    c = it.counters()
-    for k in COUNTERS:
-        assert c[k] == c_o[k], k
-    it.film.zero_()
-    it.render_waves(1, 4)
-    f_g = it.film_host()
-    np.testing.assert_array_equal(f_g[..., 3], 4.0)
-    np.testing.assert_allclose(f_g[..., :3], f_o[..., :3], rtol=1e-5, atol=1e-6)
+    for lat in (0, -1):  # the throughput kernel, and the latency kernel C1 selects
+        it.set_latency_kernel(lat)
+        it.counters(reset=True)
+        for wave in range(4):
+            f_g = _prod_film(it, wave * T, T)
+            _assert_bitwise(f_g, records_film(wl.cfg, wave * T, T, r_o[wave * T * 64:(wave + 1) * T * 64]),
+                            f"lat {lat} wave {wave + 1}")
+        c = it.counters()
+        for k in COUNTERS:
+            assert c[k] == c_o[k], (lat, k)
+        it.film.zero_()
+        it.render_waves(1, 4)
+        f_g = it.film_host()
+        np.testing.assert_array_equal(f_g[..., 3], 4.0)
+        np.testing.assert_allclose(f_g[..., :3], f_o[..., :3], rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("lat", [0, 1])
 @pytest.mark.parametrize("name", ["c3", "c4"])
-def test_fullres_production_job_ranges_bit_exact(name):
+def test_fullres_production_job_ranges_bit_exact(name, lat):
     """C3 / C4 at 1920x1080 on the 512^3 stand-ins: production-kernel films of job ranges spread over
-    all 256 waves, bit-exact vs the oracle, and the stencil counters equal."""
+    all 256 waves, bit-exact vs the oracle, and the stencil counters equal (throughput and latency kernels)."""
     from volume_path_tracer_amd.render import Integrator
 
     wl = workload(name)
     dens, temp = _grids(wl)
     it = Integrator(wl.cfg, dens, temp, device=0)
+    it.set_latency_kernel(lat)
     od, ot = _oracle_grids(dens, temp)
     T = wl.cfg.jobs_per_wave()
     rng = np.random.default_rng(11 if name == "c3" else 12)
@@ -282,8 +293,9 @@ def test_concurrent_launches_on_three_streams():
     _assert_bitwise(film.cpu().numpy(), f_o, "3-stream film")
 
 
+@pytest.mark.parametrize("lat", [0, 1])
 @pytest.mark.parametrize("name", ["c3", "c4"])
-def test_latency_launch_knobs_keep_films_bit_exact(name):
+def test_latency_launch_knobs_keep_films_bit_exact(name, lat):
     """Latency-bound launches (fewer jobs than grid lanes) spread their jobs over the wavefronts and run
     with their own gates (vpt_gpu_set_latency_tuning); a launch that fills the grid uses the normal
     path.  Every setting renders the oracle's single-wave films bit for bit, with equal counters."""
@@ -292,6 +304,7 @@ def test_latency_launch_knobs_keep_films_bit_exact(name):
     wl = workload(name, width=48, height=40, spp=12, grid_n=64)
     dens, temp = _grids(wl)
     it = Integrator(wl.cfg, dens, temp, device=0)
+    it.set_latency_kernel(lat)
     od, ot = _oracle_grids(dens, temp)
     T = wl.cfg.jobs_per_wave()
     ref = [O.render_jobs(wl.cfg, od, ot, w * T, T) for w in range(2)]
@@ -321,8 +334,9 @@ def test_latency_launch_knobs_keep_films_bit_exact(name):
     np.testing.assert_allclose(f_g[..., :3], f_o[..., :3], rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("lat", [0, 1])
 @pytest.mark.parametrize("case", ["small_voxels", "large_voxels", "unit_rotated"])
-def test_mapped_grid_production_films_bit_exact(case):
+def test_mapped_grid_production_films_bit_exact(case, lat):
     """Non-identity maps (voxel size 0.05 / 20, anisotropic, rotated) through the production kernel:
     the walk-word prefetch's padding holds in index space whatever the voxel size, so the
     single-wave films equal the oracle's bit for bit and the counters agree."""
@@ -334,6 +348,7 @@ def test_mapped_grid_production_films_bit_exact(case):
     wl = workload("c3", width=64, height=48, spp=2, grid_n=64)
     mapped_scene(wl.cfg, 64 * max(scale), 1.0 / min(scale))
     it = Integrator(wl.cfg, dens, None, device=0)
+    it.set_latency_kernel(lat)
     od = O.OracleGrid(dens, fix_majorants=True)
     T = wl.cfg.jobs_per_wave()
     it.counters(reset=True)
@@ -349,7 +364,8 @@ def test_mapped_grid_production_films_bit_exact(case):
         assert c[k] == tot[k], (k, c[k], tot[k])
 
 
-def test_temperature_kernel_blackbody_from_memory_above_the_lds_rows():
+@pytest.mark.parametrize("lat", [0, 1])
+def test_temperature_kernel_blackbody_from_memory_above_the_lds_rows(lat):
     """A temperature scale that reaches 20 000 K: the blackbody rows past the kernel's LDS copy
     (kBbLdsRows) are read from memory; the production films stay bit-exact vs the oracle."""
     from volume_path_tracer_amd.render import Integrator
@@ -358,6 +374,7 @@ def test_temperature_kernel_blackbody_from_memory_above_the_lds_rows():
     wl.cfg.volume_parameters.temperature_scale *= 10.0
     dens, temp = _grids(wl)
     it = Integrator(wl.cfg, dens, temp, device=0)
+    it.set_latency_kernel(lat)
     od, ot = _oracle_grids(dens, temp)
     T = wl.cfg.jobs_per_wave()
     for wave in (1, 2):
@@ -367,8 +384,9 @@ def test_temperature_kernel_blackbody_from_memory_above_the_lds_rows():
 
 
 
+@pytest.mark.parametrize("lat", [0, 1])
 @pytest.mark.parametrize("kind", ["shifted", "half_voxels", "sparse"])
-def test_temperature_grid_of_another_map_or_topology(kind):
+def test_temperature_grid_of_another_map_or_topology(kind, lat):
     """The temperature kernel with a temperature grid whose map / topology differ from the density's
     (tests/grids.py temperature_pair): production films bit-exact vs the oracle, counters equal."""
     from grids import look_at, temperature_pair
@@ -379,6 +397,7 @@ def test_temperature_grid_of_another_map_or_topology(kind):
     n = 128 if kind == "sparse" else 64
     look_at(wl.cfg, (0.3 * n, 0.6 * n, -2.2 * n), (0.5 * n, 0.45 * n, 0.5 * n))
     it = Integrator(wl.cfg, dens, temp, device=0)
+    it.set_latency_kernel(lat)
     od, ot = _oracle_grids(dens, temp)
     T = wl.cfg.jobs_per_wave()
     it.counters(reset=True)

@@ -90,3 +90,28 @@ def test_native_reader_rejects_malformed_buffers(tmp_path):
     p.write_bytes(b"not a nanovdb file at all")
     with pytest.raises(RuntimeError, match=r"\(1\)"):
         capi.read_nvdb_grid(p, "density")
+
+
+def test_readers_reject_other_nanovdb_major_versions():
+    """GridData::mVersion (offset 16): the layout is NanoVDB 32.x's, so a buffer of another major version is
+    VPT_E_INVALID in the in-memory path too, and in the Python reader."""
+    buf = bytearray(nvdb.buffer_from_grid(sparse_grid(), "density"))
+    for major in (31, 33):
+        bad = bytearray(buf)
+        struct.pack_into("<I", bad, 16, (major << 21) | (7 << 10))
+        with pytest.raises(RuntimeError, match="major version"):
+            capi.grid_from_nanovdb(bytes(bad))
+        with pytest.raises(nvdb.NvdbError, match="major version"):
+            nvdb.grid_from_buffer(bytes(bad))
+
+
+def test_zip_grid_size_is_bounded_before_allocating(tmp_path):
+    """A ZIP-coded .nvdb whose metadata claims a huge gridSize is rejected before the reader allocates it
+    (it must not throw std::bad_alloc through the C ABI)."""
+    p = tmp_path / "z.nvdb"
+    nvdb.write_nvdb(p, {"density": SynthGrid(1, 32).grid(copy=True)}, codec=nvdb.CODEC_ZIP)
+    data = bytearray(p.read_bytes())
+    struct.pack_into("<Q", data, 16, 1 << 50)  # FileMetaData::gridSize of the first grid
+    p.write_bytes(bytes(data))
+    with pytest.raises(RuntimeError, match=r"\(1\).*gridSize"):
+        capi.read_nvdb_grid(p, "density")

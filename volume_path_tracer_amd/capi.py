@@ -208,7 +208,11 @@ def lib() -> C.CDLL:
     # kernels see.  Loaded after /opt/rocm's (this library's link-time runtime), torch's ROCr opens the GPU a
     # second time and, on some boxes, finds none ("No HIP GPUs are available"; r03zl,
     # tools/probe_hip_init2.py).  So torch is imported before the library, whatever the caller imported.
-    import torch  # noqa: F401
+    # Host-only uses (grid readers, the C-ABI host tests) need no torch: without it there is no second runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(str(LIB_PATH))
     cfgp, gridp = C.POINTER(Configuration), C.POINTER(GridDesc)
     fp, vp = C.POINTER(C.c_float), C.c_void_p
@@ -253,6 +257,16 @@ def lib() -> C.CDLL:
     L.vpt_gpu_tile_costs.argtypes = [vp, fp, C.POINTER(C.c_uint32)]
     L.vpt_gpu_set_tile_costs.argtypes = [vp, fp]
     L.vpt_gpu_set_job_permutation.argtypes = [vp, C.POINTER(C.c_uint32), C.c_uint64]
+    if hasattr(L, "vpt_gpu_set_latency_kernel"):  # (A/B builds of older sources lack it; tests check the exports)
+        L.vpt_gpu_set_latency_kernel.argtypes = [vp, C.c_int, C.c_int]
+        L.vpt_gpu_latency_kernel_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    if hasattr(L, "vpt_gpu_stream_create"):
+        L.vpt_gpu_stream_create.argtypes = [vp, C.POINTER(vp)]
+        L.vpt_gpu_stream_destroy.argtypes = [vp, vp]
+        L.vpt_gpu_stream_sync.argtypes = [vp, vp]
+        L.vpt_gpu_film_alloc.argtypes = [vp, C.POINTER(vp)]
+        L.vpt_gpu_film_free.argtypes = [vp, vp]
+        L.vpt_gpu_film_flush_to_host.argtypes = [vp, vp, fp]
     _lib = L
     return L
 

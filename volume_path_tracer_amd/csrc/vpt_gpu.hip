@@ -50,6 +50,13 @@ constexpr int kBlockThreads = 256;
 #ifndef VPT_WAVES_TEMP
 #define VPT_WAVES_TEMP 6
 #endif
+// The latency kernel (partly filled and latency-bound launches: C1, C2, a GPU's small share of a frame):
+// at most VPT_WAVES_LAT waves per SIMD run anyway there, so it trades occupancy for registers -- the
+// lane's cold state in VGPRs instead of LDS (no LDS round trips on the per-pixel / per-bounce chain)
+// and a 512 / VPT_WAVES_LAT register budget.
+#ifndef VPT_WAVES_LAT
+#define VPT_WAVES_LAT 4
+#endif
 
 // The lanes' cold state (vpt_integrator.h LaneCold), one slot per thread of the integrator's block.
 __shared__ LaneCold g_lane_cold[kBlockThreads];
@@ -60,7 +67,8 @@ __shared__ double g_logf_tab[16][2];
 constexpr int kBbFloats = kBbLdsRows * 3;
 
 
-struct KernelEnv {
+template <bool RegCold>
+struct KernelEnvT {
   uint64_t jid_begin;
   uint64_t jid_count;
   unsigned long long* job_counter;
@@ -142,7 +150,15 @@ struct KernelEnv {
     }
     e->v[6] = 0.0f;
   }
-  __device__ __forceinline__ LaneCold& cold() { return g_lane_cold[threadIdx.x]; }
+  // The lane's cold state: its LDS slot, or (RegCold, the latency kernel) a kernel local the compiler
+  // keeps in VGPRs.
+  LaneCold* reg_cold;
+  __device__ __forceinline__ LaneCold& cold() {
+    if constexpr (RegCold)
+      return *reg_cold;
+    else
+      return g_lane_cold[threadIdx.x];
+  }
   const float* bb_lds;  // the temperature kernel's LDS copy of S.bb's first kBbLdsRows rows
   __device__ __forceinline__ const double (*logf_table() const)[2] { return g_logf_tab; }
   // blackbody_radiation_xyz from the LDS rows when the grid's temperatures stay in them (a uniform
@@ -206,10 +222,11 @@ struct KernelEnv {
     }
   }
 };
+using KernelEnv = KernelEnvT<false>;
 
 // counters[] order = vpt_counters field order
-template <bool HasTemp, bool Debug, bool Runs>
-__global__ __launch_bounds__(kBlockThreads, Debug ? VPT_WAVES_SLOW : (HasTemp ? VPT_WAVES_TEMP : VPT_WAVES_FAST)) void vpt_integrate_kernel(const DevScene* scene, KernelEnv env,
+template <bool HasTemp, bool Debug, bool Runs, bool Lat = false>
+__global__ __launch_bounds__(kBlockThreads, Lat ? VPT_WAVES_LAT : (Debug ? VPT_WAVES_SLOW : (HasTemp ? VPT_WAVES_TEMP : VPT_WAVES_FAST))) void vpt_integrate_kernel(const DevScene* scene, KernelEnvT<Lat> env,
                                                                        unsigned long long* counters) {
   __shared__ unsigned long long wg_counters[kCounterCount];
   if (threadIdx.x < kCounterCount) wg_counters[threadIdx.x] = 0;
@@ -231,6 +248,8 @@ __global__ __launch_bounds__(kBlockThreads, Debug ? VPT_WAVES_SLOW : (HasTemp ? 
 #endif
   Lane ln;
   lane_init(ln);
+  LaneCold lc_reg;
+  if constexpr (Lat) env.reg_cold = &lc_reg;
   cold_init(env.cold());
   const ScenePtr sp = (ScenePtr)scene;
   while (ln.state != ST_DONE) lane_iteration<HasTemp, Debug, Runs>(sp, ln, env);
@@ -442,6 +461,10 @@ struct vpt_gpu_ctx {
   uint32_t* perm = nullptr;        // explicit job order of launches with perm_n jobs (device)
   uint64_t perm_n = 0;
   std::vector<uint32_t> tile_rank;
+  float* staging = nullptr;        // pinned host buffer of film_count floats (vpt_gpu_film_flush_to_host)
+  int lat_mode = -1;               // latency kernel: -1 auto (launches of <= lat_per_cu blocks per CU), 0 off, 1 on
+  int lat_ungated = 1;             // its partly filled launches read the latency gates (1) or the context's (0)
+  int lat_per_cu = 1;              // resident blocks per CU of the latency kernel
 };
 
 namespace {
@@ -495,12 +518,17 @@ int release_slot(vpt_gpu_ctx* ctx, hipStream_t s, uint32_t slot) {
 // behind another's frames).  Each launch records its ring slot's event after its kernels
 // (release_slot), and a launch that reuses a slot is ordered after the slot's previous launch
 // (take_slot), so the latest event of every used slot covers all of them.
+// The events are snapshotted under the lock and waited for after it is released, so a wait never
+// blocks another thread's take_slot.
 int wait_ctx(vpt_gpu_ctx* ctx) {
+  hipEvent_t ev[kLaunchSlots];
+  uint32_t n = 0;
   {
     std::lock_guard<std::mutex> lock(ctx->slot_mu);
     for (uint32_t i = 0; i < kLaunchSlots; ++i)
-      if (ctx->slot_used[i]) VPT_HIP(hipEventSynchronize(ctx->slot_done[i]));
+      if (ctx->slot_used[i]) ev[n++] = ctx->slot_done[i];
   }
+  for (uint32_t i = 0; i < n; ++i) VPT_HIP(hipEventSynchronize(ev[i]));
   if (ctx->stream) VPT_HIP(hipStreamSynchronize(ctx->stream));
   return VPT_OK;
 }
@@ -529,6 +557,7 @@ void destroy(vpt_gpu_ctx* ctx) {
   for (uint32_t i = 0; i < kLaunchSlots; ++i)
     if (ctx->slot_done[i]) (void)hipEventDestroy(ctx->slot_done[i]);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->staging) (void)hipHostFree(ctx->staging);
   delete ctx;
 }
 
@@ -577,6 +606,7 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   (void)total;  // jids beyond num_waves are valid jobs too (TileProvider only stops at requested_waves)
   hipStream_t s = (hipStream_t)stream_ptr;  // NULL = the null stream (HIP convention)
   vpt::KernelEnv env;
+  env.reg_cold = nullptr;  // the latency kernel points it at its own local
   env.jid_begin = jid_begin;
   env.jid_count = jid_count;
   env.pixel_chunk = 1;
@@ -626,12 +656,25 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   // latency gates (every block runs for one lane).  Measured, C1 (r02): 43.3 ms (256 blocks x 64
   // lanes) -> 20.5 ms (1 792 blocks, one lane per wavefront, gates 1:65:1:1).  Same jobs, same samples.
   const bool latency = env.jid_count <= kSpreadLanes * ((uint64_t)blocks * (vpt::kBlockThreads / 64));
+  const uint64_t cus = (uint64_t)ctx->cus;
   if (!ctx->grid_user && !latency) {
-    const uint64_t cus = (uint64_t)ctx->cus, resident_per_cu = std::max<uint64_t>(1, blocks / cus);
+    const uint64_t resident_per_cu = std::max<uint64_t>(1, blocks / cus);
     const double x = (double)env.jid_count / ((double)blocks * vpt::kBlockThreads);  // items per resident lane
     const uint64_t per_cu = std::min<uint64_t>(resident_per_cu, (uint64_t)std::max(1.0, std::floor(1.5 + 1.8 * x)));
     blocks = (uint32_t)std::min<uint64_t>(blocks, cus * per_cu);
   }
+#ifdef VPT_JOB_LOG
+  const bool temp = ctx->scene.has_temperature != 0, dbg = events != nullptr;  // records = the job log
+#else
+  const bool temp = ctx->scene.has_temperature != 0, dbg = records != nullptr || events != nullptr;
+#endif
+  // The latency kernel (lane cold state in VGPRs, VPT_WAVES_LAT waves per SIMD) for launches that fill at
+  // most its resident grid anyway: latency-bound ones (on its whole grid) and partly filled ones whose
+  // rule above gives <= lat_per_cu blocks per CU (C2: 2).  Same jobs, same samples.
+  const uint64_t lat_blocks = cus * (uint64_t)ctx->lat_per_cu;
+  const bool use_lat = !dbg && ctx->lat_mode != 0 &&
+                       (ctx->lat_mode == 1 || (!ctx->grid_user && (latency || blocks <= lat_blocks)));
+  if (use_lat) blocks = (uint32_t)std::min<uint64_t>(latency ? lat_blocks : blocks, lat_blocks);
   const uint64_t T = ctx->scene.T;
   if (ctx->order_mode != VPT_ORDER_JID && jid_begin % T == 0 && jid_count % T == 0 && jid_count < (1ULL << 32)) {
     // whole waves: take the jobs in cost order (same jobs, same samples)
@@ -657,17 +700,22 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.event_count = ctx->job_counter + 2 * slot + 1;
   env.event_cap = event_cap;
   if (slot_out) *slot_out = slot;
-#ifdef VPT_JOB_LOG
-  const bool temp = ctx->scene.has_temperature != 0, dbg = events != nullptr;  // records = the job log
-#else
-  const bool temp = ctx->scene.has_temperature != 0, dbg = records != nullptr || events != nullptr;
-#endif
-  auto kernel = temp ? (dbg ? vpt::vpt_integrate_kernel<true, true, false> : vpt::vpt_integrate_kernel<true, false, false>)
-                     : ctx->use_runs
-                         ? (dbg ? vpt::vpt_integrate_kernel<false, true, true> : vpt::vpt_integrate_kernel<false, false, true>)
-                         : (dbg ? vpt::vpt_integrate_kernel<false, true, false> : vpt::vpt_integrate_kernel<false, false, false>);
-  hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, latency ? ctx->scene_lat_dev : ctx->scene_dev,
-                     env, ctx->counters);
+  const vpt::DevScene* scene = latency || (use_lat && ctx->lat_ungated) ? ctx->scene_lat_dev : ctx->scene_dev;
+  if (use_lat) {
+    vpt::KernelEnvT<true> envl;
+    static_assert(sizeof envl == sizeof env, "one layout for both kernel environments");
+    std::memcpy(&envl, &env, sizeof env);
+    auto kernel = temp ? vpt::vpt_integrate_kernel<true, false, false, true>
+                       : ctx->use_runs ? vpt::vpt_integrate_kernel<false, false, true, true>
+                                       : vpt::vpt_integrate_kernel<false, false, false, true>;
+    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, scene, envl, ctx->counters);
+  } else {
+    auto kernel = temp ? (dbg ? vpt::vpt_integrate_kernel<true, true, false> : vpt::vpt_integrate_kernel<true, false, false>)
+                       : ctx->use_runs
+                           ? (dbg ? vpt::vpt_integrate_kernel<false, true, true> : vpt::vpt_integrate_kernel<false, false, true>)
+                           : (dbg ? vpt::vpt_integrate_kernel<false, true, false> : vpt::vpt_integrate_kernel<false, false, false>);
+    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, scene, env, ctx->counters);
+  }
   VPT_HIP(hipGetLastError());
   const uint64_t npix = (uint64_t)ctx->scene.W * (uint64_t)ctx->scene.H;
   hipLaunchKernelGGL(vpt::vpt_count_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, ctx->scene_dev,
@@ -764,6 +812,13 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   VPT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
   if (per_cu < 1) per_cu = 1;
   ctx->grid_blocks = per_cu * cus;
+  int lat_per_cu = 0;
+  VPT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &lat_per_cu, temperature ? vpt::vpt_integrate_kernel<true, false, false, true>
+                               : (ctx->use_runs ? vpt::vpt_integrate_kernel<false, false, true, true>
+                                                : vpt::vpt_integrate_kernel<false, false, false, true>),
+      vpt::kBlockThreads, 0));
+  ctx->lat_per_cu = std::max(1, std::min(lat_per_cu, per_cu));
   ctx->cus = cus > 0 ? cus : 1;
   // Scheduling defaults from tools/tune.py sweeps on MI355X (C3, 256 spp): rare states run for >= 6
   // waiting lanes, density evaluations (with the deferred exact draw) for >= 36, everything runs when
@@ -943,6 +998,71 @@ int vpt_gpu_sync(vpt_gpu_ctx* ctx) {
   return wait_ctx(ctx);
 }
 
+int vpt_gpu_stream_create(vpt_gpu_ctx* ctx, void** hip_stream) {
+  if (!ctx || !hip_stream) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_stream_create: null argument");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  hipStream_t s = nullptr;
+  VPT_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  *hip_stream = s;
+  return VPT_OK;
+}
+
+int vpt_gpu_stream_destroy(vpt_gpu_ctx* ctx, void* hip_stream) {
+  if (!ctx || !hip_stream) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_stream_destroy: null argument");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  VPT_HIP(hipStreamDestroy((hipStream_t)hip_stream));
+  return VPT_OK;
+}
+
+int vpt_gpu_stream_sync(vpt_gpu_ctx* ctx, void* hip_stream) {
+  if (!ctx) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_stream_sync: null context");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  VPT_HIP(hipStreamSynchronize((hipStream_t)hip_stream));
+  return VPT_OK;
+}
+
+int vpt_gpu_film_alloc(vpt_gpu_ctx* ctx, float** film_device) {
+  if (!ctx || !film_device) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_film_alloc: null argument");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  float* f = nullptr;
+  VPT_HIP(hipMalloc((void**)&f, ctx->film_count * sizeof(float)));
+  const hipError_t e = hipMemset(f, 0, ctx->film_count * sizeof(float));
+  if (e != hipSuccess) {
+    (void)hipFree(f);
+    return vpt::set_error(VPT_E_HIP, std::string("vpt_gpu_film_alloc: ") + hipGetErrorString(e));
+  }
+  *film_device = f;
+  return VPT_OK;
+}
+
+int vpt_gpu_film_free(vpt_gpu_ctx* ctx, float* film_device) {
+  if (!ctx || !film_device || film_device == ctx->film)
+    return vpt::set_error(VPT_E_INVALID, "vpt_gpu_film_free: not a film from vpt_gpu_film_alloc");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  VPT_HIP(hipFree(film_device));
+  return VPT_OK;
+}
+
+int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* ctx, float* film_device, float* film_host) {
+  if (!ctx || !film_host) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_film_flush_to_host: null argument");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  float* f = film_device ? film_device : ctx->film;
+  const size_t bytes = ctx->film_count * sizeof(float);
+  if (!ctx->staging) VPT_HIP(hipHostMalloc((void**)&ctx->staging, bytes, hipHostMallocDefault));
+  VPT_HIP(hipMemcpyAsync(ctx->staging, f, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  VPT_HIP(hipMemsetAsync(f, 0, bytes, ctx->stream));
+  VPT_HIP(hipStreamSynchronize(ctx->stream));
+  const float* src = ctx->staging;
+  for (uint64_t i = 0; i < ctx->film_count; ++i) film_host[i] += src[i];
+  return VPT_OK;
+}
+
 int vpt_gpu_film_clear(vpt_gpu_ctx* ctx) {
   if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
   int rc = ctx_device(ctx);
@@ -1017,6 +1137,14 @@ int vpt_gpu_set_latency_tuning(vpt_gpu_ctx* ctx, int wave_lanes, int gate_min, i
   return push_scene(ctx);
 }
 
+int vpt_gpu_set_latency_kernel(vpt_gpu_ctx* ctx, int mode, int ungated) {
+  if (!ctx || mode < -1 || mode > 1 || ungated < -1 || ungated > 1)
+    return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_latency_kernel: bad argument");
+  ctx->lat_mode = mode;  // read by the next render's host code only: no wait
+  if (ungated >= 0) ctx->lat_ungated = ungated;
+  return VPT_OK;
+}
+
 int vpt_gpu_profile(vpt_gpu_ctx* ctx, uint64_t* out, int n, int reset) {
   if (!ctx || !out) return vpt::set_error(VPT_E_INVALID, "null argument");
   int rc = ctx_device(ctx);
@@ -1034,6 +1162,13 @@ int vpt_gpu_launch_info(const vpt_gpu_ctx* ctx, int* grid_blocks, int* block_thr
   if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
   if (grid_blocks) *grid_blocks = ctx->grid_blocks;
   if (block_threads) *block_threads = vpt::kBlockThreads;
+  return VPT_OK;
+}
+
+int vpt_gpu_latency_kernel_info(const vpt_gpu_ctx* ctx, int* mode, int* resident_blocks_per_cu) {
+  if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
+  if (mode) *mode = ctx->lat_mode;
+  if (resident_blocks_per_cu) *resident_blocks_per_cu = ctx->lat_per_cu;
   return VPT_OK;
 }
 

@@ -8,7 +8,7 @@
 // the layout below is restated from NanoVDB 32.x (NanoVDB.h; float grids, NANOVDB_USE_SINGLE_ROOT_KEY),
 // as volume_path_tracer_amd/nvdb.py does in Python -- parity with the real library is unpinned:
 //
-//   GridData     672 B  magic u64 @0, gridSize u64 @32, Map {mMatF 9f, mInvMatF 9f, mVecF 3f} @296,
+//   GridData     672 B  magic u64 @0, version u32 @16 (major = bits 21+, must be 32), gridSize u64 @32, Map {mMatF 9f, mInvMatF 9f, mVecF 3f} @296,
 //                       gridClass u32 @632, gridType u32 @636 (1 = float)
 //   TreeData      64 B  @672: node offsets i64 [leaf, lower, upper, root] from TreeData
 //   RootData      64 B  bbox 6 i32, tableSize u32 @24, background f32 @28; then tableSize tiles of 32 B:
@@ -29,6 +29,8 @@
 #include <cstring>
 #include <fstream>
 #include <memory>
+#include <new>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -46,6 +48,7 @@ constexpr size_t kGridData = 672, kTreeData = 64, kRootData = 64, kRootTile = 32
 constexpr size_t kUpperMasks = 32, kUpperTable = 8256, kUpperSize = 8256 + 32768 * 8;
 constexpr size_t kLowerMasks = 32, kLowerTable = 1088, kLowerSize = 1088 + 4096 * 8;
 constexpr size_t kLeafMask = 16, kLeafMax = 84, kLeafValues = 96, kLeafSize = 96 + 512 * 4;
+constexpr uint64_t kMaxGridBytes = 1ULL << 40;  // 1 TiB: larger is not a grid this host could hold
 
 struct Buf {
   const uint8_t* p;
@@ -77,6 +80,8 @@ int flatten(const Buf& b, OwnedGrid& o) {
   if (b.n < kGridData + kTreeData) return bad("shorter than GridData + TreeData");
   const uint64_t magic = b.at<uint64_t>(0);
   if (magic != kMagicNumber && magic != kMagicGrid) return bad("bad magic");
+  if ((b.at<uint32_t>(16) >> 21) != 32)  // GridData::mVersion: the layout above is NanoVDB 32.x's
+    return bad("unsupported NanoVDB major version " + std::to_string(b.at<uint32_t>(16) >> 21));
   if (b.at<uint32_t>(636) != kGridTypeFloat) return bad("grid type is not float");
   const uint64_t grid_size = b.at<uint64_t>(32);
   if (grid_size > b.n) return bad("gridSize exceeds the buffer");
@@ -170,6 +175,9 @@ int read_blob(const std::vector<uint8_t>& f, size_t& pos, uint16_t codec, uint64
   uint64_t n;
   std::memcpy(&n, f.data() + pos, 8);
   if (n > f.size() - pos - 8) return set_error(VPT_E_INVALID, "nvdb: grid '" + name + "' truncated");
+  // gridSize comes from the file: bound it before allocating (deflate expands at most ~1032:1)
+  if (out && (grid_size > kMaxGridBytes || grid_size > 1032 * (n + 64)))
+    return set_error(VPT_E_INVALID, "nvdb: grid '" + name + "': implausible gridSize " + std::to_string(grid_size));
   if (out) {
     out->resize(grid_size);
     uLongf len = (uLongf)grid_size;
@@ -186,19 +194,37 @@ int read_blob(const std::vector<uint8_t>& f, size_t& pos, uint16_t codec, uint64
 extern "C" int vpt_grid_from_nanovdb(const void* grid_buffer, size_t bytes, vpt_grid_desc** out) {
   if (!grid_buffer || !out) return vpt::set_error(VPT_E_INVALID, "vpt_grid_from_nanovdb: null argument");
   *out = nullptr;
-  std::unique_ptr<vpt::OwnedGrid> o(vpt::owned_grid_new());
-  const int rc = vpt::flatten(vpt::Buf{static_cast<const uint8_t*>(grid_buffer), bytes}, *o);
-  if (rc) return rc;
-  *out = &o.release()->d;
-  return VPT_OK;
+  try {  // no C++ exception crosses the C ABI (allocation failures of a huge grid)
+    std::unique_ptr<vpt::OwnedGrid> o(vpt::owned_grid_new());
+    const int rc = vpt::flatten(vpt::Buf{static_cast<const uint8_t*>(grid_buffer), bytes}, *o);
+    if (rc) return rc;
+    *out = &o.release()->d;
+    return VPT_OK;
+  } catch (const std::bad_alloc&) {
+    return vpt::set_error(VPT_E_NOMEM, "vpt_grid_from_nanovdb: out of host memory");
+  } catch (const std::exception& e) {
+    return vpt::set_error(VPT_E_INVALID, std::string("vpt_grid_from_nanovdb: ") + e.what());
+  }
 }
 
 // nanovdb::io::readGrid(path, name) for float grids (src/volume_grids.cpp:38-46): file segments
 // (FileHeader 16 B: magic, version, gridCount u16, codec u16; gridCount x (FileMetaData 176 B: gridSize
 // @0, gridType @32, nameSize @136, codec @168; name); then the grid blobs).
+static int read_nvdb(const char* path, const char* grid_name, vpt_grid_desc** out);
+
 extern "C" int vpt_grid_read_nvdb(const char* path, const char* grid_name, vpt_grid_desc** out) {
   if (!path || !grid_name || !out) return vpt::set_error(VPT_E_INVALID, "vpt_grid_read_nvdb: null argument");
   *out = nullptr;
+  try {  // no C++ exception crosses the C ABI
+    return read_nvdb(path, grid_name, out);
+  } catch (const std::bad_alloc&) {
+    return vpt::set_error(VPT_E_NOMEM, "vpt_grid_read_nvdb: out of host memory");
+  } catch (const std::exception& e) {
+    return vpt::set_error(VPT_E_INVALID, std::string("vpt_grid_read_nvdb: ") + e.what());
+  }
+}
+
+static int read_nvdb(const char* path, const char* grid_name, vpt_grid_desc** out) {
   std::ifstream in(path, std::ios::binary);
   if (!in) return vpt::set_error(VPT_E_IO, std::string("vpt_grid_read_nvdb: cannot open ") + path);
   std::vector<uint8_t> f((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());

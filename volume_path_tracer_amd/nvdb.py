@@ -104,6 +104,9 @@ def grid_from_buffer(blob: bytes) -> capi.Grid:
     magic, = struct.unpack_from("<Q", blob, 0)
     if magic not in (MAGIC_NUMBER, MAGIC_GRID):
         raise NvdbError("grid buffer: bad magic")
+    version, = struct.unpack_from("<I", blob, 16)  # GridData::mVersion
+    if (version >> 21) != 32:
+        raise NvdbError(f"grid buffer: unsupported NanoVDB major version {version >> 21}")
     gtype, = struct.unpack_from("<I", blob, 636)
     if gtype != GRID_TYPE_FLOAT:
         raise NvdbError(f"grid buffer: grid type {gtype} is not float")

@@ -192,6 +192,17 @@ class Integrator:
         """-1: the creation-time choice; 0 / 1: force the run-skipping kernel variant off / on."""
         capi.check(capi.lib().vpt_gpu_set_run_skipping(self.h, int(mode)), "vpt_gpu_set_run_skipping")
 
+    def set_latency_kernel(self, mode: int, ungated: int = -1) -> None:
+        """The latency kernel (lane cold state in VGPRs, 4-5 waves per SIMD): -1 auto (launches that fill at
+        most its resident grid: C1, C2, small shares), 0 never, 1 always; `ungated` 1 / 0: its partly filled
+        launches use the latency gates / the context's (-1 keeps).  Samples never depend on it."""
+        capi.check(capi.lib().vpt_gpu_set_latency_kernel(self.h, int(mode), int(ungated)), "vpt_gpu_set_latency_kernel")
+
+    def latency_kernel_info(self) -> dict:
+        m, b = C.c_int(), C.c_int()
+        capi.check(capi.lib().vpt_gpu_latency_kernel_info(self.h, C.byref(m), C.byref(b)), "vpt_gpu_latency_kernel_info")
+        return {"mode": int(m.value), "resident_blocks_per_cu": int(b.value)}
+
     def kernel_variant(self) -> dict:
         """The production kernel this context launches."""
         t, r = C.c_int(), C.c_int()
