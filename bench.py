@@ -114,12 +114,17 @@ def cpu_baseline(wl, dens, temp, budget_s: float = 15.0, runs: int = 3):
         secs.append(ms / 1e3)
     rates.sort()
     med = rates[len(rates) // 2]
+    node = info["nproc"] or threads
     return {"value": round(med, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"waves 1..{k} of {cfg.width}x{cfg.height} ({k * per_wave} samples) per run, median of {runs} "
                       f"runs ({', '.join(f'{r:.3f}' for r in rates)} Msamples/s, {sum(secs):.1f} s), oracle worker "
                       f"pool (main.cpp:62-87 restated), {threads} threads",
             "spread": round((rates[-1] - rates[0]) / med, 4),
-            "per_thread": round(med / threads, 5), "host": info}
+            "per_thread": round(med / threads, 5), "host": info,
+            # not measured: the per-thread rate times every hardware thread of the node (the job is granted
+            # `cores` of them), an upper bound that ignores SMT and memory contention
+            "node_extrapolated": {"threads": node, "value": round(med / threads * node, 3), "unit": "Msamples/s",
+                                  "kind": "linear extrapolation of per_thread, not a measurement"}}
 
 
 def spawn_ranks(args) -> int:
@@ -480,6 +485,8 @@ def main():
             cb = cpu_baseline(wl, dens, temp, args.cpu_budget)
             out["cpu_baseline"] = cb
             out["speedup_vs_cpu_baseline"] = round(value / cb["value"], 1) if cb["value"] else None
+            ne = cb["node_extrapolated"]["value"]
+            out["speedup_vs_cpu_node_extrapolated"] = round(value / ne, 1) if ne else None
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

@@ -336,6 +336,26 @@ int vpt_gpu_film_free(vpt_gpu_ctx* ctx, float* film_device);
  * buffer owned by the context. */
 int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* ctx, float* film_device, float* film_host_hxwx4);
 
+/* Feeds: one launch of the production kernel that renders job ids pushed by the host while it runs --
+ * the drop-in's way of handing the GPU a TileProvider's tokens as they are taken, with a bounded queue and
+ * no per-batch launch drain (a launch lasts as long as its longest job; a feed's lanes keep taking pushed
+ * jobs instead).  vpt_gpu_feed_open launches it on hip_stream (a stream of this context,
+ * vpt_gpu_stream_create) into film_device (NULL = the context's own film); `window` (rounded up to a power
+ * of two, >= 1024) bounds the jobs pushed and not yet started: vpt_gpu_feed_push blocks while the window is
+ * full (VPT_E_STATE if the launch stops taking jobs for 120 s).  Job ids are any jids (< 2^62), e.g.
+ * token.jid(); their samples equal vpt_gpu_render_jobs's.  vpt_gpu_feed_close publishes the end: the
+ * launch ends once every pushed job is rendered, then adds their sample counts to the film (asynchronous,
+ * on the feed's stream).  vpt_gpu_feed_query: whether a closed feed's work is complete (non-blocking) and
+ * the jobs pushed.  vpt_gpu_feed_destroy closes if needed, waits for the feed's work and frees it;
+ * VPT_E_STATE if lanes gave up waiting for jobs (a lane waits at most 30 s, so a launch always ends).
+ * Feeds use the host-pinned ring (8 bytes per window slot) and run the reference RNG mode. */
+typedef struct vpt_gpu_feed vpt_gpu_feed;
+int vpt_gpu_feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t window, vpt_gpu_feed** out);
+int vpt_gpu_feed_push(vpt_gpu_feed* feed, const uint64_t* jids, uint64_t n);
+int vpt_gpu_feed_close(vpt_gpu_feed* feed);
+int vpt_gpu_feed_query(vpt_gpu_feed* feed, int* done, uint64_t* pushed);
+int vpt_gpu_feed_destroy(vpt_gpu_feed* feed);
+
 /* Zero the context's own film. */
 int vpt_gpu_film_clear(vpt_gpu_ctx* ctx);
 /* Device pointer of the context's own film (for an RCCL reduce), and its element count H*W*4. */

@@ -63,23 +63,23 @@ namespace vpt_gpu {
 // token is released as soon as its job id is recorded.  Every recorded job is rendered (no token is
 // dropped), and the GPU film needs no tile exclusivity: its adds are fp32 atomics.
 //
-// What the caller sees while it runs (main.cpp:101-132 shows the film at 5 FPS with progress() and
-// eta()):
-//   * token run-ahead is bounded: jobs are taken in rounds of batch_jobs, each round launched at once on
-//     one of `rounds_in_flight` streams, and a round's tokens are taken only after the round that last
-//     used its stream has completed -- so the provider's job counter (progress(), eta()) runs ahead of
-//     the rendered work by at most rounds_in_flight rounds, and stop_at_next_wave() stops within them;
-//   * the film is progressive: rounds render into one of two device films; every flush_seconds the
-//     current one is retired (later rounds go to the other), and once its rounds have completed it is
-//     added into film_host (under a mutex shared by all callers) and zeroed.  Sample counts in film_host
-//     therefore rise during the run, a whole job at a time, and the final film is the same sum.
-// Rounds on alternating streams overlap: a launch lasts as long as its longest job, and the next
-// round's jobs fill that drain instead of waiting behind it.
+// The tokens' job ids go to the GPU through a feed (vpt_gpu_feed_*): one running launch of the
+// production kernel takes them as they are pushed, batch_jobs at a time, so
+//   * the launch never drains between batches (a launch lasts as long as its longest job; a feed's lanes
+//     keep taking the jobs pushed after it);
+//   * token run-ahead is bounded: a push blocks while window_jobs pushed jobs have not started, so the
+//     provider's job counter (progress(), eta(), what stop_at_next_wave() cuts) leads the GPU by at most
+//     the window plus the jobs in flight -- as the reference's workers each hold the token they render;
+//   * the film is progressive (main.cpp:101-132 shows it at 5 FPS): every flush_seconds the running feed
+//     is closed and a new one opened on the other stream and film (its lanes start as the old launch's
+//     drain frees the CUs); once the old launch has ended, its film is added into film_host (under a
+//     mutex shared by all callers) and zeroed.  film_host's sample counts thus rise during the run, by
+//     whole jobs, and the final film is the same sum.
 using JobRuns = std::vector<std::pair<uint64_t, uint64_t>>;  // contiguous (jid_begin, count) runs
 
 struct DrainOptions {
-  unsigned rounds_in_flight = 2;  // token run-ahead bound, in rounds of batch_jobs
   double flush_seconds = 0.2;     // progressive film period (main.cpp's window draws at 5 FPS)
+  uint64_t window_jobs = 1 << 19;  // pushed jobs not yet started on the GPU (C3: 16 waves, ~25 ms of work)
 };
 
 // Takes up to max_jobs tokens; on_token(token&) sees each before it is released.  Returns the count.
@@ -101,104 +101,92 @@ uint64_t take_jobs(Provider& tp, uint64_t max_jobs, JobRuns& runs, OnToken&& on_
   return taken;
 }
 
-inline int render_runs(vpt_gpu_ctx* ctx, const JobRuns& runs, float* film_device, void* hip_stream) {
-  for (const auto& r : runs)
-    if (int rc = vpt_gpu_render_jobs(ctx, r.first, r.second, film_device, hip_stream)) return rc;
-  return VPT_OK;
-}
-
 inline std::mutex& film_mutex() {  // the host film is shared by every caller
   static std::mutex mu;
   return mu;
 }
 
-// The streams and the second device film of one drain() call.
-class DrainPipeline {
+// Two streams, two device films and the feeds that render into them, for one drain() call.
+class FeedPipeline {
  public:
-  DrainPipeline(vpt_gpu_ctx* ctx, unsigned rounds) : ctx_(ctx), streams_(rounds, nullptr), round_film_(rounds, -1) {}
-  ~DrainPipeline() {
-    for (void* s : streams_)
-      if (s) {
-        (void)vpt_gpu_stream_sync(ctx_, s);
-        (void)vpt_gpu_stream_destroy(ctx_, s);
-      }
+  explicit FeedPipeline(vpt_gpu_ctx* ctx) : ctx_(ctx) {}
+  ~FeedPipeline() {
+    for (int i = 0; i < 2; ++i) {
+      if (feeds_[i]) (void)vpt_gpu_feed_destroy(feeds_[i]);
+      if (streams_[i]) (void)vpt_gpu_stream_destroy(ctx_, streams_[i]);
+    }
     if (films_[1]) (void)vpt_gpu_film_free(ctx_, films_[1]);
   }
-  int init() {
+  int init(uint64_t window) {
+    window_ = window;
     for (void*& s : streams_)
       if (int rc = vpt_gpu_stream_create(ctx_, &s)) return rc;
-    return vpt_gpu_film_alloc(ctx_, &films_[1]);
+    if (int rc = vpt_gpu_film_alloc(ctx_, &films_[1])) return rc;
+    last_switch_ = std::chrono::steady_clock::now();
+    return vpt_gpu_feed_open(ctx_, films_[0], streams_[0], window_, &feeds_[0]);
   }
-  // Round k goes to stream k % rounds: wait for the round that last used it, then flush the retired film
-  // if its last round has completed.
-  int begin_round(uint64_t k, float* film_host) {
-    const size_t i = (size_t)(k % streams_.size());
-    if (round_film_[i] >= 0) {
-      if (int rc = vpt_gpu_stream_sync(ctx_, streams_[i])) return rc;
-      --inflight_[round_film_[i]];
-      round_film_[i] = -1;
+  int push(const JobRuns& runs) {
+    ids_.clear();
+    for (const auto& r : runs)
+      for (uint64_t i = 0; i < r.second; ++i) ids_.push_back(r.first + i);
+    return vpt_gpu_feed_push(feeds_[cur_], ids_.data(), ids_.size());
+  }
+  // Adds the retired feed's film to film_host once its launch has ended; every flush_seconds retires the
+  // current feed (the other one must have been flushed) and opens the next on the other stream and film.
+  int tick(double flush_seconds, float* film_host) {
+    const int old = cur_ ^ 1;
+    if (feeds_[old]) {
+      int done = 0;
+      if (int rc = vpt_gpu_feed_query(feeds_[old], &done, nullptr)) return rc;
+      if (done)
+        if (int rc = flush(old, film_host)) return rc;
     }
-    return retired_ >= 0 && inflight_[retired_] == 0 ? flush(retired_, film_host) : VPT_OK;
-  }
-  // Retire the current film when the period is up (and the other film is free).
-  void maybe_retire(double flush_seconds) {
     const auto now = std::chrono::steady_clock::now();
-    if (retired_ < 0 && std::chrono::duration<double>(now - last_retire_).count() >= flush_seconds) {
-      retired_ = current_;
-      current_ ^= 1;
-      last_retire_ = now;
+    if (!feeds_[old] && std::chrono::duration<double>(now - last_switch_).count() >= flush_seconds) {
+      if (int rc = vpt_gpu_feed_close(feeds_[cur_])) return rc;
+      cur_ = old;
+      last_switch_ = now;
+      return vpt_gpu_feed_open(ctx_, films_[cur_], streams_[cur_], window_, &feeds_[cur_]);
     }
-  }
-  int launch(uint64_t k, const JobRuns& runs) {
-    const size_t i = (size_t)(k % streams_.size());
-    round_film_[i] = current_;
-    ++inflight_[current_];
-    return render_runs(ctx_, runs, films_[current_], streams_[i]);
+    return VPT_OK;
   }
   int finish(float* film_host) {
-    for (size_t i = 0; i < streams_.size(); ++i)
-      if (round_film_[i] >= 0) {
-        if (int rc = vpt_gpu_stream_sync(ctx_, streams_[i])) return rc;
-        --inflight_[round_film_[i]];
-        round_film_[i] = -1;
-      }
-    for (int f = 0; f < 2; ++f)
-      if (int rc = flush(f, film_host)) return rc;
+    for (int i = 0; i < 2; ++i)
+      if (feeds_[i])
+        if (int rc = flush(i, film_host)) return rc;
     return VPT_OK;
   }
 
  private:
-  int flush(int f, float* film_host) {
+  int flush(int i, float* film_host) {
+    const int rc = vpt_gpu_feed_destroy(feeds_[i]);  // waits for the feed's launch and its sample counts
+    feeds_[i] = nullptr;
+    if (rc) return rc;
     std::lock_guard<std::mutex> lock(film_mutex());
-    if (int rc = vpt_gpu_film_flush_to_host(ctx_, films_[f], film_host)) return rc;
-    if (retired_ == f) retired_ = -1;
-    return VPT_OK;
+    return vpt_gpu_film_flush_to_host(ctx_, films_[i], film_host);
   }
   vpt_gpu_ctx* ctx_;
-  std::vector<void*> streams_;
-  std::vector<int> round_film_;   // film of the round last launched on each stream (-1: none / done)
+  uint64_t window_ = 0;
+  void* streams_[2] = {nullptr, nullptr};
   float* films_[2] = {nullptr, nullptr};  // [0]: the context's own film (NULL), [1]: allocated
-  int inflight_[2] = {0, 0};      // rounds launched into each film and not known to be complete
-  int current_ = 0, retired_ = -1;
-  std::chrono::steady_clock::time_point last_retire_ = std::chrono::steady_clock::now();
+  vpt_gpu_feed* feeds_[2] = {nullptr, nullptr};
+  int cur_ = 0;
+  std::vector<uint64_t> ids_;
+  std::chrono::steady_clock::time_point last_switch_;
 };
 
-// `first`: job runs already taken by the caller (launched as round 0).
+// `first`: job runs already taken by the caller (pushed first).
 template <class Provider>
 int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs, const DrainOptions& opt = {},
           const JobRuns* first = nullptr) {
-  DrainPipeline pipe(ctx, std::max(1u, opt.rounds_in_flight));
-  if (int rc = pipe.init()) return rc;
+  FeedPipeline pipe(ctx);
+  if (int rc = pipe.init(opt.window_jobs)) return rc;
+  if (first)
+    if (int rc = pipe.push(*first)) return rc;
   JobRuns runs;
-  for (uint64_t k = 0;; ++k) {
-    if (int rc = pipe.begin_round(k, film_host)) return rc;
-    if (k == 0 && first) {
-      runs = *first;
-    } else if (!take_jobs(tp, std::max<uint64_t>(1, batch_jobs), runs, [](auto&) {})) {
-      break;
-    }
-    pipe.maybe_retire(opt.flush_seconds);
-    if (int rc = pipe.launch(k, runs)) return rc;
+  while (take_jobs(tp, std::max<uint64_t>(1, batch_jobs), runs, [](auto&) {})) {
+    if (int rc = pipe.push(runs)) return rc;
+    if (int rc = pipe.tick(opt.flush_seconds, film_host)) return rc;
   }
   return pipe.finish(film_host);
 }
@@ -407,8 +395,9 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
     ~Ctx() { vpt_gpu_destroy(c); }
   } guard{ctx};
   float* film_host = reinterpret_cast<float*>(film.data().data());  // H x W x (X, Y, Z, W)
-  // the first batch is round 0; later rounds: 8 waves of jobs each
-  return drain(ctx, tp, film_host, 8 * T, DrainOptions{}, &runs);
+  // the first batch is pushed first; then 4096 tokens per push (a token is one 8x8 job: 64 samples)
+  (void)T;
+  return drain(ctx, tp, film_host, 4096, DrainOptions{}, &runs);
 }
 
 template <class WorkerParameters, class Volume, class Camera, class TileProvider, class Image, class RNG>

@@ -208,3 +208,54 @@ def test_library_before_torch_keeps_one_hip_runtime():
     r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "runtimes 1 samples 256" in r.stdout, r.stdout
+
+
+@pytest.mark.gpu
+def test_feed_renders_pushed_jobs_in_any_order():
+    """vpt_gpu_feed_*: job ids pushed while the launch runs -- out of order, with gaps and past a full
+    window (1024 slots for 2 880 jobs, so pushes wait for the GPU) -- render the oracle's samples; the
+    close adds exactly the pushed jobs' sample counts.  Two feeds of one context on two streams."""
+    import ctypes as C
+
+    import torch
+
+    from volume_path_tracer_amd import capi
+    from volume_path_tracer_amd.render import Integrator
+
+    wl = workload("c3", width=96, height=80, spp=24, grid_n=64)
+    dens = SynthGrid(1, 64).grid()
+    it = Integrator(wl.cfg, dens, None, device=0)
+    L = capi.lib()
+    T = wl.cfg.jobs_per_wave()
+    rng = np.random.default_rng(3)
+    jids = rng.permutation(24 * T)[: 24 * T - 37].astype(np.uint64)  # 37 jobs never pushed
+    films = [torch.zeros_like(it.film) for _ in range(2)]
+    streams = [C.c_void_p() for _ in range(2)]
+    for s in streams:
+        capi.check(L.vpt_gpu_stream_create(it.h, C.byref(s)), "stream")
+    feeds = []
+    halves = np.array_split(jids, 2)
+    for k in range(2):
+        f = C.c_void_p()
+        capi.check(L.vpt_gpu_feed_open(it.h, C.c_void_p(films[k].data_ptr()), streams[k], 1000, C.byref(f)), "open")
+        feeds.append(f)
+    for part in np.array_split(halves[0], 7):
+        capi.check(L.vpt_gpu_feed_push(feeds[0], part.ctypes.data_as(C.POINTER(C.c_uint64)), part.size), "push")
+    capi.check(L.vpt_gpu_feed_push(feeds[1], halves[1].ctypes.data_as(C.POINTER(C.c_uint64)), halves[1].size), "push")
+    for f in feeds:
+        capi.check(L.vpt_gpu_feed_close(f), "close")
+        capi.check(L.vpt_gpu_feed_destroy(f), "destroy")
+    for s in streams:
+        capi.check(L.vpt_gpu_stream_destroy(it.h, s), "stream destroy")
+    total = (films[0] + films[1]).cpu().numpy()
+    od = O.OracleGrid(dens, fix_majorants=True)
+    ref = np.zeros_like(total)
+    # the oracle renders the pushed jobs (contiguous runs of the sorted ids)
+    s = np.sort(jids).astype(np.int64)
+    breaks = np.flatnonzero(np.diff(s) != 1) + 1
+    for run in np.split(s, breaks):
+        f, _, _ = O.render_jobs(wl.cfg, od, None, int(run[0]), int(run.size))
+        ref += f
+    counts = np.bincount((jids % T).astype(np.int64), minlength=T).reshape(wl.cfg.height // 8, wl.cfg.width // 8)
+    np.testing.assert_array_equal(total[..., 3], np.kron(counts, np.ones((8, 8))))
+    np.testing.assert_allclose(total[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)

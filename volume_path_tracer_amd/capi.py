@@ -267,6 +267,12 @@ def lib() -> C.CDLL:
         L.vpt_gpu_film_alloc.argtypes = [vp, C.POINTER(vp)]
         L.vpt_gpu_film_free.argtypes = [vp, vp]
         L.vpt_gpu_film_flush_to_host.argtypes = [vp, vp, fp]
+    if hasattr(L, "vpt_gpu_feed_open"):
+        L.vpt_gpu_feed_open.argtypes = [vp, vp, vp, C.c_uint64, C.POINTER(vp)]
+        L.vpt_gpu_feed_push.argtypes = [vp, C.POINTER(C.c_uint64), C.c_uint64]
+        L.vpt_gpu_feed_close.argtypes = [vp]
+        L.vpt_gpu_feed_query.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_uint64)]
+        L.vpt_gpu_feed_destroy.argtypes = [vp]
     _lib = L
     return L
 

@@ -14,7 +14,9 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "vpt_internal.h"
@@ -60,6 +62,13 @@ constexpr int kBlockThreads = 256;
 
 // The lanes' cold state (vpt_integrator.h LaneCold), one slot per thread of the integrator's block.
 __shared__ LaneCold g_lane_cold[kBlockThreads];
+// Feed mode (vpt_gpu_feed_*): the published word's closed bit, an empty ring slot, a lane's "item
+// reserved, not yet published" mark (LaneCold::pix), and how long a lane waits for its item before it
+// gives up (s_memrealtime ticks at 100 MHz: 30 s).
+constexpr uint64_t kFeedClosed = 1ULL << 63;
+constexpr uint64_t kFeedEmpty = ~0ULL;
+constexpr int32_t kFeedPending = -2;
+constexpr uint32_t kFeedDeadline = 3000000000u;
 // LDS copies of the small lookup tables the evaluation reads per lane (logf's 16 x 2 doubles; the
 // temperature kernel's 501 x 3 blackbody table): LDS reads instead of vector-memory loads, which
 // would count in vmcnt with the walk's loads.
@@ -86,6 +95,14 @@ struct KernelEnvT {
   vpt_event* events;                 // Logger events (trace launches only)
   unsigned long long* event_count;
   uint64_t event_cap;
+  // Feed mode (vpt_gpu_feed_*: the launch takes job ids the host pushes while it runs): host-pinned
+  // coherent memory shared with the host -- the published word (items published | kFeedClosed) and
+  // the ring of job ids (kFeedEmpty once read) -- and an error word in device memory.  nullptr:
+  // items are job_counter values < jid_count (every other launch).
+  const uint64_t* feed_word;
+  uint64_t* feed_ring;
+  uint64_t feed_mask;                // ring slots - 1 (a power of two)
+  unsigned* feed_error;
 
   // Adds w for every active lane with w != 0 (w uniform per call site) to a workgroup counter.
   __device__ __forceinline__ void tally(int32_t k, int32_t w) {
@@ -189,16 +206,56 @@ struct KernelEnvT {
   // one lane with a few jobs in a row wins: C1 frames on the full grid (r02g,
   // profiles/r02g_c1_lanes_sweep.txt), 1 / 2 / 3 lanes: 8 spp (x = 1.1) 23.3 / 29.3 / - ms, 16 spp
   // (x = 2.3) 31.7 / 32.5 / 35.6, 32 spp (x = 4.6) 51.9 / 43.1 / 42.1 (5 lanes: 41.5).
-  __device__ __forceinline__ bool fetch_job(uint64_t& j, int32_t wave_lanes) {
+  __device__ __forceinline__ int fetch_job(uint64_t& j, int32_t wave_lanes) {
+    if (!RegCold && feed_word) return fetch_feed(j);  // (feeds run the throughput kernels only)
     if (wave_lanes == 0) {
       const float x = (float)jid_count * __builtin_amdgcn_rcpf((float)(gridDim.x * (kBlockThreads / 64)));
       wave_lanes = x < 3.0f ? 1 : 1 + (int32_t)x;
     }
     if ((int32_t)__lane_id() >= wave_lanes) return false;
     unsigned long long v = atomicAdd(job_counter, 1ULL);
-    if (v >= jid_count) return false;
+    if (v >= jid_count) return 0;
     j = v;
-    return true;
+    return 1;
+  }
+  // Feed mode: the lane reserves item k (one atomic on the launch's counter) and keeps it in its cold
+  // state (item_lo / item_hi; pix = kFeedPending) until the host has published it: then it reads the job
+  // id from ring slot k & feed_mask and marks the slot empty for the host to reuse.  Once the feed is
+  // closed, items beyond the published count are never published: the lane ends.  A lane that waits
+  // kFeedDeadline without either (a host that died) ends too and flags feed_error, so the grid always
+  // drains.  The loads and stores of host memory are vector-memory atomics of system scope.
+  __device__ int fetch_feed(uint64_t& j) {
+    LaneCold& lc = cold();
+    const uint32_t now = (uint32_t)__builtin_amdgcn_s_memrealtime();  // 100 MHz
+    if (lc.pix != kFeedPending) {
+      const uint64_t k = atomicAdd(job_counter, 1ULL);
+      lc.item_lo = (uint32_t)k;
+      lc.item_hi = (uint32_t)(k >> 32);
+      lc.pix = kFeedPending;
+      lc.x0 = (int32_t)now;  // wait start
+    }
+    const uint64_t k = ((uint64_t)lc.item_hi << 32) | lc.item_lo;
+    // Relaxed system-scope loads of host memory go to the host every time; the slot is read only after
+    // the word has shown it published (a control dependency), and the host wrote it before the word.
+    const uint64_t w = __hip_atomic_load(feed_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (k < (w & ~kFeedClosed)) {
+      uint64_t* slot = feed_ring + (k & feed_mask);
+      j = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      // The empty mark is stored only once the id has arrived (a posted write may overtake a read on the
+      // host link, and the host reuses the slot as soon as it sees the mark): the asm takes j as an input,
+      // so the compiler waits for the load before it.
+      uint64_t empty = kFeedEmpty;
+      asm volatile("" : "+v"(empty) : "v"(j));
+      __hip_atomic_store(slot, empty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      lc.pix = 0;
+      return 1;
+    }
+    if (w & kFeedClosed) return 0;
+    if (now - (uint32_t)lc.x0 > kFeedDeadline) {
+      atomicOr(feed_error, 1u);
+      return 0;
+    }
+    return -1;
   }
   __device__ __forceinline__ void film_add(const DevScene& S, const Lane& ln, int32_t px, int32_t py, int32_t rw) {
     float* f = film + ((int64_t)py * S.W + px) * 4;
@@ -252,7 +309,15 @@ __global__ __launch_bounds__(kBlockThreads, Lat ? VPT_WAVES_LAT : (Debug ? VPT_W
   if constexpr (Lat) env.reg_cold = &lc_reg;
   cold_init(env.cold());
   const ScenePtr sp = (ScenePtr)scene;
-  while (ln.state != ST_DONE) lane_iteration<HasTemp, Debug, Runs>(sp, ln, env);
+  while (ln.state != ST_DONE) {
+    lane_iteration<HasTemp, Debug, Runs>(sp, ln, env);
+    // Feed mode: a wavefront whose every live lane waits for the host to publish its item sleeps between
+    // polls (~27 us), so idle wavefronts do not flood the host link with reads.
+    if (!Debug && !Lat && env.feed_word &&
+        __builtin_amdgcn_ballot_w64(ln.state == ST_FETCH && env.cold().pix == kFeedPending) ==
+            __builtin_amdgcn_read_exec())
+      for (int i = 0; i < 8; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   atomicAdd(wg_counters + CNT_DDA_STEPS, (unsigned long long)ln.n_dda);
   __syncthreads();
   if (threadIdx.x < kCounterCount && wg_counters[threadIdx.x])
@@ -278,6 +343,18 @@ __global__ void vpt_count_kernel(const DevScene* scene, float* film, uint64_t ji
   if (t >= end || t + k0 * T >= end) return;
   const uint64_t n = (end - 1 - t) / T - k0 + 1;
   atomicAdd(film + p * 4 + 3, (float)n);
+}
+
+// The film's sample-count channel of a feed (vpt_gpu_feed_close): a pixel of tile t gains the number of
+// its jobs the host pushed, counts[t] (the same integer sums as vpt_count_kernel's).
+__global__ void vpt_tile_count_kernel(const DevScene* scene, float* film, const uint32_t* counts) {
+  const DevScene& S = *scene;
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= (uint64_t)S.W * (uint64_t)S.H) return;
+  const int32_t px = (int32_t)(p % (uint64_t)S.W), py = (int32_t)(p / (uint64_t)S.W);
+  if (S.single_pixel_enabled && (px != S.sp_x || py != S.sp_y)) return;
+  const uint32_t n = counts[(uint64_t)(py / S.th) * S.ntx + (uint64_t)(px / S.tw)];
+  if (n) atomicAdd(film + p * 4 + 3, (float)n);
 }
 
 // Volume::log_majorant_trace (src/volume.cpp:176-192) of one world ray, on one lane: every
@@ -421,6 +498,16 @@ static void free_grid(DeviceGrid& d) {
   d = DeviceGrid{};
 }
 
+}  // namespace vpt
+
+namespace vpt {
+// The shared state of an open feed, as its launch sees it (see KernelEnvT::fetch_feed).
+struct FeedLaunch {
+  const uint64_t* word;
+  uint64_t* ring;
+  uint64_t mask;
+  unsigned* error;
+};
 }  // namespace vpt
 
 struct vpt_gpu_ctx {
@@ -597,11 +684,14 @@ int ensure_order(vpt_gpu_ctx* ctx) {
 }
 
 int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film, float* records, void* stream_ptr,
-           vpt_event* events = nullptr, uint64_t event_cap = 0, uint32_t* slot_out = nullptr) {
+           vpt_event* events = nullptr, uint64_t event_cap = 0, uint32_t* slot_out = nullptr,
+           const vpt::FeedLaunch* feed = nullptr) {
   if (!ctx) return vpt::set_error(VPT_E_INVALID, "render: null context");
   int rc = ctx_device(ctx);
   if (rc) return rc;
   if (jid_count == 0) return VPT_OK;
+  if (feed && (ctx->scene.pixel_mode || records || events))
+    return vpt::set_error(VPT_E_INVALID, "render: feeds run the reference RNG mode's production kernels only");
   const uint64_t total = ctx->scene.T * (uint64_t)ctx->cfg.num_waves;
   (void)total;  // jids beyond num_waves are valid jobs too (TileProvider only stops at requested_waves)
   hipStream_t s = (hipStream_t)stream_ptr;  // NULL = the null stream (HIP convention)
@@ -672,11 +762,11 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   // most its resident grid anyway: latency-bound ones (on its whole grid) and partly filled ones whose
   // rule above gives <= lat_per_cu blocks per CU (C2: 2).  Same jobs, same samples.
   const uint64_t lat_blocks = cus * (uint64_t)ctx->lat_per_cu;
-  const bool use_lat = !dbg && ctx->lat_mode != 0 &&
+  const bool use_lat = !dbg && !feed && ctx->lat_mode != 0 &&
                        (ctx->lat_mode == 1 || (!ctx->grid_user && (latency || blocks <= lat_blocks)));
   if (use_lat) blocks = (uint32_t)std::min<uint64_t>(latency ? lat_blocks : blocks, lat_blocks);
   const uint64_t T = ctx->scene.T;
-  if (ctx->order_mode != VPT_ORDER_JID && jid_begin % T == 0 && jid_count % T == 0 && jid_count < (1ULL << 32)) {
+  if (!feed && ctx->order_mode != VPT_ORDER_JID && jid_begin % T == 0 && jid_count % T == 0 && jid_count < (1ULL << 32)) {
     // whole waves: take the jobs in cost order (same jobs, same samples)
     if ((rc = ensure_order(ctx))) return rc;
     const uint32_t n = (uint32_t)(jid_count / T);
@@ -692,11 +782,15 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
     env.order_tail_n = tail;
     env.order_tail_k0 = (n - tail) * (uint32_t)T;
   }
-  if (ctx->perm && ctx->perm_n == jid_count && !ctx->scene.pixel_mode) env.perm = ctx->perm;
+  if (!feed && ctx->perm && ctx->perm_n == jid_count && !ctx->scene.pixel_mode) env.perm = ctx->perm;
   uint32_t slot = 0;
   if ((rc = take_slot(ctx, s, slot))) return rc;
   env.job_counter = ctx->job_counter + 2 * slot;
   env.events = events;
+  env.feed_word = feed ? feed->word : nullptr;
+  env.feed_ring = feed ? feed->ring : nullptr;
+  env.feed_mask = feed ? feed->mask : 0;
+  env.feed_error = feed ? feed->error : nullptr;
   env.event_count = ctx->job_counter + 2 * slot + 1;
   env.event_cap = event_cap;
   if (slot_out) *slot_out = slot;
@@ -718,9 +812,11 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   }
   VPT_HIP(hipGetLastError());
   const uint64_t npix = (uint64_t)ctx->scene.W * (uint64_t)ctx->scene.H;
-  hipLaunchKernelGGL(vpt::vpt_count_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, ctx->scene_dev,
-                     env.film, jid_begin, jid_count);
-  VPT_HIP(hipGetLastError());
+  if (!feed) {  // a feed adds its sample counts when it is closed (vpt_tile_count_kernel)
+    hipLaunchKernelGGL(vpt::vpt_count_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, ctx->scene_dev,
+                       env.film, jid_begin, jid_count);
+    VPT_HIP(hipGetLastError());
+  }
   return release_slot(ctx, s, slot);
 }
 
@@ -1061,6 +1157,158 @@ int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* ctx, float* film_device, float* film
   const float* src = ctx->staging;
   for (uint64_t i = 0; i < ctx->film_count; ++i) film_host[i] += src[i];
   return VPT_OK;
+}
+
+}  // extern "C"
+
+// A feed: one launch of the production kernel that renders job ids as the host pushes them (see
+// include/vpt_gpu.h).  Its host-pinned, coherent block holds the published word, then the ring of
+// job ids, then the per-tile job counts the close adds to the film's sample-count channel.
+struct vpt_gpu_feed {
+  vpt_gpu_ctx* ctx = nullptr;
+  hipStream_t stream = nullptr;
+  float* film = nullptr;
+  uint64_t* block = nullptr;  // hipHostMalloc'd: [8] word + padding, [cap] ring, then uint32 counts[T]
+  uint64_t* word = nullptr;
+  uint64_t* ring = nullptr;
+  uint32_t* counts = nullptr;
+  uint64_t cap = 0;
+  uint64_t published = 0;
+  unsigned* error = nullptr;  // device
+  hipEvent_t closed_ev = nullptr;
+  bool closed = false;
+};
+
+namespace {
+constexpr double kFeedHostWaitS = 120.0;  // a push waiting this long for a ring slot gives up
+
+void feed_free(vpt_gpu_feed* f) {
+  if (!f) return;
+  (void)hipSetDevice(f->ctx->device);
+  if (f->closed_ev) (void)hipEventDestroy(f->closed_ev);
+  (void)hipFree(f->error);
+  (void)hipHostFree(f->block);
+  delete f;
+}
+
+// Publishes items [0, published) and, with close, the end of the feed (release: the ring and count
+// stores are visible to the GPU before the word that publishes them).
+void feed_publish(vpt_gpu_feed* f, bool close) {
+  __atomic_store_n(f->word, f->published | (close ? vpt::kFeedClosed : 0), __ATOMIC_RELEASE);
+}
+}  // namespace
+
+extern "C" {
+
+int vpt_gpu_feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t window, vpt_gpu_feed** out) {
+  if (!ctx || !out || !hip_stream) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_open: null argument");
+  *out = nullptr;
+  if (ctx->scene.pixel_mode) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_open: feeds run the reference RNG mode");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  uint64_t cap = 1024;
+  while (cap < window && cap < (1ULL << 26)) cap <<= 1;
+  std::unique_ptr<vpt_gpu_feed, void (*)(vpt_gpu_feed*)> f(new vpt_gpu_feed(), feed_free);
+  f->ctx = ctx;
+  f->stream = (hipStream_t)hip_stream;
+  f->film = film_device ? film_device : ctx->film;
+  f->cap = cap;
+  const size_t bytes = (8 + cap) * sizeof(uint64_t) + ctx->scene.T * sizeof(uint32_t);
+  VPT_HIP(hipHostMalloc((void**)&f->block, bytes, hipHostMallocCoherent | hipHostMallocMapped));
+  f->word = f->block;
+  f->ring = f->block + 8;  // its own cache lines, away from the word the waiting wavefronts poll
+  f->counts = reinterpret_cast<uint32_t*>(f->ring + cap);
+  for (uint64_t i = 0; i < cap; ++i) f->ring[i] = vpt::kFeedEmpty;
+  std::memset(f->counts, 0, ctx->scene.T * sizeof(uint32_t));
+  __atomic_store_n(f->word, 0ULL, __ATOMIC_RELEASE);
+  VPT_HIP(hipMalloc((void**)&f->error, sizeof(unsigned)));
+  VPT_HIP(hipMemsetAsync(f->error, 0, sizeof(unsigned), f->stream));
+  VPT_HIP(hipEventCreateWithFlags(&f->closed_ev, hipEventDisableTiming));
+  uint64_t *word_dev = nullptr, *ring_dev = nullptr;
+  VPT_HIP(hipHostGetDevicePointer((void**)&word_dev, f->word, 0));
+  ring_dev = word_dev + 8;
+  const vpt::FeedLaunch fl{word_dev, ring_dev, cap - 1, f->error};
+  if ((rc = render(ctx, 0, ~0ULL >> 1, f->film, nullptr, hip_stream, nullptr, 0, nullptr, &fl))) return rc;
+  *out = f.release();
+  return VPT_OK;
+}
+
+int vpt_gpu_feed_push(vpt_gpu_feed* f, const uint64_t* jids, uint64_t n) {
+  if (!f || (n && !jids)) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_push: null argument");
+  if (f->closed) return vpt::set_error(VPT_E_STATE, "vpt_gpu_feed_push: the feed is closed");
+  const uint64_t T = f->ctx->scene.T;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t jid = jids[i];
+    if (jid >> 62) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_push: job id out of range");
+    uint64_t* slot = f->ring + (f->published & (f->cap - 1));
+    if (__atomic_load_n(slot, __ATOMIC_ACQUIRE) != vpt::kFeedEmpty) {
+      // the window is full (cap items published and not yet started): publish what we have, then wait
+      feed_publish(f, false);
+      while (__atomic_load_n(slot, __ATOMIC_ACQUIRE) != vpt::kFeedEmpty) {
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kFeedHostWaitS)
+          return vpt::set_error(VPT_E_STATE, "vpt_gpu_feed_push: the feed's launch stopped taking jobs");
+      }
+    }
+    *slot = jid;
+    ++f->counts[jid % T];
+    ++f->published;
+  }
+  feed_publish(f, false);
+  return VPT_OK;
+}
+
+int vpt_gpu_feed_close(vpt_gpu_feed* f) {
+  if (!f) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_close: null feed");
+  if (f->closed) return VPT_OK;
+  int rc = ctx_device(f->ctx);
+  if (rc) return rc;
+  f->closed = true;
+  feed_publish(f, true);
+  // after the launch: the pushed jobs' sample counts (read from the pinned block, final now)
+  uint32_t* counts_dev = nullptr;
+  VPT_HIP(hipHostGetDevicePointer((void**)&counts_dev, f->counts, 0));
+  const uint64_t npix = (uint64_t)f->ctx->scene.W * (uint64_t)f->ctx->scene.H;
+  hipLaunchKernelGGL(vpt::vpt_tile_count_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, f->stream,
+                     f->ctx->scene_dev, f->film, counts_dev);
+  VPT_HIP(hipGetLastError());
+  VPT_HIP(hipEventRecord(f->closed_ev, f->stream));
+  return VPT_OK;
+}
+
+int vpt_gpu_feed_query(vpt_gpu_feed* f, int* done, uint64_t* pushed) {
+  if (!f) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_query: null feed");
+  if (pushed) *pushed = f->published;
+  if (done) {
+    *done = 0;
+    if (f->closed) {
+      const hipError_t e = hipEventQuery(f->closed_ev);
+      if (e == hipSuccess)
+        *done = 1;
+      else if (e != hipErrorNotReady)
+        return vpt::set_error(VPT_E_HIP, std::string("vpt_gpu_feed_query: ") + hipGetErrorString(e));
+    }
+  }
+  return VPT_OK;
+}
+
+int vpt_gpu_feed_destroy(vpt_gpu_feed* f) {
+  if (!f) return VPT_OK;
+  int rc = vpt_gpu_feed_close(f);
+  bool complete = false;
+  if (rc == VPT_OK) {
+    const hipError_t e = hipEventSynchronize(f->closed_ev);
+    if (e != hipSuccess)
+      rc = vpt::set_error(VPT_E_HIP, std::string("vpt_gpu_feed_destroy: ") + hipGetErrorString(e));
+    else
+      complete = true;
+  }
+  unsigned err = 0;
+  if (complete && hipMemcpy(&err, f->error, sizeof err, hipMemcpyDeviceToHost) == hipSuccess && err)
+    rc = vpt::set_error(VPT_E_STATE, "vpt_gpu_feed_destroy: lanes of the feed's launch gave up waiting for jobs");
+  if (complete) feed_free(f);  // (after a HIP failure the launch may still read the block: leak it)
+  return rc;
 }
 
 int vpt_gpu_film_clear(vpt_gpu_ctx* ctx) {
