@@ -405,10 +405,13 @@ def main():
     if args.rng_mode == "pixel":
         from volume_path_tracer_amd import capi
         it.set_rng_mode(capi.VPT_RNG_PIXEL)
-    lat_mode = {"auto": -1, "off": 0, "on": 1}[args.latency_kernel]
-    it.set_latency_kernel(lat_mode)
+    from volume_path_tracer_amd import capi as _capi
+    lat_info = None
+    if hasattr(_capi.lib(), "vpt_gpu_set_latency_kernel"):  # (A/B runs against older library builds lack it)
+        it.set_latency_kernel({"auto": -1, "off": 0, "on": 1}[args.latency_kernel])
+        lat_info = it.latency_kernel_info()
     log(f"[rank {rank}] grids ready in {time.time() - t0:.1f}s: {dens.leaf_count} leaves, "
-        f"launch {it.launch_info()}, latency kernel {it.latency_kernel_info()}")
+        f"launch {it.launch_info()}, latency kernel {lat_info}")
 
     spp = wl.spp
     ranges = D.rank_job_ranges(rank, world, spp, it.jobs_per_wave, args.mode)

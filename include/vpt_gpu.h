@@ -347,8 +347,11 @@ int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* ctx, float* film_device, float* film
  * launch ends once every pushed job is rendered, then adds their sample counts to the film (asynchronous,
  * on the feed's stream).  vpt_gpu_feed_query: whether a closed feed's work is complete (non-blocking) and
  * the jobs pushed.  vpt_gpu_feed_destroy closes if needed, waits for the feed's work and frees it;
- * VPT_E_STATE if lanes gave up waiting for jobs (a lane waits at most 30 s, so a launch always ends).
- * Feeds use the host-pinned ring (8 bytes per window slot) and run the reference RNG mode. */
+ * VPT_E_STATE if lanes gave up waiting for jobs (a lane waits at most 30 s, so a launch always ends: a
+ * feed left open without pushes that long ends by itself).  A feed's launch holds the device's CUs until it
+ * is closed -- a second feed opened meanwhile starts as the first one's lanes leave -- so push to a feed
+ * only after the feeds opened before it have been closed.  Feeds use a host-pinned ring (8 bytes per
+ * window slot) and run the reference RNG mode. */
 typedef struct vpt_gpu_feed vpt_gpu_feed;
 int vpt_gpu_feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t window, vpt_gpu_feed** out);
 int vpt_gpu_feed_push(vpt_gpu_feed* feed, const uint64_t* jids, uint64_t n);

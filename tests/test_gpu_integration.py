@@ -213,8 +213,9 @@ def test_library_before_torch_keeps_one_hip_runtime():
 @pytest.mark.gpu
 def test_feed_renders_pushed_jobs_in_any_order():
     """vpt_gpu_feed_*: job ids pushed while the launch runs -- out of order, with gaps and past a full
-    window (1024 slots for 2 880 jobs, so pushes wait for the GPU) -- render the oracle's samples; the
-    close adds exactly the pushed jobs' sample counts.  Two feeds of one context on two streams."""
+    window (1024 slots for ~2 000 jobs, so pushes wait for the GPU) -- render the oracle's samples; the
+    close adds exactly the pushed jobs' sample counts.  Two feeds of one context on two streams, the
+    second opened while the first runs (its lanes start as the first's leave, once it is closed)."""
     import ctypes as C
 
     import torch
@@ -241,9 +242,10 @@ def test_feed_renders_pushed_jobs_in_any_order():
         feeds.append(f)
     for part in np.array_split(halves[0], 7):
         capi.check(L.vpt_gpu_feed_push(feeds[0], part.ctypes.data_as(C.POINTER(C.c_uint64)), part.size), "push")
+    capi.check(L.vpt_gpu_feed_close(feeds[0]), "close")  # the first launch holds the CUs until then
     capi.check(L.vpt_gpu_feed_push(feeds[1], halves[1].ctypes.data_as(C.POINTER(C.c_uint64)), halves[1].size), "push")
+    capi.check(L.vpt_gpu_feed_close(feeds[1]), "close")
     for f in feeds:
-        capi.check(L.vpt_gpu_feed_close(f), "close")
         capi.check(L.vpt_gpu_feed_destroy(f), "destroy")
     for s in streams:
         capi.check(L.vpt_gpu_stream_destroy(it.h, s), "stream destroy")
