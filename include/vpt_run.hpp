@@ -37,6 +37,7 @@
 #include <array>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -106,9 +107,13 @@ inline std::mutex& film_mutex() {  // the host film is shared by every caller
   return mu;
 }
 
-// Two streams, two device films and the feeds that render into them, for one drain() call.
+// Two streams, two device films and the feeds that render into them, for one drain() call.  push() and
+// tick() are called under mu() when other threads push into the same pipeline (run()'s helpers).
 class FeedPipeline {
  public:
+  std::mutex& mu() { return mu_; }
+  std::condition_variable& cv() { return cv_; }
+  std::atomic<int> helpers{0};  // helper threads attached (see detail::Helpers)
   explicit FeedPipeline(vpt_gpu_ctx* ctx) : ctx_(ctx) {}
   ~FeedPipeline() {
     for (int i = 0; i < 2; ++i) {
@@ -173,22 +178,90 @@ class FeedPipeline {
   int cur_ = 0;
   std::vector<uint64_t> ids_;
   std::chrono::steady_clock::time_point last_switch_;
+  std::mutex mu_;
+  std::condition_variable cv_;
 };
 
-// `first`: job runs already taken by the caller (pushed first).
+namespace detail {
+// run()'s threads on one provider (main.cpp starts num_workers of them): each GPU is driven by the one
+// thread that claimed it; the others -- "helpers" -- take tokens too and push their job ids into a driving
+// thread's pipeline, because one thread takes ~50 M tokens/s (one 8x8 job each) and a GPU can render more
+// (C4: ~84 M jobs/s; several GPUs share one provider).
+struct Helpers {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<FeedPipeline*> pipes;  // pipelines that accept helpers
+  int drivers = 0;                   // threads that claimed a device and have not finished
+  size_t next = 0;
+  static Helpers& get() {
+    static Helpers h;
+    return h;
+  }
+};
+
+}  // namespace detail
+
+// `first`: job runs already taken by the caller (pushed first).  `share`: other threads of run() may
+// push into this pipeline while it drains (detail::Helpers); drain returns once they have detached.
 template <class Provider>
 int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs, const DrainOptions& opt = {},
-          const JobRuns* first = nullptr) {
+          const JobRuns* first = nullptr, bool share = false) {
   FeedPipeline pipe(ctx);
   if (int rc = pipe.init(opt.window_jobs)) return rc;
   if (first)
     if (int rc = pipe.push(*first)) return rc;
-  JobRuns runs;
-  while (take_jobs(tp, std::max<uint64_t>(1, batch_jobs), runs, [](auto&) {})) {
-    if (int rc = pipe.push(runs)) return rc;
-    if (int rc = pipe.tick(opt.flush_seconds, film_host)) return rc;
+  detail::Helpers& hub = detail::Helpers::get();
+  if (share) {
+    std::lock_guard<std::mutex> l(hub.mu);
+    hub.pipes.push_back(&pipe);
+    hub.cv.notify_all();
   }
-  return pipe.finish(film_host);
+  int rc = VPT_OK;
+  JobRuns runs;
+  while (rc == VPT_OK && take_jobs(tp, std::max<uint64_t>(1, batch_jobs), runs, [](auto&) {})) {
+    std::lock_guard<std::mutex> l(pipe.mu());
+    if ((rc = pipe.push(runs)) == VPT_OK) rc = pipe.tick(opt.flush_seconds, film_host);
+  }
+  if (share) {  // no new helper attaches; the attached ones push their last jobs, then detach
+    {
+      std::lock_guard<std::mutex> l(hub.mu);
+      hub.pipes.erase(std::find(hub.pipes.begin(), hub.pipes.end(), &pipe));
+    }
+    std::unique_lock<std::mutex> l(pipe.mu());
+    while (pipe.helpers.load() > 0) {
+      pipe.cv().wait_for(l, std::chrono::milliseconds(5));
+      if (rc == VPT_OK) rc = pipe.tick(opt.flush_seconds, film_host);
+    }
+  }
+  const int frc = pipe.finish(film_host);
+  return rc ? rc : frc;
+}
+
+// A helper thread of run(): takes tokens batch_jobs at a time and pushes their job ids into a driving
+// thread's pipeline, until the provider is exhausted (or no thread drives a GPU).
+template <class Provider>
+int help(Provider& tp, uint64_t batch_jobs) {
+  detail::Helpers& hub = detail::Helpers::get();
+  FeedPipeline* pipe = nullptr;
+  {
+    std::unique_lock<std::mutex> l(hub.mu);
+    hub.cv.wait(l, [&] { return !hub.pipes.empty() || hub.drivers == 0; });
+    if (hub.pipes.empty()) return VPT_OK;
+    pipe = hub.pipes[hub.next++ % hub.pipes.size()];
+    ++pipe->helpers;  // under hub.mu: its driver cannot have stopped accepting helpers
+  }
+  int rc = VPT_OK;
+  JobRuns runs;
+  while (rc == VPT_OK && take_jobs(tp, std::max<uint64_t>(1, batch_jobs), runs, [](auto&) {})) {
+    std::lock_guard<std::mutex> l(pipe->mu());
+    rc = pipe->push(runs);
+  }
+  {
+    std::lock_guard<std::mutex> l(pipe->mu());
+    --pipe->helpers;
+    pipe->cv().notify_all();
+  }
+  return rc;
 }
 
 namespace detail {
@@ -267,6 +340,9 @@ inline int claim_device() {
   for (int d = 0; d < n; ++d)
     if (!D.busy[d]) {
       D.busy[d] = true;
+      // counted as a driver before any thread can find the devices taken (and help, or leave if none drives)
+      std::lock_guard<std::mutex> l(Helpers::get().mu);
+      ++Helpers::get().drivers;
       return d;
     }
   return -2;
@@ -276,10 +352,15 @@ inline void release_device(int d) {
   std::lock_guard<std::mutex> lock(D.mu);
   D.busy[(size_t)d] = false;
 }
-struct DeviceClaim {
+struct DeviceClaim {  // a driving thread counts in Helpers::drivers from its claim to its return
   int device = claim_device();
   ~DeviceClaim() {
-    if (device >= 0) release_device(device);
+    if (device < 0) return;
+    release_device(device);
+    Helpers& h = Helpers::get();
+    std::lock_guard<std::mutex> l(h.mu);
+    --h.drivers;
+    h.cv.notify_all();
   }
 };
 
@@ -329,7 +410,7 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
     std::fprintf(stderr, "vpt_gpu::run: no HIP device (the integrator has no CPU fallback)\n");
     return VPT_E_HIP;
   }
-  if (device < 0) return VPT_OK;  // another worker thread drives each GPU
+  if (device < 0) return help(tp, 4096);  // another worker thread drives each GPU: take tokens for them
 
   const auto size = film.size();
   const int64_t W = (int64_t)size.x(), H = (int64_t)size.y();
@@ -397,7 +478,7 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   float* film_host = reinterpret_cast<float*>(film.data().data());  // H x W x (X, Y, Z, W)
   // the first batch is pushed first; then 4096 tokens per push (a token is one 8x8 job: 64 samples)
   (void)T;
-  return drain(ctx, tp, film_host, 4096, DrainOptions{}, &runs);
+  return drain(ctx, tp, film_host, 4096, DrainOptions{}, &runs, true);
 }
 
 template <class WorkerParameters, class Volume, class Camera, class TileProvider, class Image, class RNG>

@@ -5,7 +5,7 @@
 //
 //   run_gpu_harness config=<scene.json> out=<film.f32> [mode=drain|run w= h= waves= threads= batch=
 //                   grid_n= dist= temperature=0|1 stop_after=<jobs> nvdb=<file.nvdb> gridbuf=<file>
-//                   tempbuf=<file> window= flush_ms= grid_blocks= sample_ms=]
+//                   tempbuf=<file> window= flush_ms= helpers= grid_blocks= sample_ms=]
 //
 // mode=drain (default): each thread owns a context made with vpt_gpu_create and calls
 //   vpt_gpu::drain(ctx, tp, film, batch).  The volume is nvdb= (vpt_grid_read_nvdb: "density", and
@@ -17,7 +17,8 @@
 //   to the RandomNumberGenerator.
 // The camera looks at the volume from (0, 0, -dist) unless dist=0 (then the scene file's camera).
 // stop_after: after that many jobs thread 0 calls tp.stop_at_next_wave() (tile_provider.cpp:107-110).
-// window / flush_ms: vpt_gpu::DrainOptions of mode=drain; grid_blocks: vpt_gpu_set_tuning's grid override.
+// window / flush_ms: vpt_gpu::DrainOptions of mode=drain; helpers: threads that take tokens for the drain
+// threads (vpt_gpu::help, as run()'s threads that find every GPU driven); grid_blocks: vpt_gpu_set_tuning's grid override.
 // sample_ms: a thread samples, every sample_ms, the jobs handed out and the samples in the host film (what
 // main.cpp's 5-FPS window shows: film_to_image(film) and provider.progress(), main.cpp:101-132) and prints
 // them as "sample <ms> <waves handed out> <waves in the film>".  The render time is printed as render_ms.
@@ -193,8 +194,27 @@ int main(int argc, char** argv) {
       const auto r0 = std::chrono::steady_clock::now();
       if (sample_ms > 0) sampler_thread = std::thread(sampler);
       std::vector<std::thread> pool;
-      for (int i = 0; i < threads; ++i) pool.emplace_back([&, i] { rc[i] = vpt_gpu::drain(ctx[i], sp, fh, batch, opt); });
-      for (auto& t : pool) t.join();
+      // helpers=N: N more threads take tokens for the drivers (vpt_gpu::help, as run()'s non-driving threads do)
+      const int helpers = (int)num("helpers", 0);
+      for (int i = 0; i < threads; ++i)
+        pool.emplace_back([&, i] { rc[i] = vpt_gpu::drain(ctx[i], sp, fh, batch, opt, nullptr, helpers > 0); });
+      std::vector<int> hrc(helpers, 0);
+      {
+        // the drivers register their pipelines as they start; helpers wait for one (Helpers::drivers counts
+        // the devices claimed by run(), which drain mode bypasses: count the drivers here instead)
+        std::lock_guard<std::mutex> l(vpt_gpu::detail::Helpers::get().mu);
+        vpt_gpu::detail::Helpers::get().drivers += helpers > 0 ? threads : 0;
+      }
+      for (int i = 0; i < helpers; ++i) pool.emplace_back([&, i] { hrc[i] = vpt_gpu::help(sp, batch); });
+      for (int i = 0; i < threads; ++i) pool[i].join();
+      {
+        std::lock_guard<std::mutex> l(vpt_gpu::detail::Helpers::get().mu);
+        vpt_gpu::detail::Helpers::get().drivers -= helpers > 0 ? threads : 0;
+        vpt_gpu::detail::Helpers::get().cv.notify_all();
+      }
+      for (size_t i = threads; i < pool.size(); ++i) pool[i].join();
+      for (int r : hrc)
+        if (r) return fail("vpt_gpu::help");
       std::printf("run_gpu_harness: render_ms %.1f\n",
                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count());
     }

@@ -67,6 +67,18 @@ def test_run_gpu_threads_share_one_tile_provider(tmp_path, threads, batch):
 
 @pytest.mark.gpu
 @pytest.mark.spawns
+def test_drain_with_helper_threads(tmp_path):
+    """Two helper threads take tokens for the driving thread (vpt_gpu::help, what run()'s threads that find
+    every GPU driven do): every job lands in the driver's feeds exactly once."""
+    w, h, waves = 72, 40, 6
+    film, log = _harness(tmp_path, "wdas_cloud.json", w, h, waves, 1, 5, helpers=2)
+    np.testing.assert_array_equal(film[..., 3], waves)
+    ref = _oracle_film("c3", w, h, waves)
+    np.testing.assert_allclose(film[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.spawns
 def test_run_gpu_fire_scene_batches_over_two_waves(tmp_path):
     """Temperature grid (fire.json) and batches of two waves."""
     w, h, waves = 48, 32, 4

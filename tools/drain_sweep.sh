@@ -22,3 +22,10 @@ run nof flush_ms=100000 "$@"
 run default2 "$@"
 run s50 sample_ms=50 "$@"
 grep "^sample" $O/s50.log | head -40
+# helper threads taking tokens for the driver (run()'s other worker threads), C3 and C4 (the token-bound one)
+run h3 helpers=3 "$@"
+timeout -k 10 120 $H config=volume_path_tracer_amd/scenes/fire.json out=$O/film_c4.f32 w=1920 h=1080 waves=256 grid_n=512 \
+  threads=1 batch=4096 temperature=1 > $O/c4_h0.log 2>&1 && echo "c4 helpers=0 $(grep render_ms $O/c4_h0.log)"
+timeout -k 10 120 $H config=volume_path_tracer_amd/scenes/fire.json out=$O/film_c4.f32 w=1920 h=1080 waves=256 grid_n=512 \
+  threads=1 batch=4096 temperature=1 helpers=3 > $O/c4_h3.log 2>&1 && echo "c4 helpers=3 $(grep render_ms $O/c4_h3.log)"
+rm -f $O/film_c4.f32
