@@ -273,3 +273,20 @@ def test_feed_renders_pushed_jobs_in_any_order():
     counts = np.bincount((jids % T).astype(np.int64), minlength=T).reshape(wl.cfg.height // 8, wl.cfg.width // 8)
     np.testing.assert_array_equal(total[..., 3], np.kron(counts, np.ones((8, 8))))
     np.testing.assert_allclose(total[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_python_run_switches_feeds_every_batch():
+    """render.run (the Python drop-in) with a feed switch after every batch of 7 tokens (flush_seconds 0):
+    many closed / reopened launches on two streams and films, each added into the host film once its
+    launch has ended -- the film equals the oracle's and every sample is counted once."""
+    from volume_path_tracer_amd.render import Integrator, TileProvider, run
+
+    w, h, waves = 40, 24, 3
+    wl = workload("c3", width=w, height=h, spp=waves, grid_n=64)
+    it = Integrator(wl.cfg, SynthGrid(1, 64).grid(), None, device=0)
+    tp = TileProvider(wl.cfg.output_size, waves, wl.cfg.tile_size)
+    film = run(wl.cfg, it, tp, batch_jobs=7, flush_seconds=0.0, window=1024)
+    np.testing.assert_array_equal(film[..., 3], waves)
+    ref = _oracle_film("c3", w, h, waves)
+    np.testing.assert_allclose(film[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)

@@ -32,7 +32,7 @@ def main(argv=None) -> int:
     ap.add_argument("--spp", type=int, default=None, help="override num_waves")
     ap.add_argument("--size", default=None, help="override output_size, WxH")
     ap.add_argument("--device", type=int, default=0)
-    ap.add_argument("--batch-waves", type=int, default=8, help="waves per kernel launch")
+    ap.add_argument("--batch-jobs", type=int, default=4096, help="tokens taken per push into the running launch")
     ap.add_argument("--film-out", default=None, help="also save the raw XYZW film (.npy)")
     ap.add_argument("--event-log", default=None,
                     help="write the Logger event log (log.csv format) of the first --event-jobs jobs")
@@ -68,7 +68,7 @@ def main(argv=None) -> int:
         tp = TileProvider(cfg.output_size, cfg.num_waves, cfg.tile_size)
         tp.reset_eta()
         t0 = time.perf_counter()
-        film = run(cfg, it, tp, batch_waves=args.batch_waves)
+        film = run(cfg, it, tp, batch_jobs=args.batch_jobs)
         ms = (time.perf_counter() - t0) * 1e3
         print(f"[vpt] Rendering complete in {ms:.0f} ms ({cfg.width}x{cfg.height}, {cfg.num_waves} spp)",
               file=sys.stderr)

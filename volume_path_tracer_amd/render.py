@@ -290,20 +290,78 @@ class Integrator:
         return self.film.cpu().numpy()
 
 
+class Feed:
+    """A running launch that renders job ids as they are pushed (vpt_gpu_feed_*, include/vpt_gpu.h) into
+    `film` (a device tensor of the context's film shape) on `stream` (a torch stream of the device)."""
+
+    def __init__(self, integrator: "Integrator", film, stream, window: int = 1 << 19):
+        self.it, self.film, self.stream = integrator, film, stream
+        h = C.c_void_p()
+        capi.check(capi.lib().vpt_gpu_feed_open(integrator.h, C.c_void_p(film.data_ptr()),
+                                                C.c_void_p(int(stream.cuda_stream)), int(window), C.byref(h)),
+                   "vpt_gpu_feed_open")
+        self.h = h
+
+    def push(self, jids) -> None:
+        j = np.ascontiguousarray(jids, np.uint64)
+        capi.check(capi.lib().vpt_gpu_feed_push(self.h, j.ctypes.data_as(C.POINTER(C.c_uint64)), j.size),
+                   "vpt_gpu_feed_push")
+
+    def close(self) -> None:
+        capi.check(capi.lib().vpt_gpu_feed_close(self.h), "vpt_gpu_feed_close")
+
+    def done(self) -> bool:
+        d = C.c_int()
+        capi.check(capi.lib().vpt_gpu_feed_query(self.h, C.byref(d), None), "vpt_gpu_feed_query")
+        return bool(d.value)
+
+    def destroy(self) -> None:
+        if self.h:
+            h, self.h = self.h, None
+            capi.check(capi.lib().vpt_gpu_feed_destroy(h), "vpt_gpu_feed_destroy")
+
+
 def run(cfg: capi.Configuration, integrator: Integrator, tp: TileProvider, film: Optional[np.ndarray] = None,
-        batch_waves: int = 8) -> np.ndarray:
-    """Drop-in for vpt::run (worker.cpp:92-208): drain `tp` on the GPU and add into `film`
-    (host float32 [H][W][4], the reference's Image<float,4> layout)."""
-    batch = max(1, batch_waves) * tp.num_tiles
-    while True:
-        begin, count = tp.next_batch(batch)
-        if count == 0:
-            break
-        integrator.render_jobs(begin, count)
-    out = integrator.film_host()
-    if film is not None:
-        film += out
-        return film
+        batch_jobs: int = 4096, flush_seconds: float = 0.2, window: int = 1 << 19) -> np.ndarray:
+    """Drop-in for vpt::run (worker.cpp:92-208): drain `tp` on the GPU into `film` (host float32 [H][W][4],
+    the reference's Image<float,4> layout), as include/vpt_run.hpp's drain does: job ids go to a running
+    launch through a feed (bounded window, no launch drain between batches), and every flush_seconds the
+    feed is closed and the next opened on the other stream and device film, the finished one being added
+    into `film` -- which therefore fills in during the run (main.cpp:101-132 shows it at 5 FPS)."""
+    torch = integrator.torch
+    out = film if film is not None else np.zeros((integrator.cfg.height, integrator.cfg.width, 4), np.float32)
+    films = [torch.zeros_like(integrator.film) for _ in range(2)]
+    streams = [torch.cuda.Stream(device=integrator.dev) for _ in range(2)]
+    feeds = [Feed(integrator, films[0], streams[0], window), None]
+    cur, last = 0, time.monotonic()
+
+    def flush(i):
+        feeds[i].destroy()
+        feeds[i] = None
+        torch.cuda.synchronize(integrator.dev)
+        out[...] += films[i].cpu().numpy()
+        films[i].zero_()
+
+    try:
+        while True:
+            begin, count = tp.next_batch(batch_jobs)
+            if count == 0:
+                break
+            feeds[cur].push(np.arange(begin, begin + count, dtype=np.uint64))
+            old = cur ^ 1
+            if feeds[old] is not None and feeds[old].done():
+                flush(old)
+            if feeds[old] is None and time.monotonic() - last >= flush_seconds:
+                feeds[cur].close()
+                cur, last = old, time.monotonic()
+                feeds[cur] = Feed(integrator, films[cur], streams[cur], window)
+        for i in (cur ^ 1, cur):
+            if feeds[i] is not None:
+                flush(i)
+    finally:
+        for f in feeds:
+            if f is not None:
+                f.destroy()
     return out
 
 
