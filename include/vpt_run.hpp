@@ -112,7 +112,6 @@ inline std::mutex& film_mutex() {  // the host film is shared by every caller
 class FeedPipeline {
  public:
   std::mutex& mu() { return mu_; }
-  std::condition_variable& cv() { return cv_; }
   std::atomic<int> helpers{0};  // helper threads attached (see detail::Helpers)
   explicit FeedPipeline(vpt_gpu_ctx* ctx) : ctx_(ctx) {}
   ~FeedPipeline() {
@@ -179,7 +178,6 @@ class FeedPipeline {
   std::vector<uint64_t> ids_;
   std::chrono::steady_clock::time_point last_switch_;
   std::mutex mu_;
-  std::condition_variable cv_;
 };
 
 namespace detail {
@@ -227,9 +225,9 @@ int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs,
       std::lock_guard<std::mutex> l(hub.mu);
       hub.pipes.erase(std::find(hub.pipes.begin(), hub.pipes.end(), &pipe));
     }
-    std::unique_lock<std::mutex> l(pipe.mu());
     while (pipe.helpers.load() > 0) {
-      pipe.cv().wait_for(l, std::chrono::milliseconds(5));
+      std::this_thread::sleep_for(std::chrono::milliseconds(2));
+      std::lock_guard<std::mutex> l(pipe.mu());
       if (rc == VPT_OK) rc = pipe.tick(opt.flush_seconds, film_host);
     }
   }
@@ -256,11 +254,7 @@ int help(Provider& tp, uint64_t batch_jobs) {
     std::lock_guard<std::mutex> l(pipe->mu());
     rc = pipe->push(runs);
   }
-  {
-    std::lock_guard<std::mutex> l(pipe->mu());
-    --pipe->helpers;
-    pipe->cv().notify_all();
-  }
+  --pipe->helpers;  // the last touch: its driver may finish and destroy the pipeline from here on
   return rc;
 }
 

@@ -1,0 +1,170 @@
+// dropin_mock.cpp -- TEST HARNESS (CPU only): include/vpt_run.hpp's drain / help threads over a mock of the
+// C ABI's stream, film and feed calls, so the host-side protocol -- tokens taken by drivers and helpers,
+// pushes under the pipeline's lock, feed switches, the progressive film, helpers detaching before the
+// driver's final flush -- is checked without a GPU: every job id the provider hands out must be "rendered"
+// (pushed into some open feed) exactly once, and the host film must count every sample once.
+//
+//   dropin_mock drivers=<n> helpers=<n> w= h= waves= batch= flush_ms= window= stop_after=
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "tile_provider_headless.hpp"
+#include "vpt_run.hpp"
+
+namespace {
+int64_t g_w = 0, g_h = 0, g_tw = 8, g_th = 8, g_ntx = 0;
+std::mutex g_mu;
+std::vector<uint32_t> g_rendered;  // per jid: times pushed into an open feed
+std::atomic<int> g_open_feeds{0}, g_max_open{0};
+}  // namespace
+
+struct vpt_gpu_ctx {
+  std::vector<float> own;
+};
+struct vpt_gpu_feed {
+  vpt_gpu_ctx* ctx;
+  float* film;
+  bool closed = false;
+};
+
+extern "C" {
+const char* vpt_last_error(void) { return "mock"; }
+int vpt_gpu_stream_create(vpt_gpu_ctx*, void** s) {
+  *s = new int(0);
+  return VPT_OK;
+}
+int vpt_gpu_stream_destroy(vpt_gpu_ctx*, void* s) {
+  delete static_cast<int*>(s);
+  return VPT_OK;
+}
+int vpt_gpu_stream_sync(vpt_gpu_ctx*, void*) { return VPT_OK; }
+int vpt_gpu_film_alloc(vpt_gpu_ctx*, float** f) {
+  *f = new float[(size_t)(g_w * g_h * 4)]();
+  return VPT_OK;
+}
+int vpt_gpu_film_free(vpt_gpu_ctx*, float* f) {
+  delete[] f;
+  return VPT_OK;
+}
+int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* c, float* f, float* host) {
+  float* src = f ? f : c->own.data();
+  for (int64_t i = 0; i < g_w * g_h * 4; ++i) {
+    host[i] += src[i];
+    src[i] = 0.0f;
+  }
+  return VPT_OK;
+}
+int vpt_gpu_feed_open(vpt_gpu_ctx* c, float* film, void* stream, uint64_t, vpt_gpu_feed** out) {
+  if (!stream) return VPT_E_INVALID;
+  *out = new vpt_gpu_feed{c, film ? film : c->own.data()};
+  const int n = ++g_open_feeds;
+  int m = g_max_open.load();
+  while (n > m && !g_max_open.compare_exchange_weak(m, n)) {
+  }
+  return VPT_OK;
+}
+int vpt_gpu_feed_push(vpt_gpu_feed* f, const uint64_t* jids, uint64_t n) {
+  if (f->closed) return VPT_E_STATE;
+  const int64_t T = (int64_t)g_rendered.size() ? g_ntx * ((g_h + g_th - 1) / g_th) : 1;
+  for (uint64_t i = 0; i < n; ++i) {
+    {
+      std::lock_guard<std::mutex> l(g_mu);
+      if (jids[i] >= g_rendered.size()) return VPT_E_INVALID;
+      ++g_rendered[jids[i]];
+    }
+    const int64_t tile = (int64_t)(jids[i] % (uint64_t)T), x0 = (tile % g_ntx) * g_tw, y0 = (tile / g_ntx) * g_th;
+    for (int64_t y = y0; y < std::min(g_h, y0 + g_th); ++y)
+      for (int64_t x = x0; x < std::min(g_w, x0 + g_tw); ++x) f->film[(y * g_w + x) * 4 + 3] += 1.0f;  // the count
+  }
+  if (n % 3 == 0) std::this_thread::yield();  // let other threads interleave
+  return VPT_OK;
+}
+int vpt_gpu_feed_close(vpt_gpu_feed* f) {
+  f->closed = true;
+  return VPT_OK;
+}
+int vpt_gpu_feed_query(vpt_gpu_feed* f, int* done, uint64_t*) {
+  *done = f->closed ? 1 : 0;
+  return VPT_OK;
+}
+int vpt_gpu_feed_destroy(vpt_gpu_feed* f) {
+  --g_open_feeds;
+  delete f;
+  return VPT_OK;
+}
+}
+
+int main(int argc, char** argv) {
+  std::map<std::string, long long> a{{"drivers", 1}, {"helpers", 0}, {"w", 72}, {"h", 40}, {"waves", 5},
+                                     {"batch", 7}, {"flush_ms", 0}, {"window", 1024}, {"stop_after", 0}};
+  for (int i = 1; i < argc; ++i) {
+    const char* eq = std::strchr(argv[i], '=');
+    if (eq) a[std::string(argv[i], eq - argv[i])] = std::atoll(eq + 1);
+  }
+  g_w = a["w"];
+  g_h = a["h"];
+  g_ntx = (g_w + g_tw - 1) / g_tw;
+  vpt_headless::TileProvider tp(g_w, g_h, (unsigned)a["waves"], g_tw, g_th);
+  const uint64_t T = tp.num_tiles(), total = T * (uint64_t)a["waves"];
+  g_rendered.assign(total + 8 * T, 0);  // room for jids past a stop
+  std::atomic<uint64_t> handed{0};
+  struct Stopping {
+    vpt_headless::TileProvider& tp;
+    std::atomic<uint64_t>& handed;
+    uint64_t stop_after;
+    vpt_headless::TileProvider::token next() {
+      if (handed.fetch_add(1) + 1 == stop_after) tp.stop_at_next_wave();
+      return tp.next();
+    }
+  } sp{tp, handed, (uint64_t)a["stop_after"]};
+  std::vector<float> film((size_t)(g_w * g_h * 4), 0.0f);
+  const int drivers = (int)a["drivers"], helpers = (int)a["helpers"];
+  std::vector<vpt_gpu_ctx> ctx(drivers);
+  for (auto& c : ctx) c.own.assign(film.size(), 0.0f);
+  vpt_gpu::DrainOptions opt;
+  opt.flush_seconds = (double)a["flush_ms"] / 1000.0;
+  opt.window_jobs = (uint64_t)a["window"];
+  {
+    std::lock_guard<std::mutex> l(vpt_gpu::detail::Helpers::get().mu);
+    vpt_gpu::detail::Helpers::get().drivers += drivers;  // (run() counts them when they claim a device)
+  }
+  std::vector<int> rc(drivers + helpers, 0);
+  std::vector<std::thread> pool;
+  for (int i = 0; i < drivers; ++i)
+    pool.emplace_back([&, i] { rc[i] = vpt_gpu::drain(&ctx[i], sp, film.data(), (uint64_t)a["batch"], opt, nullptr, true); });
+  for (int i = 0; i < helpers; ++i) pool.emplace_back([&, i] { rc[drivers + i] = vpt_gpu::help(sp, (uint64_t)a["batch"]); });
+  for (int i = 0; i < drivers; ++i) pool[i].join();
+  {
+    std::lock_guard<std::mutex> l(vpt_gpu::detail::Helpers::get().mu);
+    vpt_gpu::detail::Helpers::get().drivers -= drivers;
+    vpt_gpu::detail::Helpers::get().cv.notify_all();
+  }
+  for (size_t i = drivers; i < pool.size(); ++i) pool[i].join();
+  for (int r : rc)
+    if (r) {
+      std::printf("dropin_mock: a thread returned %d\n", r);
+      return 1;
+    }
+  // every job of the waves that ran rendered exactly once; none beyond them
+  const uint64_t waves = tp.max_wave_started(), ran = T * waves;
+  for (uint64_t j = 0; j < g_rendered.size(); ++j)
+    if (g_rendered[j] != (j < ran ? 1u : 0u)) {
+      std::printf("dropin_mock: jid %llu rendered %u times\n", (unsigned long long)j, g_rendered[j]);
+      return 1;
+    }
+  for (size_t p = 3; p < film.size(); p += 4)
+    if (film[p] != (float)waves) {
+      std::printf("dropin_mock: pixel %zu counts %g samples, want %llu\n", p / 4, film[p], (unsigned long long)waves);
+      return 1;
+    }
+  std::printf("dropin_mock: ok %llu waves, %llu jobs, max %d feeds open\n", (unsigned long long)waves,
+              (unsigned long long)ran, g_max_open.load());
+  return 0;
+}

@@ -1,0 +1,30 @@
+"""The drop-in's host protocol (include/vpt_run.hpp: drain's feeds and film switches, run()'s helper threads)
+over a mock of the C ABI's stream / film / feed calls, built with ThreadSanitizer (tests/native/dropin_mock.cpp;
+no GPU): with 1-3 driving threads, 0-7 helpers, batches of 1-7 tokens, film switches every batch and
+stop_at_next_wave() mid-run, every job id the TileProvider hands out is pushed into an open feed exactly
+once, the host film counts every sample once, and TSan reports no race."""
+import os
+import subprocess
+from pathlib import Path
+
+import pytest
+
+MOCK = Path(__file__).resolve().parent / "native" / "build" / "dropin_mock"
+
+CASES = [
+    "drivers=1 helpers=0",
+    "drivers=1 helpers=3",
+    "drivers=2 helpers=5 batch=3",
+    "drivers=3 helpers=2 flush_ms=1 batch=1",
+    "drivers=1 helpers=4 stop_after=50 batch=2",
+    "drivers=2 helpers=7 batch=1 w=200 h=120 waves=4",
+]
+
+
+@pytest.mark.parametrize("args", CASES)
+def test_dropin_protocol_renders_every_token_once(args):
+    assert MOCK.exists(), "build with __graft_entry__.build() (tests/native/Makefile)"
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66")
+    for _ in range(3):
+        r = subprocess.run([str(MOCK), *args.split()], capture_output=True, text=True, timeout=120, env=env)
+        assert r.returncode == 0 and "dropin_mock: ok" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
