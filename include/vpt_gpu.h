@@ -350,7 +350,10 @@ int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* ctx, float* film_device, float* film
  * VPT_E_STATE if lanes gave up waiting for jobs (a lane waits at most 30 s, so a launch always ends: a
  * feed left open without pushes that long ends by itself).  A feed's launch holds the device's CUs until it
  * is closed -- a second feed opened meanwhile starts as the first one's lanes leave -- so push to a feed
- * only after the feeds opened before it have been closed.  Feeds use a host-pinned ring (8 bytes per
+ * only after the feeds opened before it have been closed; and a call that waits for the whole device
+ * (hipDeviceSynchronize, and hipFree / hipHostMalloc / hipHostFree may) waits for an open feed's lanes to
+ * give up: wait for streams instead.  A destroyed feed's memory is kept by the context for the next
+ * vpt_gpu_feed_open (freed by vpt_gpu_destroy).  Feeds use a host-pinned ring (8 bytes per
  * window slot) and run the reference RNG mode. */
 typedef struct vpt_gpu_feed vpt_gpu_feed;
 int vpt_gpu_feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t window, vpt_gpu_feed** out);

@@ -263,7 +263,7 @@ struct KernelEnvT {
     }
     if (w & kFeedClosed) return 0;
     if (now - (uint32_t)lc.x0 > kFeedDeadline) {
-      atomicOr(feed_error, 1u);
+      __hip_atomic_store(feed_error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // (host memory: a store)
       return 0;
     }
     return -1;
@@ -615,6 +615,8 @@ struct FeedLaunch {
 };
 }  // namespace vpt
 
+struct vpt_gpu_feed;
+
 struct vpt_gpu_ctx {
   int device = 0;
   vpt_configuration cfg{};
@@ -654,6 +656,11 @@ struct vpt_gpu_ctx {
   uint64_t perm_n = 0;
   std::vector<uint32_t> tile_rank;
   float* staging = nullptr;        // pinned host buffer of film_count floats (vpt_gpu_film_flush_to_host)
+  // Feeds whose launches have ended, kept for reuse: while a feed is open its launch holds the device,
+  // and a call that waits for the whole device (hipFree, hipHostFree, hipHostMalloc may) would wait for
+  // that launch -- i.e. until its lanes give up -- so a feed's memory is allocated once and freed with
+  // the context.
+  std::vector<vpt_gpu_feed*> feed_pool;
 #ifdef VPT_EXP_COMPACT
   uint4* xbuf = nullptr;           // the compaction experiment's exchange buffer (grid_blocks blocks)
 #endif
@@ -734,8 +741,11 @@ int ctx_device(vpt_gpu_ctx* ctx) {
   return VPT_OK;
 }
 
+void feed_pool_free(vpt_gpu_ctx* ctx);
+
 void destroy(vpt_gpu_ctx* ctx) {
   if (!ctx) return;
+  feed_pool_free(ctx);
   (void)hipSetDevice(ctx->device);
   vpt::free_grid(ctx->density);
   vpt::free_grid(ctx->temperature);
@@ -1263,7 +1273,7 @@ int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* ctx, float* film_device, float* film
   if (rc) return rc;
   float* f = film_device ? film_device : ctx->film;
   const size_t bytes = ctx->film_count * sizeof(float);
-  if (!ctx->staging) VPT_HIP(hipHostMalloc((void**)&ctx->staging, bytes, hipHostMallocDefault));
+  if (!ctx->staging) VPT_HIP(hipHostMalloc((void**)&ctx->staging, bytes, hipHostMallocDefault));  // (feeds allocate it first)
   VPT_HIP(hipMemcpyAsync(ctx->staging, f, bytes, hipMemcpyDeviceToHost, ctx->stream));
   VPT_HIP(hipMemsetAsync(f, 0, bytes, ctx->stream));
   VPT_HIP(hipStreamSynchronize(ctx->stream));
@@ -1281,13 +1291,13 @@ struct vpt_gpu_feed {
   vpt_gpu_ctx* ctx = nullptr;
   hipStream_t stream = nullptr;
   float* film = nullptr;
-  uint64_t* block = nullptr;  // hipHostMalloc'd: [8] word + padding, [cap] ring, then uint32 counts[T]
+  uint64_t* block = nullptr;  // hipHostMalloc'd: [8] word, error word, padding; [cap] ring; uint32 counts[T]
   uint64_t* word = nullptr;
+  uint32_t* error = nullptr;  // block[1]: a lane that gave up waiting stores 1 here
   uint64_t* ring = nullptr;
   uint32_t* counts = nullptr;
   uint64_t cap = 0;
   uint64_t published = 0;
-  unsigned* error = nullptr;  // device
   hipEvent_t closed_ev = nullptr;
   bool closed = false;
 };
@@ -1299,9 +1309,13 @@ void feed_free(vpt_gpu_feed* f) {
   if (!f) return;
   (void)hipSetDevice(f->ctx->device);
   if (f->closed_ev) (void)hipEventDestroy(f->closed_ev);
-  (void)hipFree(f->error);
   (void)hipHostFree(f->block);
   delete f;
+}
+
+void feed_pool_free(vpt_gpu_ctx* ctx) {
+  for (vpt_gpu_feed* f : ctx->feed_pool) feed_free(f);
+  ctx->feed_pool.clear();
 }
 
 // Publishes items [0, published) and, with close, the end of the feed (release: the ring and count
@@ -1321,26 +1335,39 @@ int vpt_gpu_feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, ui
   if (rc) return rc;
   uint64_t cap = 1024;
   while (cap < window && cap < (1ULL << 26)) cap <<= 1;
-  std::unique_ptr<vpt_gpu_feed, void (*)(vpt_gpu_feed*)> f(new vpt_gpu_feed(), feed_free);
-  f->ctx = ctx;
+  // the context's film staging, before any feed holds the device (vpt_gpu_film_flush_to_host)
+  if (!ctx->staging) VPT_HIP(hipHostMalloc((void**)&ctx->staging, ctx->film_count * sizeof(float), hipHostMallocDefault));
+  std::unique_ptr<vpt_gpu_feed, void (*)(vpt_gpu_feed*)> f(nullptr, feed_free);
+  for (size_t i = 0; i < ctx->feed_pool.size(); ++i)
+    if (ctx->feed_pool[i]->cap == cap) {  // a pooled feed of this window
+      f.reset(ctx->feed_pool[i]);
+      ctx->feed_pool.erase(ctx->feed_pool.begin() + (ptrdiff_t)i);
+      break;
+    }
+  if (!f) {
+    f.reset(new vpt_gpu_feed());
+    f->ctx = ctx;
+    f->cap = cap;
+    const size_t bytes = (8 + cap) * sizeof(uint64_t) + ctx->scene.T * sizeof(uint32_t);
+    VPT_HIP(hipHostMalloc((void**)&f->block, bytes, hipHostMallocCoherent | hipHostMallocMapped));
+    f->word = f->block;
+    f->error = reinterpret_cast<uint32_t*>(f->block + 1);
+    f->ring = f->block + 8;  // its own cache lines, away from the word the waiting wavefronts poll
+    f->counts = reinterpret_cast<uint32_t*>(f->ring + cap);
+    VPT_HIP(hipEventCreateWithFlags(&f->closed_ev, hipEventDisableTiming));
+  }
   f->stream = (hipStream_t)hip_stream;
   f->film = film_device ? film_device : ctx->film;
-  f->cap = cap;
-  const size_t bytes = (8 + cap) * sizeof(uint64_t) + ctx->scene.T * sizeof(uint32_t);
-  VPT_HIP(hipHostMalloc((void**)&f->block, bytes, hipHostMallocCoherent | hipHostMallocMapped));
-  f->word = f->block;
-  f->ring = f->block + 8;  // its own cache lines, away from the word the waiting wavefronts poll
-  f->counts = reinterpret_cast<uint32_t*>(f->ring + cap);
+  f->published = 0;
+  f->closed = false;
   for (uint64_t i = 0; i < cap; ++i) f->ring[i] = vpt::kFeedEmpty;
   std::memset(f->counts, 0, ctx->scene.T * sizeof(uint32_t));
+  __atomic_store_n(f->error, 0u, __ATOMIC_RELAXED);
   __atomic_store_n(f->word, 0ULL, __ATOMIC_RELEASE);
-  VPT_HIP(hipMalloc((void**)&f->error, sizeof(unsigned)));
-  VPT_HIP(hipMemsetAsync(f->error, 0, sizeof(unsigned), f->stream));
-  VPT_HIP(hipEventCreateWithFlags(&f->closed_ev, hipEventDisableTiming));
   uint64_t *word_dev = nullptr, *ring_dev = nullptr;
   VPT_HIP(hipHostGetDevicePointer((void**)&word_dev, f->word, 0));
   ring_dev = word_dev + 8;
-  const vpt::FeedLaunch fl{word_dev, ring_dev, cap - 1, f->error};
+  const vpt::FeedLaunch fl{word_dev, ring_dev, cap - 1, reinterpret_cast<unsigned*>(word_dev + 1)};
   if ((rc = render(ctx, 0, ~0ULL >> 1, f->film, nullptr, hip_stream, nullptr, 0, nullptr, &fl))) return rc;
   *out = f.release();
   return VPT_OK;
@@ -1417,10 +1444,9 @@ int vpt_gpu_feed_destroy(vpt_gpu_feed* f) {
     else
       complete = true;
   }
-  unsigned err = 0;
-  if (complete && hipMemcpy(&err, f->error, sizeof err, hipMemcpyDeviceToHost) == hipSuccess && err)
+  if (complete && __atomic_load_n(f->error, __ATOMIC_ACQUIRE))
     rc = vpt::set_error(VPT_E_STATE, "vpt_gpu_feed_destroy: lanes of the feed's launch gave up waiting for jobs");
-  if (complete) feed_free(f);  // (after a HIP failure the launch may still read the block: leak it)
+  if (complete) f->ctx->feed_pool.push_back(f);  // (after a HIP failure the launch may still read the block: leak it)
   return rc;
 }
 

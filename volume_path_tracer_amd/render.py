@@ -336,11 +336,15 @@ def run(cfg: capi.Configuration, integrator: Integrator, tp: TileProvider, film:
     cur, last = 0, time.monotonic()
 
     def flush(i):
+        # only this feed's stream: the other feed's launch holds the device until it is closed, so a
+        # device-wide synchronize would wait for its lanes to give up
         feeds[i].destroy()
         feeds[i] = None
-        torch.cuda.synchronize(integrator.dev)
-        out[...] += films[i].cpu().numpy()
-        films[i].zero_()
+        with torch.cuda.stream(streams[i]):
+            host = films[i].to("cpu", non_blocking=False)
+            films[i].zero_()
+        streams[i].synchronize()
+        out[...] += host.numpy()
 
     try:
         while True:
