@@ -352,7 +352,8 @@ int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* ctx, float* film_device, float* film
  * is closed -- a second feed opened meanwhile starts as the first one's lanes leave -- so push to a feed
  * only after the feeds opened before it have been closed; and a call that waits for the whole device
  * (hipDeviceSynchronize, and hipFree / hipHostMalloc / hipHostFree may) waits for an open feed's lanes to
- * give up: wait for streams instead.  A destroyed feed's memory is kept by the context for the next
+ * give up: wait for streams instead.  The launch leaves two blocks' slots free, so small kernels and copies
+ * on other streams (vpt_gpu_film_flush_to_host's copy and clear) still run beside it.  A destroyed feed's memory is kept by the context for the next
  * vpt_gpu_feed_open (freed by vpt_gpu_destroy).  Feeds use a host-pinned ring (8 bytes per
  * window slot) and run the reference RNG mode. */
 typedef struct vpt_gpu_feed vpt_gpu_feed;

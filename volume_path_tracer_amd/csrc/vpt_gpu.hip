@@ -801,6 +801,8 @@ int ensure_order(vpt_gpu_ctx* ctx) {
   return rank_tiles(ctx);
 }
 
+constexpr uint32_t kFeedSpareBlocks = 2;  // (1 792 resident blocks on 256 CUs: 0.1 % of the grid)
+
 int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film, float* records, void* stream_ptr,
            vpt_event* events = nullptr, uint64_t event_cap = 0, uint32_t* slot_out = nullptr,
            const vpt::FeedLaunch* feed = nullptr) {
@@ -883,6 +885,11 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   const bool use_lat = !dbg && !feed && ctx->lat_mode != 0 &&
                        (ctx->lat_mode == 1 || (!ctx->grid_user && (latency || blocks <= lat_blocks)));
   if (use_lat) blocks = (uint32_t)std::min<uint64_t>(latency ? lat_blocks : blocks, lat_blocks);
+  // A feed's launch holds its slots until it is closed, and the previous feed's film is copied out and
+  // cleared (copy / fill kernels on another stream) while it runs: kFeedSpareBlocks block slots stay free
+  // for them, or they would wait for the open launch, whose lanes wait for the host (r04e: the Python
+  // drop-in's film flush stalled until the lanes' 30 s deadline).
+  if (feed && blocks > 2 * kFeedSpareBlocks) blocks -= kFeedSpareBlocks;
   const uint64_t T = ctx->scene.T;
   if (!feed && ctx->order_mode != VPT_ORDER_JID && jid_begin % T == 0 && jid_count % T == 0 && jid_count < (1ULL << 32)) {
     // whole waves: take the jobs in cost order (same jobs, same samples)

@@ -330,21 +330,22 @@ def run(cfg: capi.Configuration, integrator: Integrator, tp: TileProvider, film:
     into `film` -- which therefore fills in during the run (main.cpp:101-132 shows it at 5 FPS)."""
     torch = integrator.torch
     out = film if film is not None else np.zeros((integrator.cfg.height, integrator.cfg.width, 4), np.float32)
+    if out.dtype != np.float32 or not out.flags.c_contiguous or out.size != integrator.film.numel():
+        raise ValueError("run: film must be a C-contiguous float32 [H][W][4] array")
     films = [torch.zeros_like(integrator.film) for _ in range(2)]
     streams = [torch.cuda.Stream(device=integrator.dev) for _ in range(2)]
     feeds = [Feed(integrator, films[0], streams[0], window), None]
     cur, last = 0, time.monotonic()
 
     def flush(i):
-        # only this feed's stream: the other feed's launch holds the device until it is closed, so a
-        # device-wide synchronize would wait for its lanes to give up
+        # no device-wide synchronize: the other feed's launch holds the device until it is closed, so it
+        # would wait for that launch's lanes to give up; vpt_gpu_film_flush_to_host (as vpt_run.hpp's drain)
+        # copies through the context's pinned staging and waits for its own stream only
         feeds[i].destroy()
         feeds[i] = None
-        with torch.cuda.stream(streams[i]):
-            host = films[i].to("cpu", non_blocking=False)
-            films[i].zero_()
-        streams[i].synchronize()
-        out[...] += host.numpy()
+        capi.check(capi.lib().vpt_gpu_film_flush_to_host(integrator.h, C.c_void_p(films[i].data_ptr()),
+                                                          out.ctypes.data_as(C.POINTER(C.c_float))),
+                   "vpt_gpu_film_flush_to_host")
 
     try:
         while True:
