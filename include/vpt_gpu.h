@@ -362,6 +362,14 @@ int vpt_gpu_feed_push(vpt_gpu_feed* feed, const uint64_t* jids, uint64_t n);
 int vpt_gpu_feed_close(vpt_gpu_feed* feed);
 int vpt_gpu_feed_query(vpt_gpu_feed* feed, int* done, uint64_t* pushed);
 int vpt_gpu_feed_destroy(vpt_gpu_feed* feed);
+/* A staged feed: its close also queues, on the feed's stream behind the launch, the copy of its film into
+ * a pinned host buffer of the feed and the film's clearing -- so retiring it needs no GPU work queued later
+ * (work queued while another feed is open may wait behind that feed's launch: streams can share a
+ * hardware queue).  vpt_gpu_feed_collect closes if needed, waits, adds the staged film into film_host
+ * (film_count floats; the caller serialises writers of film_host) and frees the feed like destroy. */
+int vpt_gpu_feed_open_staged(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t window,
+                             vpt_gpu_feed** out);
+int vpt_gpu_feed_collect(vpt_gpu_feed* feed, float* film_host);
 
 /* Zero the context's own film. */
 int vpt_gpu_film_clear(vpt_gpu_ctx* ctx);

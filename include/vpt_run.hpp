@@ -73,8 +73,9 @@ namespace vpt_gpu {
 //     the window plus the jobs in flight -- as the reference's workers each hold the token they render;
 //   * the film is progressive (main.cpp:101-132 shows it at 5 FPS): every flush_seconds the running feed
 //     is closed and a new one opened on the other stream and film (its lanes start as the old launch's
-//     drain frees the CUs); once the old launch has ended, its film is added into film_host (under a
-//     mutex shared by all callers) and zeroed.  film_host's sample counts thus rise during the run, by
+//     drain frees the CUs); the old feed's close queues its film's copy to pinned memory and clearing
+//     behind its launch, and once those have run the film is added into film_host (under a mutex shared
+//     by all callers).  film_host's sample counts thus rise during the run, by
 //     whole jobs, and the final film is the same sum.
 using JobRuns = std::vector<std::pair<uint64_t, uint64_t>>;  // contiguous (jid_begin, count) runs
 
@@ -127,7 +128,7 @@ class FeedPipeline {
       if (int rc = vpt_gpu_stream_create(ctx_, &s)) return rc;
     if (int rc = vpt_gpu_film_alloc(ctx_, &films_[1])) return rc;
     last_switch_ = std::chrono::steady_clock::now();
-    return vpt_gpu_feed_open(ctx_, films_[0], streams_[0], window_, &feeds_[0]);
+    return vpt_gpu_feed_open_staged(ctx_, films_[0], streams_[0], window_, &feeds_[0]);
   }
   int push(const JobRuns& runs) {
     ids_.clear();
@@ -150,7 +151,7 @@ class FeedPipeline {
       if (int rc = vpt_gpu_feed_close(feeds_[cur_])) return rc;
       cur_ = old;
       last_switch_ = now;
-      return vpt_gpu_feed_open(ctx_, films_[cur_], streams_[cur_], window_, &feeds_[cur_]);
+      return vpt_gpu_feed_open_staged(ctx_, films_[cur_], streams_[cur_], window_, &feeds_[cur_]);
     }
     return VPT_OK;
   }
@@ -162,12 +163,13 @@ class FeedPipeline {
   }
 
  private:
+  // The feed's close queued its film's copy-out and clearing (a staged feed: nothing is queued on the GPU
+  // while the other feed's launch runs); collect waits for them and adds the film into film_host.
   int flush(int i, float* film_host) {
-    const int rc = vpt_gpu_feed_destroy(feeds_[i]);  // waits for the feed's launch and its sample counts
-    feeds_[i] = nullptr;
-    if (rc) return rc;
     std::lock_guard<std::mutex> lock(film_mutex());
-    return vpt_gpu_film_flush_to_host(ctx_, films_[i], film_host);
+    const int rc = vpt_gpu_feed_collect(feeds_[i], film_host);
+    feeds_[i] = nullptr;
+    return rc;
   }
   vpt_gpu_ctx* ctx_;
   uint64_t window_ = 0;

@@ -5,6 +5,7 @@
 // (pushed into some open feed) exactly once, and the host film must count every sample once.
 //
 //   dropin_mock drivers=<n> helpers=<n> w= h= waves= batch= flush_ms= window= stop_after=
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -32,6 +33,8 @@ struct vpt_gpu_feed {
   vpt_gpu_ctx* ctx;
   float* film;
   bool closed = false;
+  bool staged = false;
+  std::vector<float> copy;  // a staged feed's film, copied out at close
 };
 
 extern "C" {
@@ -63,7 +66,9 @@ int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* c, float* f, float* host) {
 }
 int vpt_gpu_feed_open(vpt_gpu_ctx* c, float* film, void* stream, uint64_t, vpt_gpu_feed** out) {
   if (!stream) return VPT_E_INVALID;
-  *out = new vpt_gpu_feed{c, film ? film : c->own.data()};
+  *out = new vpt_gpu_feed();
+  (*out)->ctx = c;
+  (*out)->film = film ? film : c->own.data();
   const int n = ++g_open_feeds;
   int m = g_max_open.load();
   while (n > m && !g_max_open.compare_exchange_weak(m, n)) {
@@ -86,8 +91,18 @@ int vpt_gpu_feed_push(vpt_gpu_feed* f, const uint64_t* jids, uint64_t n) {
   if (n % 3 == 0) std::this_thread::yield();  // let other threads interleave
   return VPT_OK;
 }
+int vpt_gpu_feed_open_staged(vpt_gpu_ctx* c, float* film, void* stream, uint64_t w, vpt_gpu_feed** out) {
+  const int rc = vpt_gpu_feed_open(c, film, stream, w, out);
+  if (rc == VPT_OK) (*out)->staged = true;
+  return rc;
+}
 int vpt_gpu_feed_close(vpt_gpu_feed* f) {
+  if (f->closed) return VPT_OK;
   f->closed = true;
+  if (f->staged) {
+    f->copy.assign(f->film, f->film + g_w * g_h * 4);
+    std::fill(f->film, f->film + g_w * g_h * 4, 0.0f);
+  }
   return VPT_OK;
 }
 int vpt_gpu_feed_query(vpt_gpu_feed* f, int* done, uint64_t*) {
@@ -98,6 +113,12 @@ int vpt_gpu_feed_destroy(vpt_gpu_feed* f) {
   --g_open_feeds;
   delete f;
   return VPT_OK;
+}
+int vpt_gpu_feed_collect(vpt_gpu_feed* f, float* host) {
+  if (!f->staged) return VPT_E_INVALID;
+  vpt_gpu_feed_close(f);
+  for (int64_t i = 0; i < g_w * g_h * 4; ++i) host[i] += f->copy[i];
+  return vpt_gpu_feed_destroy(f);
 }
 }
 

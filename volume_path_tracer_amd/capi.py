@@ -273,6 +273,9 @@ def lib() -> C.CDLL:
         L.vpt_gpu_feed_close.argtypes = [vp]
         L.vpt_gpu_feed_query.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_uint64)]
         L.vpt_gpu_feed_destroy.argtypes = [vp]
+    if hasattr(L, "vpt_gpu_feed_open_staged"):
+        L.vpt_gpu_feed_open_staged.argtypes = [vp, vp, vp, C.c_uint64, C.POINTER(vp)]
+        L.vpt_gpu_feed_collect.argtypes = [vp, fp]
     _lib = L
     return L
 

@@ -1280,7 +1280,7 @@ int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* ctx, float* film_device, float* film
   if (rc) return rc;
   float* f = film_device ? film_device : ctx->film;
   const size_t bytes = ctx->film_count * sizeof(float);
-  if (!ctx->staging) VPT_HIP(hipHostMalloc((void**)&ctx->staging, bytes, hipHostMallocDefault));  // (feeds allocate it first)
+  if (!ctx->staging) VPT_HIP(hipHostMalloc((void**)&ctx->staging, bytes, hipHostMallocDefault));
   VPT_HIP(hipMemcpyAsync(ctx->staging, f, bytes, hipMemcpyDeviceToHost, ctx->stream));
   VPT_HIP(hipMemsetAsync(f, 0, bytes, ctx->stream));
   VPT_HIP(hipStreamSynchronize(ctx->stream));
@@ -1303,6 +1303,8 @@ struct vpt_gpu_feed {
   uint32_t* error = nullptr;  // block[1]: a lane that gave up waiting stores 1 here
   uint64_t* ring = nullptr;
   uint32_t* counts = nullptr;
+  float* staged = nullptr;  // hipHostMalloc'd film_count floats (a staged feed's film, copied out at close)
+  bool stage = false;
   uint64_t cap = 0;
   uint64_t published = 0;
   hipEvent_t closed_ev = nullptr;
@@ -1317,6 +1319,7 @@ void feed_free(vpt_gpu_feed* f) {
   (void)hipSetDevice(f->ctx->device);
   if (f->closed_ev) (void)hipEventDestroy(f->closed_ev);
   (void)hipHostFree(f->block);
+  if (f->staged) (void)hipHostFree(f->staged);
   delete f;
 }
 
@@ -1334,7 +1337,10 @@ void feed_publish(vpt_gpu_feed* f, bool close) {
 
 extern "C" {
 
-int vpt_gpu_feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t window, vpt_gpu_feed** out) {
+}  // extern "C"
+
+namespace {
+int feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t window, bool stage, vpt_gpu_feed** out) {
   if (!ctx || !out || !hip_stream) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_open: null argument");
   *out = nullptr;
   if (ctx->scene.pixel_mode) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_open: feeds run the reference RNG mode");
@@ -1342,8 +1348,6 @@ int vpt_gpu_feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, ui
   if (rc) return rc;
   uint64_t cap = 1024;
   while (cap < window && cap < (1ULL << 26)) cap <<= 1;
-  // the context's film staging, before any feed holds the device (vpt_gpu_film_flush_to_host)
-  if (!ctx->staging) VPT_HIP(hipHostMalloc((void**)&ctx->staging, ctx->film_count * sizeof(float), hipHostMallocDefault));
   std::unique_ptr<vpt_gpu_feed, void (*)(vpt_gpu_feed*)> f(nullptr, feed_free);
   for (size_t i = 0; i < ctx->feed_pool.size(); ++i)
     if (ctx->feed_pool[i]->cap == cap) {  // a pooled feed of this window
@@ -1363,6 +1367,9 @@ int vpt_gpu_feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, ui
     f->counts = reinterpret_cast<uint32_t*>(f->ring + cap);
     VPT_HIP(hipEventCreateWithFlags(&f->closed_ev, hipEventDisableTiming));
   }
+  if (stage && !f->staged)
+    VPT_HIP(hipHostMalloc((void**)&f->staged, ctx->film_count * sizeof(float), hipHostMallocDefault));
+  f->stage = stage;
   f->stream = (hipStream_t)hip_stream;
   f->film = film_device ? film_device : ctx->film;
   f->published = 0;
@@ -1378,6 +1385,38 @@ int vpt_gpu_feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, ui
   if ((rc = render(ctx, 0, ~0ULL >> 1, f->film, nullptr, hip_stream, nullptr, 0, nullptr, &fl))) return rc;
   *out = f.release();
   return VPT_OK;
+}
+
+// Waits for a closed feed's work; with film_host, adds its staged film there.  The feed goes back to the
+// context's pool unless a HIP failure leaves its launch possibly still reading the block (then it leaks).
+int feed_finish(vpt_gpu_feed* f, float* film_host) {
+  bool complete = false;
+  int rc = VPT_OK;
+  const hipError_t e = hipEventSynchronize(f->closed_ev);
+  if (e != hipSuccess)
+    rc = vpt::set_error(VPT_E_HIP, std::string("vpt_gpu_feed_destroy: ") + hipGetErrorString(e));
+  else
+    complete = true;
+  if (complete && __atomic_load_n(f->error, __ATOMIC_ACQUIRE))
+    rc = vpt::set_error(VPT_E_STATE, "vpt_gpu_feed_destroy: lanes of the feed's launch gave up waiting for jobs");
+  if (rc == VPT_OK && film_host) {
+    const float* src = f->staged;
+    for (uint64_t i = 0; i < f->ctx->film_count; ++i) film_host[i] += src[i];
+  }
+  if (complete) f->ctx->feed_pool.push_back(f);
+  return rc;
+}
+}  // namespace
+
+extern "C" {
+
+int vpt_gpu_feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t window, vpt_gpu_feed** out) {
+  return feed_open(ctx, film_device, hip_stream, window, false, out);
+}
+
+int vpt_gpu_feed_open_staged(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t window,
+                             vpt_gpu_feed** out) {
+  return feed_open(ctx, film_device, hip_stream, window, true, out);
 }
 
 int vpt_gpu_feed_push(vpt_gpu_feed* f, const uint64_t* jids, uint64_t n) {
@@ -1420,6 +1459,11 @@ int vpt_gpu_feed_close(vpt_gpu_feed* f) {
   hipLaunchKernelGGL(vpt::vpt_tile_count_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, f->stream,
                      f->ctx->scene_dev, f->film, counts_dev);
   VPT_HIP(hipGetLastError());
+  if (f->stage) {  // queued now, ahead of any feed opened after this one (which may share a hardware queue)
+    const size_t bytes = f->ctx->film_count * sizeof(float);
+    VPT_HIP(hipMemcpyAsync(f->staged, f->film, bytes, hipMemcpyDeviceToHost, f->stream));
+    VPT_HIP(hipMemsetAsync(f->film, 0, bytes, f->stream));
+  }
   VPT_HIP(hipEventRecord(f->closed_ev, f->stream));
   return VPT_OK;
 }
@@ -1442,19 +1486,15 @@ int vpt_gpu_feed_query(vpt_gpu_feed* f, int* done, uint64_t* pushed) {
 
 int vpt_gpu_feed_destroy(vpt_gpu_feed* f) {
   if (!f) return VPT_OK;
-  int rc = vpt_gpu_feed_close(f);
-  bool complete = false;
-  if (rc == VPT_OK) {
-    const hipError_t e = hipEventSynchronize(f->closed_ev);
-    if (e != hipSuccess)
-      rc = vpt::set_error(VPT_E_HIP, std::string("vpt_gpu_feed_destroy: ") + hipGetErrorString(e));
-    else
-      complete = true;
-  }
-  if (complete && __atomic_load_n(f->error, __ATOMIC_ACQUIRE))
-    rc = vpt::set_error(VPT_E_STATE, "vpt_gpu_feed_destroy: lanes of the feed's launch gave up waiting for jobs");
-  if (complete) f->ctx->feed_pool.push_back(f);  // (after a HIP failure the launch may still read the block: leak it)
-  return rc;
+  const int rc = vpt_gpu_feed_close(f);
+  return rc ? rc : feed_finish(f, nullptr);
+}
+
+int vpt_gpu_feed_collect(vpt_gpu_feed* f, float* film_host) {
+  if (!f || !film_host) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_collect: null argument");
+  if (!f->stage) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_collect: not a staged feed (vpt_gpu_feed_open_staged)");
+  const int rc = vpt_gpu_feed_close(f);
+  return rc ? rc : feed_finish(f, film_host);
 }
 
 int vpt_gpu_film_clear(vpt_gpu_ctx* ctx) {

@@ -292,14 +292,15 @@ class Integrator:
 
 class Feed:
     """A running launch that renders job ids as they are pushed (vpt_gpu_feed_*, include/vpt_gpu.h) into
-    `film` (a device tensor of the context's film shape) on `stream` (a torch stream of the device)."""
+    `film` (a device tensor of the context's film shape) on `stream` (a torch stream of the device).  A
+    staged feed's close also queues its film's copy-out and clearing; collect() adds the film to a host film."""
 
-    def __init__(self, integrator: "Integrator", film, stream, window: int = 1 << 19):
+    def __init__(self, integrator: "Integrator", film, stream, window: int = 1 << 19, staged: bool = False):
         self.it, self.film, self.stream = integrator, film, stream
         h = C.c_void_p()
-        capi.check(capi.lib().vpt_gpu_feed_open(integrator.h, C.c_void_p(film.data_ptr()),
-                                                C.c_void_p(int(stream.cuda_stream)), int(window), C.byref(h)),
-                   "vpt_gpu_feed_open")
+        fn = "vpt_gpu_feed_open_staged" if staged else "vpt_gpu_feed_open"
+        capi.check(getattr(capi.lib(), fn)(integrator.h, C.c_void_p(film.data_ptr()),
+                                           C.c_void_p(int(stream.cuda_stream)), int(window), C.byref(h)), fn)
         self.h = h
 
     def push(self, jids) -> None:
@@ -320,6 +321,13 @@ class Feed:
             h, self.h = self.h, None
             capi.check(capi.lib().vpt_gpu_feed_destroy(h), "vpt_gpu_feed_destroy")
 
+    def collect(self, film_host: np.ndarray) -> None:
+        """Waits for a staged feed and adds its film into film_host (float32, C-contiguous); frees it."""
+        assert film_host.dtype == np.float32 and film_host.flags.c_contiguous
+        h, self.h = self.h, None
+        capi.check(capi.lib().vpt_gpu_feed_collect(h, film_host.ctypes.data_as(C.POINTER(C.c_float))),
+                   "vpt_gpu_feed_collect")
+
 
 def run(cfg: capi.Configuration, integrator: Integrator, tp: TileProvider, film: Optional[np.ndarray] = None,
         batch_jobs: int = 4096, flush_seconds: float = 0.2, window: int = 1 << 19) -> np.ndarray:
@@ -334,18 +342,15 @@ def run(cfg: capi.Configuration, integrator: Integrator, tp: TileProvider, film:
         raise ValueError("run: film must be a C-contiguous float32 [H][W][4] array")
     films = [torch.zeros_like(integrator.film) for _ in range(2)]
     streams = [torch.cuda.Stream(device=integrator.dev) for _ in range(2)]
-    feeds = [Feed(integrator, films[0], streams[0], window), None]
+    feeds = [Feed(integrator, films[0], streams[0], window, staged=True), None]
     cur, last = 0, time.monotonic()
 
     def flush(i):
-        # no device-wide synchronize: the other feed's launch holds the device until it is closed, so it
-        # would wait for that launch's lanes to give up; vpt_gpu_film_flush_to_host (as vpt_run.hpp's drain)
-        # copies through the context's pinned staging and waits for its own stream only
-        feeds[i].destroy()
-        feeds[i] = None
-        capi.check(capi.lib().vpt_gpu_film_flush_to_host(integrator.h, C.c_void_p(films[i].data_ptr()),
-                                                          out.ctypes.data_as(C.POINTER(C.c_float))),
-                   "vpt_gpu_film_flush_to_host")
+        # staged feeds (as vpt_run.hpp's drain): nothing is queued on the GPU while the other feed's launch
+        # runs -- it holds the device until closed, and work queued meanwhile (a film copy, a device-wide
+        # synchronize) could wait behind it until its lanes give up
+        f, feeds[i] = feeds[i], None
+        f.collect(out)
 
     try:
         while True:
@@ -359,7 +364,7 @@ def run(cfg: capi.Configuration, integrator: Integrator, tp: TileProvider, film:
             if feeds[old] is None and time.monotonic() - last >= flush_seconds:
                 feeds[cur].close()
                 cur, last = old, time.monotonic()
-                feeds[cur] = Feed(integrator, films[cur], streams[cur], window)
+                feeds[cur] = Feed(integrator, films[cur], streams[cur], window, staged=True)
         for i in (cur ^ 1, cur):
             if feeds[i] is not None:
                 flush(i)
