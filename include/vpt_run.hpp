@@ -164,10 +164,20 @@ class FeedPipeline {
 
  private:
   // The feed's close queued its film's copy-out and clearing (a staged feed: nothing is queued on the GPU
-  // while the other feed's launch runs); collect waits for them and adds the film into film_host.
+  // while the other feed's launch runs); collect adds the film into film_host once they have run.  The
+  // wait happens before the film lock: another caller's launch may be waiting for this device's CUs,
+  // which this feed's launch holds until that caller -- maybe blocked on the lock -- closes its feed.
   int flush(int i, float* film_host) {
-    std::lock_guard<std::mutex> lock(film_mutex());
-    const int rc = vpt_gpu_feed_collect(feeds_[i], film_host);
+    int rc = vpt_gpu_feed_close(feeds_[i]);
+    for (int done = 0; rc == VPT_OK && !done;)
+      if ((rc = vpt_gpu_feed_query(feeds_[i], &done, nullptr)) == VPT_OK && !done)
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+    if (rc == VPT_OK) {
+      std::lock_guard<std::mutex> lock(film_mutex());
+      rc = vpt_gpu_feed_collect(feeds_[i], film_host);
+    } else {
+      (void)vpt_gpu_feed_destroy(feeds_[i]);
+    }
     feeds_[i] = nullptr;
     return rc;
   }

@@ -2,7 +2,10 @@
 // C ABI's stream, film and feed calls, so the host-side protocol -- tokens taken by drivers and helpers,
 // pushes under the pipeline's lock, feed switches, the progressive film, helpers detaching before the
 // driver's final flush -- is checked without a GPU: every job id the provider hands out must be "rendered"
-// (pushed into some open feed) exactly once, and the host film must count every sample once.
+// (pushed into some open feed) exactly once, and the host film must count every sample once.  The mock
+// keeps the GPU's one blocking rule: a feed's launch holds the device (every context shares one here) until
+// it is closed, so a feed's work completes only once it and every feed opened before it are closed; a wait
+// that cannot end that way within 5 s is reported as a deadlock.
 //
 //   dropin_mock drivers=<n> helpers=<n> w= h= waves= batch= flush_ms= window= stop_after=
 #include <algorithm>
@@ -24,6 +27,8 @@ int64_t g_w = 0, g_h = 0, g_tw = 8, g_th = 8, g_ntx = 0;
 std::mutex g_mu;
 std::vector<uint32_t> g_rendered;  // per jid: times pushed into an open feed
 std::atomic<int> g_open_feeds{0}, g_max_open{0};
+std::mutex g_dev_mu;            // the "device": feeds in open order
+std::vector<struct vpt_gpu_feed*> g_dev_feeds;
 }  // namespace
 
 struct vpt_gpu_ctx {
@@ -36,6 +41,27 @@ struct vpt_gpu_feed {
   bool staged = false;
   std::vector<float> copy;  // a staged feed's film, copied out at close
 };
+
+namespace {
+bool complete(vpt_gpu_feed* f) {  // closed, and every feed opened before it closed (its launch has run)
+  std::lock_guard<std::mutex> l(g_dev_mu);
+  for (vpt_gpu_feed* g : g_dev_feeds) {
+    if (!g->closed) return false;
+    if (g == f) return true;
+  }
+  return true;
+}
+int wait_complete(vpt_gpu_feed* f) {
+  for (int i = 0; i < 50000 && !complete(f); ++i) std::this_thread::sleep_for(std::chrono::microseconds(100));
+  if (complete(f)) return VPT_OK;
+  std::printf("dropin_mock: deadlock: waited 5 s for a feed behind an open one\n");
+  return VPT_E_STATE;
+}
+void dev_remove(vpt_gpu_feed* f) {
+  std::lock_guard<std::mutex> l(g_dev_mu);
+  g_dev_feeds.erase(std::find(g_dev_feeds.begin(), g_dev_feeds.end(), f));
+}
+}  // namespace
 
 extern "C" {
 const char* vpt_last_error(void) { return "mock"; }
@@ -69,6 +95,10 @@ int vpt_gpu_feed_open(vpt_gpu_ctx* c, float* film, void* stream, uint64_t, vpt_g
   *out = new vpt_gpu_feed();
   (*out)->ctx = c;
   (*out)->film = film ? film : c->own.data();
+  {
+    std::lock_guard<std::mutex> l(g_dev_mu);
+    g_dev_feeds.push_back(*out);
+  }
   const int n = ++g_open_feeds;
   int m = g_max_open.load();
   while (n > m && !g_max_open.compare_exchange_weak(m, n)) {
@@ -97,6 +127,7 @@ int vpt_gpu_feed_open_staged(vpt_gpu_ctx* c, float* film, void* stream, uint64_t
   return rc;
 }
 int vpt_gpu_feed_close(vpt_gpu_feed* f) {
+  std::lock_guard<std::mutex> l(g_dev_mu);
   if (f->closed) return VPT_OK;
   f->closed = true;
   if (f->staged) {
@@ -106,19 +137,27 @@ int vpt_gpu_feed_close(vpt_gpu_feed* f) {
   return VPT_OK;
 }
 int vpt_gpu_feed_query(vpt_gpu_feed* f, int* done, uint64_t*) {
-  *done = f->closed ? 1 : 0;
+  *done = complete(f) ? 1 : 0;
   return VPT_OK;
 }
 int vpt_gpu_feed_destroy(vpt_gpu_feed* f) {
+  vpt_gpu_feed_close(f);
+  const int rc = wait_complete(f);
+  dev_remove(f);
   --g_open_feeds;
   delete f;
-  return VPT_OK;
+  return rc;
 }
 int vpt_gpu_feed_collect(vpt_gpu_feed* f, float* host) {
   if (!f->staged) return VPT_E_INVALID;
   vpt_gpu_feed_close(f);
-  for (int64_t i = 0; i < g_w * g_h * 4; ++i) host[i] += f->copy[i];
-  return vpt_gpu_feed_destroy(f);
+  int rc = wait_complete(f);
+  if (rc == VPT_OK)
+    for (int64_t i = 0; i < g_w * g_h * 4; ++i) host[i] += f->copy[i];
+  dev_remove(f);
+  --g_open_feeds;
+  delete f;
+  return rc;
 }
 }
 
