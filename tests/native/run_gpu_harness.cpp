@@ -219,7 +219,10 @@ int main(int argc, char** argv) {
                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count());
     }
     for (int i = 0; i < threads; ++i)
-      if (rc[i]) return fail("vpt_gpu::drain");
+      if (rc[i]) {  // (the message was set on the worker thread: vpt_last_error is per thread)
+        std::fprintf(stderr, "run_gpu_harness: vpt_gpu::drain on thread %d returned %d\n", i, rc[i]);
+        return 1;
+      }
     for (auto* c : ctx) vpt_gpu_destroy(c);
     vpt_grid_free(dens);
     if (temp) vpt_grid_free(temp);

@@ -1314,6 +1314,16 @@ struct vpt_gpu_feed {
 namespace {
 constexpr double kFeedHostWaitS = 120.0;  // a push waiting this long for a ring slot gives up
 
+// VPT_FEED_TRACE=1: one stderr line per feed event (open / close / a push's wait for a ring slot / the
+// end of its work), milliseconds since the first event -- for diagnosing a drop-in's host protocol.
+void feed_trace(const vpt_gpu_feed* f, const char* what, double a = 0, double b = 0) {
+  static const bool on = std::getenv("VPT_FEED_TRACE") && std::atoi(std::getenv("VPT_FEED_TRACE")) > 0;
+  if (!on) return;
+  static const auto t0 = std::chrono::steady_clock::now();
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  std::fprintf(stderr, "feed %10.2f ms %p %-8s %.0f %.0f\n", ms, (const void*)f, what, a, b);
+}
+
 void feed_free(vpt_gpu_feed* f) {
   if (!f) return;
   (void)hipSetDevice(f->ctx->device);
@@ -1383,6 +1393,7 @@ int feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t w
   ring_dev = word_dev + 8;
   const vpt::FeedLaunch fl{word_dev, ring_dev, cap - 1, reinterpret_cast<unsigned*>(word_dev + 1)};
   if ((rc = render(ctx, 0, ~0ULL >> 1, f->film, nullptr, hip_stream, nullptr, 0, nullptr, &fl))) return rc;
+  feed_trace(f.get(), stage ? "open_stg" : "open", (double)cap, (double)(uintptr_t)hip_stream);
   *out = f.release();
   return VPT_OK;
 }
@@ -1392,11 +1403,13 @@ int feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t w
 int feed_finish(vpt_gpu_feed* f, float* film_host) {
   bool complete = false;
   int rc = VPT_OK;
+  feed_trace(f, "wait", (double)f->published);
   const hipError_t e = hipEventSynchronize(f->closed_ev);
   if (e != hipSuccess)
     rc = vpt::set_error(VPT_E_HIP, std::string("vpt_gpu_feed_destroy: ") + hipGetErrorString(e));
   else
     complete = true;
+  feed_trace(f, "ended", (double)f->published, complete ? (double)__atomic_load_n(f->error, __ATOMIC_ACQUIRE) : -1.0);
   if (complete && __atomic_load_n(f->error, __ATOMIC_ACQUIRE))
     rc = vpt::set_error(VPT_E_STATE, "vpt_gpu_feed_destroy: lanes of the feed's launch gave up waiting for jobs");
   if (rc == VPT_OK && film_host) {
@@ -1431,11 +1444,14 @@ int vpt_gpu_feed_push(vpt_gpu_feed* f, const uint64_t* jids, uint64_t n) {
     if (__atomic_load_n(slot, __ATOMIC_ACQUIRE) != vpt::kFeedEmpty) {
       // the window is full (cap items published and not yet started): publish what we have, then wait
       feed_publish(f, false);
+      const auto w0 = std::chrono::steady_clock::now();
       while (__atomic_load_n(slot, __ATOMIC_ACQUIRE) != vpt::kFeedEmpty) {
         std::this_thread::sleep_for(std::chrono::microseconds(50));
         if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kFeedHostWaitS)
           return vpt::set_error(VPT_E_STATE, "vpt_gpu_feed_push: the feed's launch stopped taking jobs");
       }
+      const double waited = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+      if (waited > 1.0) feed_trace(f, "slotwait", (double)f->published, waited);
     }
     *slot = jid;
     ++f->counts[jid % T];
@@ -1452,6 +1468,7 @@ int vpt_gpu_feed_close(vpt_gpu_feed* f) {
   if (rc) return rc;
   f->closed = true;
   feed_publish(f, true);
+  feed_trace(f, "close", (double)f->published);
   // after the launch: the pushed jobs' sample counts (read from the pinned block, final now)
   uint32_t* counts_dev = nullptr;
   VPT_HIP(hipHostGetDevicePointer((void**)&counts_dev, f->counts, 0));
