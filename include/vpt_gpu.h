@@ -352,8 +352,7 @@ int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* ctx, float* film_device, float* film
  * is closed -- a second feed opened meanwhile starts as the first one's lanes leave -- so push to a feed
  * only after the feeds opened before it have been closed; and a call that waits for the whole device
  * (hipDeviceSynchronize, and hipFree / hipHostMalloc / hipHostFree may) waits for an open feed's lanes to
- * give up: wait for streams instead.  The launch leaves two blocks' slots free, so small kernels and copies
- * on other streams (vpt_gpu_film_flush_to_host's copy and clear) still run beside it.  A destroyed feed's memory is kept by the context for the next
+ * give up: wait for streams instead.  A destroyed feed's memory is kept by the context for the next
  * vpt_gpu_feed_open (freed by vpt_gpu_destroy).  Feeds use a host-pinned ring (8 bytes per
  * window slot) and run the reference RNG mode. */
 typedef struct vpt_gpu_feed vpt_gpu_feed;
@@ -362,11 +361,12 @@ int vpt_gpu_feed_push(vpt_gpu_feed* feed, const uint64_t* jids, uint64_t n);
 int vpt_gpu_feed_close(vpt_gpu_feed* feed);
 int vpt_gpu_feed_query(vpt_gpu_feed* feed, int* done, uint64_t* pushed);
 int vpt_gpu_feed_destroy(vpt_gpu_feed* feed);
-/* A staged feed: its close also queues, on the feed's stream behind the launch, the copy of its film into
- * a pinned host buffer of the feed and the film's clearing -- so retiring it needs no GPU work queued later
- * (work queued while another feed is open may wait behind that feed's launch: streams can share a
- * hardware queue).  vpt_gpu_feed_collect closes if needed, waits, adds the staged film into film_host
- * (film_count floats; the caller serialises writers of film_host) and frees the feed like destroy. */
+/* A staged feed: its launch's last block copies the film into a pinned host buffer of the feed and clears
+ * it, so retiring the feed needs no GPU work queued after the launch (work queued while another feed is
+ * open may wait for the CUs that feed's launch holds).  vpt_gpu_feed_collect closes if needed, waits, adds
+ * the copy and the pushed jobs' sample counts into film_host (film_count floats; the caller serialises
+ * writers of film_host) and frees the feed like destroy.  The ring of a feed holds at least twice the
+ * launch's lanes (window rounded up). */
 int vpt_gpu_feed_open_staged(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t window,
                              vpt_gpu_feed** out);
 int vpt_gpu_feed_collect(vpt_gpu_feed* feed, float* film_host);

@@ -73,9 +73,9 @@ namespace vpt_gpu {
 //     the window plus the jobs in flight -- as the reference's workers each hold the token they render;
 //   * the film is progressive (main.cpp:101-132 shows it at 5 FPS): every flush_seconds the running feed
 //     is closed and a new one opened on the other stream and film (its lanes start as the old launch's
-//     drain frees the CUs); the old feed's close queues its film's copy to pinned memory and clearing
-//     behind its launch, and once those have run the film is added into film_host (under a mutex shared
-//     by all callers).  film_host's sample counts thus rise during the run, by
+//     drain frees the CUs); the old launch's last block copies its film to pinned memory and clears it,
+//     and once the launch has ended the copy is added into film_host (under a mutex shared by all
+//     callers).  film_host's sample counts thus rise during the run, by
 //     whole jobs, and the final film is the same sum.
 using JobRuns = std::vector<std::pair<uint64_t, uint64_t>>;  // contiguous (jid_begin, count) runs
 
@@ -156,15 +156,18 @@ class FeedPipeline {
     return VPT_OK;
   }
   int finish(float* film_host) {
-    for (int i = 0; i < 2; ++i)
+    for (vpt_gpu_feed* f : feeds_)  // every feed closed before any wait: an open one holds the device
+      if (f)
+        if (int rc = vpt_gpu_feed_close(f)) return rc;
+    for (int i : {cur_ ^ 1, cur_})
       if (feeds_[i])
         if (int rc = flush(i, film_host)) return rc;
     return VPT_OK;
   }
 
  private:
-  // The feed's close queued its film's copy-out and clearing (a staged feed: nothing is queued on the GPU
-  // while the other feed's launch runs); collect adds the film into film_host once they have run.  The
+  // A staged feed's launch copies out and clears its own film (nothing is queued on the GPU while the
+  // other feed's launch runs); collect adds the copy into film_host once the launch has ended.  The
   // wait happens before the film lock: another caller's launch may be waiting for this device's CUs,
   // which this feed's launch holds until that caller -- maybe blocked on the lock -- closes its feed.
   int flush(int i, float* film_host) {

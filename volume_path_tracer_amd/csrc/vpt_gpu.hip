@@ -63,11 +63,12 @@ constexpr int kBlockThreads = 256;
 // The lanes' cold state (vpt_integrator.h LaneCold), one slot per thread of the integrator's block.
 __shared__ LaneCold g_lane_cold[kBlockThreads];
 // Feed mode (vpt_gpu_feed_*): the published word's closed bit, an empty ring slot, a lane's "item
-// reserved, not yet published" mark (LaneCold::pix), and how long a lane waits for its item before it
-// gives up (s_memrealtime ticks at 100 MHz: 30 s).
+// reserved, not yet published" and "waiting, nothing reserved" marks (LaneCold::pix), and how long a lane
+// waits before it gives up (s_memrealtime ticks at 100 MHz: 30 s).
 constexpr uint64_t kFeedClosed = 1ULL << 63;
 constexpr uint64_t kFeedEmpty = ~0ULL;
 constexpr int32_t kFeedPending = -2;
+constexpr int32_t kFeedWait = -3;
 constexpr uint32_t kFeedDeadline = 3000000000u;
 // LDS copies of the small lookup tables the evaluation reads per lane (logf's 16 x 2 doubles; the
 // temperature kernel's 501 x 3 blackbody table): LDS reads instead of vector-memory loads, which
@@ -103,6 +104,7 @@ struct KernelEnvT {
   uint64_t* feed_ring;
   uint64_t feed_mask;                // ring slots - 1 (a power of two)
   unsigned* feed_error;
+  float* feed_staged;                // a staged feed: the film's host-pinned copy, written by the last block
 
   // Adds w for every active lane with w != 0 (w uniform per call site) to a workgroup counter.
   __device__ __forceinline__ void tally(int32_t k, int32_t w) {
@@ -231,25 +233,41 @@ struct KernelEnvT {
   }
   // Feed mode: the lane reserves item k (one atomic on the launch's counter) and keeps it in its cold
   // state (item_lo / item_hi; pix = kFeedPending) until the host has published it: then it reads the job
-  // id from ring slot k & feed_mask and marks the slot empty for the host to reuse.  Once the feed is
-  // closed, items beyond the published count are never published: the lane ends.  A lane that waits
-  // kFeedDeadline without either (a host that died) ends too and flags feed_error, so the grid always
-  // drains.  The loads and stores of host memory are vector-memory atomics of system scope.
+  // id from ring slot k & feed_mask and marks the slot empty for the host to reuse.  A lane reserves only
+  // while the counter is below the published count (else it waits with nothing reserved, pix =
+  // kFeedWait): a reserved, unpublished item pins its ring slot until its lane asks again, which behind
+  // busy wave-mates (the fetch block is gated) can take milliseconds -- and the host's window stalls on
+  // that slot (r04 fd: 1.35 s stalls, C3 frame 3.7 s).  Once the feed is closed, items beyond the
+  // published count are never published: the lane ends.  A lane that waits kFeedDeadline without either
+  // (a host that died) ends too and flags feed_error, so the grid always drains.  The loads and stores of
+  // host memory are vector-memory atomics of system scope.
   __device__ int fetch_feed(uint64_t& j) {
     LaneCold& lc = cold();
     const uint32_t now = (uint32_t)__builtin_amdgcn_s_memrealtime();  // 100 MHz
-    if (lc.pix != kFeedPending) {
-      const uint64_t k = atomicAdd(job_counter, 1ULL);
-      lc.item_lo = (uint32_t)k;
-      lc.item_hi = (uint32_t)(k >> 32);
-      lc.pix = kFeedPending;
-      lc.x0 = (int32_t)now;  // wait start
-    }
-    const uint64_t k = ((uint64_t)lc.item_hi << 32) | lc.item_lo;
     // Relaxed system-scope loads of host memory go to the host every time; the slot is read only after
     // the word has shown it published (a control dependency), and the host wrote it before the word.
     const uint64_t w = __hip_atomic_load(feed_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (k < (w & ~kFeedClosed)) {
+    const uint64_t published = w & ~kFeedClosed;
+    if (lc.pix != kFeedPending) {
+      if (__hip_atomic_load(job_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= published) {
+        if (w & kFeedClosed) return 0;
+        if (lc.pix != kFeedWait) {
+          lc.pix = kFeedWait;
+          lc.x0 = (int32_t)now;  // wait start
+        } else if (now - (uint32_t)lc.x0 > kFeedDeadline) {
+          __hip_atomic_store(feed_error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // (host memory: a store)
+          return 0;
+        }
+        return -1;
+      }
+      const uint64_t k = atomicAdd(job_counter, 1ULL);
+      lc.item_lo = (uint32_t)k;
+      lc.item_hi = (uint32_t)(k >> 32);
+      if (lc.pix != kFeedWait) lc.x0 = (int32_t)now;  // wait start
+      lc.pix = kFeedPending;
+    }
+    const uint64_t k = ((uint64_t)lc.item_hi << 32) | lc.item_lo;
+    if (k < published) {
       uint64_t* slot = feed_ring + (k & feed_mask);
       j = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       // The empty mark is stored only once the id has arrived (a posted write may overtake a read on the
@@ -382,6 +400,28 @@ __device__ __forceinline__ void compact_loop(ScenePtr sp, Lane& ln, Env& env) {
 #endif
 
 // counters[] order = vpt_counters field order
+// A staged feed's retirement, run by the launch's last block once every block has ended: the film is
+// copied into the feed's host-pinned buffer and cleared, inside the launch -- nothing is queued behind it,
+// where a copy or fill could wait for the CUs the next feed's launch holds (r04 fd: 34 s).  The host adds
+// the sample counts it kept per tile when it collects the copy (vpt_gpu_feed_collect).
+__device__ __forceinline__ void feed_retire(const KernelEnv& env, const DevScene& S) {
+  __shared__ int last;
+  __threadfence();  // this thread's film adds are done device-wide before its block counts as ended
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(env.event_count, 1ULL) == (unsigned long long)gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();  // every block's adds are visible to this block's loads
+  float4* film = reinterpret_cast<float4*>(env.film);
+  float4* out = reinterpret_cast<float4*>(env.feed_staged);
+  const uint64_t n = (uint64_t)S.W * (uint64_t)S.H;
+  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const float4 v = film[i];
+    out[i] = v;
+    film[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+}
+
 template <bool HasTemp, bool Debug, bool Runs, bool Lat = false>
 __global__ __launch_bounds__(kBlockThreads, Lat ? VPT_WAVES_LAT : (Debug ? VPT_WAVES_SLOW : (HasTemp ? VPT_WAVES_TEMP : VPT_WAVES_FAST))) void vpt_integrate_kernel(const DevScene* scene, KernelEnvT<Lat> env,
                                                                        unsigned long long* counters) {
@@ -419,7 +459,8 @@ __global__ __launch_bounds__(kBlockThreads, Lat ? VPT_WAVES_LAT : (Debug ? VPT_W
     // Feed mode: a wavefront whose every live lane waits for the host to publish its item sleeps between
     // polls (~27 us), so idle wavefronts do not flood the host link with reads.
     if (!Debug && !Lat && env.feed_word &&
-        __builtin_amdgcn_ballot_w64(ln.state == ST_FETCH && env.cold().pix == kFeedPending) ==
+        __builtin_amdgcn_ballot_w64(ln.state == ST_FETCH && (env.cold().pix == kFeedPending ||
+                                                              env.cold().pix == kFeedWait)) ==
             __builtin_amdgcn_read_exec())
       for (int i = 0; i < 8; ++i) __builtin_amdgcn_s_sleep(127);
   }
@@ -430,6 +471,8 @@ __global__ __launch_bounds__(kBlockThreads, Lat ? VPT_WAVES_LAT : (Debug ? VPT_W
 #if defined(VPT_PROFILE) || defined(VPT_PROFILE_TIME)
   if (threadIdx.x < PT_COUNT) atomicAdd(env.prof_buf + 2 * PB_COUNT + threadIdx.x, wg_prof[threadIdx.x]);
 #endif
+  if constexpr (!Debug && !Lat)
+    if (env.feed_staged) feed_retire(env, *scene);
 }
 
 // The film's sample-count channel for the job range [jid_begin, jid_begin + jid_count): a pixel of
@@ -612,6 +655,7 @@ struct FeedLaunch {
   uint64_t* ring;
   uint64_t mask;
   unsigned* error;
+  float* staged;  // nullptr unless a staged feed
 };
 }  // namespace vpt
 
@@ -801,8 +845,6 @@ int ensure_order(vpt_gpu_ctx* ctx) {
   return rank_tiles(ctx);
 }
 
-constexpr uint32_t kFeedSpareBlocks = 2;  // (1 792 resident blocks on 256 CUs: 0.1 % of the grid)
-
 int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film, float* records, void* stream_ptr,
            vpt_event* events = nullptr, uint64_t event_cap = 0, uint32_t* slot_out = nullptr,
            const vpt::FeedLaunch* feed = nullptr) {
@@ -885,11 +927,6 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   const bool use_lat = !dbg && !feed && ctx->lat_mode != 0 &&
                        (ctx->lat_mode == 1 || (!ctx->grid_user && (latency || blocks <= lat_blocks)));
   if (use_lat) blocks = (uint32_t)std::min<uint64_t>(latency ? lat_blocks : blocks, lat_blocks);
-  // A feed's launch holds its slots until it is closed, and the previous feed's film is copied out and
-  // cleared (copy / fill kernels on another stream) while it runs: kFeedSpareBlocks block slots stay free
-  // for them, or they would wait for the open launch, whose lanes wait for the host (r04e: the Python
-  // drop-in's film flush stalled until the lanes' 30 s deadline).
-  if (feed && blocks > 2 * kFeedSpareBlocks) blocks -= kFeedSpareBlocks;
   const uint64_t T = ctx->scene.T;
   if (!feed && ctx->order_mode != VPT_ORDER_JID && jid_begin % T == 0 && jid_count % T == 0 && jid_count < (1ULL << 32)) {
     // whole waves: take the jobs in cost order (same jobs, same samples)
@@ -916,6 +953,7 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.feed_ring = feed ? feed->ring : nullptr;
   env.feed_mask = feed ? feed->mask : 0;
   env.feed_error = feed ? feed->error : nullptr;
+  env.feed_staged = feed ? feed->staged : nullptr;
 #ifdef VPT_EXP_COMPACT
   if (!ctx->xbuf)
     VPT_HIP(hipMalloc((void**)&ctx->xbuf, (size_t)ctx->grid_blocks * vpt::kBlockThreads * vpt::kXWords * 4));
@@ -1303,7 +1341,7 @@ struct vpt_gpu_feed {
   uint32_t* error = nullptr;  // block[1]: a lane that gave up waiting stores 1 here
   uint64_t* ring = nullptr;
   uint32_t* counts = nullptr;
-  float* staged = nullptr;  // hipHostMalloc'd film_count floats (a staged feed's film, copied out at close)
+  float* staged = nullptr;  // hipHostMalloc'd film_count floats: a staged feed's film, copied by its launch
   bool stage = false;
   uint64_t cap = 0;
   uint64_t published = 0;
@@ -1356,8 +1394,12 @@ int feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t w
   if (ctx->scene.pixel_mode) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_open: feeds run the reference RNG mode");
   int rc = ctx_device(ctx);
   if (rc) return rc;
+  // The ring holds at least twice the launch's lanes: a lane reserves an item only while some are
+  // published, so reservations lead the consumed items by at most the lanes, and the host keeps pushing
+  // while the lanes it has already fed work (C3: 458 752 lanes, ring 2^20).
+  const uint64_t lanes = (uint64_t)ctx->grid_blocks * vpt::kBlockThreads;
   uint64_t cap = 1024;
-  while (cap < window && cap < (1ULL << 26)) cap <<= 1;
+  while ((cap < window || cap < 2 * lanes) && cap < (1ULL << 26)) cap <<= 1;
   std::unique_ptr<vpt_gpu_feed, void (*)(vpt_gpu_feed*)> f(nullptr, feed_free);
   for (size_t i = 0; i < ctx->feed_pool.size(); ++i)
     if (ctx->feed_pool[i]->cap == cap) {  // a pooled feed of this window
@@ -1391,7 +1433,9 @@ int feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t w
   uint64_t *word_dev = nullptr, *ring_dev = nullptr;
   VPT_HIP(hipHostGetDevicePointer((void**)&word_dev, f->word, 0));
   ring_dev = word_dev + 8;
-  const vpt::FeedLaunch fl{word_dev, ring_dev, cap - 1, reinterpret_cast<unsigned*>(word_dev + 1)};
+  float* staged_dev = nullptr;
+  if (stage) VPT_HIP(hipHostGetDevicePointer((void**)&staged_dev, f->staged, 0));
+  const vpt::FeedLaunch fl{word_dev, ring_dev, cap - 1, reinterpret_cast<unsigned*>(word_dev + 1), staged_dev};
   if ((rc = render(ctx, 0, ~0ULL >> 1, f->film, nullptr, hip_stream, nullptr, 0, nullptr, &fl))) return rc;
   feed_trace(f.get(), stage ? "open_stg" : "open", (double)cap, (double)(uintptr_t)hip_stream);
   *out = f.release();
@@ -1413,8 +1457,20 @@ int feed_finish(vpt_gpu_feed* f, float* film_host) {
   if (complete && __atomic_load_n(f->error, __ATOMIC_ACQUIRE))
     rc = vpt::set_error(VPT_E_STATE, "vpt_gpu_feed_destroy: lanes of the feed's launch gave up waiting for jobs");
   if (rc == VPT_OK && film_host) {
+    // the launch's last block copied the film here; the sample counts are the jobs pushed per tile (the
+    // same integer sums as vpt_count_kernel's; single_pixel: that pixel only)
+    const vpt::DevScene& S = f->ctx->scene;
     const float* src = f->staged;
-    for (uint64_t i = 0; i < f->ctx->film_count; ++i) film_host[i] += src[i];
+    for (int32_t y = 0; y < S.H; ++y)
+      for (int32_t x = 0; x < S.W; ++x) {
+        const uint64_t p = ((uint64_t)y * (uint64_t)S.W + (uint64_t)x) * 4;
+        const bool counted = !S.single_pixel_enabled || (x == S.sp_x && y == S.sp_y);
+        const uint32_t n = counted ? f->counts[(uint64_t)(y / S.th) * S.ntx + (uint64_t)(x / S.tw)] : 0u;
+        film_host[p] += src[p];
+        film_host[p + 1] += src[p + 1];
+        film_host[p + 2] += src[p + 2];
+        film_host[p + 3] += src[p + 3] + (float)n;
+      }
   }
   if (complete) f->ctx->feed_pool.push_back(f);
   return rc;
@@ -1442,11 +1498,14 @@ int vpt_gpu_feed_push(vpt_gpu_feed* f, const uint64_t* jids, uint64_t n) {
     if (jid >> 62) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_push: job id out of range");
     uint64_t* slot = f->ring + (f->published & (f->cap - 1));
     if (__atomic_load_n(slot, __ATOMIC_ACQUIRE) != vpt::kFeedEmpty) {
-      // the window is full (cap items published and not yet started): publish what we have, then wait
+      // the window is full (cap items published and not yet started): publish what we have, then wait --
+      // spinning first (slots free at the GPU's job rate, tens of millions a second: a sleep between
+      // checks would hold the lanes back), sleeping once the wait is long (a launch not yet started)
       feed_publish(f, false);
       const auto w0 = std::chrono::steady_clock::now();
-      while (__atomic_load_n(slot, __ATOMIC_ACQUIRE) != vpt::kFeedEmpty) {
-        std::this_thread::sleep_for(std::chrono::microseconds(50));
+      for (uint32_t spins = 0; __atomic_load_n(slot, __ATOMIC_ACQUIRE) != vpt::kFeedEmpty; ++spins) {
+        if (spins < (1u << 16)) continue;
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
         if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kFeedHostWaitS)
           return vpt::set_error(VPT_E_STATE, "vpt_gpu_feed_push: the feed's launch stopped taking jobs");
       }
@@ -1469,6 +1528,10 @@ int vpt_gpu_feed_close(vpt_gpu_feed* f) {
   f->closed = true;
   feed_publish(f, true);
   feed_trace(f, "close", (double)f->published);
+  if (f->stage) {  // the launch retires its own film; the host adds the counts at collect
+    VPT_HIP(hipEventRecord(f->closed_ev, f->stream));
+    return VPT_OK;
+  }
   // after the launch: the pushed jobs' sample counts (read from the pinned block, final now)
   uint32_t* counts_dev = nullptr;
   VPT_HIP(hipHostGetDevicePointer((void**)&counts_dev, f->counts, 0));
@@ -1476,11 +1539,6 @@ int vpt_gpu_feed_close(vpt_gpu_feed* f) {
   hipLaunchKernelGGL(vpt::vpt_tile_count_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, f->stream,
                      f->ctx->scene_dev, f->film, counts_dev);
   VPT_HIP(hipGetLastError());
-  if (f->stage) {  // queued now, ahead of any feed opened after this one (which may share a hardware queue)
-    const size_t bytes = f->ctx->film_count * sizeof(float);
-    VPT_HIP(hipMemcpyAsync(f->staged, f->film, bytes, hipMemcpyDeviceToHost, f->stream));
-    VPT_HIP(hipMemsetAsync(f->film, 0, bytes, f->stream));
-  }
   VPT_HIP(hipEventRecord(f->closed_ev, f->stream));
   return VPT_OK;
 }

@@ -293,7 +293,8 @@ class Integrator:
 class Feed:
     """A running launch that renders job ids as they are pushed (vpt_gpu_feed_*, include/vpt_gpu.h) into
     `film` (a device tensor of the context's film shape) on `stream` (a torch stream of the device).  A
-    staged feed's close also queues its film's copy-out and clearing; collect() adds the film to a host film."""
+    staged feed's launch copies out and clears its own film at its end; collect() adds that copy and the
+    sample counts to a host film."""
 
     def __init__(self, integrator: "Integrator", film, stream, window: int = 1 << 19, staged: bool = False):
         self.it, self.film, self.stream = integrator, film, stream
@@ -365,6 +366,9 @@ def run(cfg: capi.Configuration, integrator: Integrator, tp: TileProvider, film:
                 feeds[cur].close()
                 cur, last = old, time.monotonic()
                 feeds[cur] = Feed(integrator, films[cur], streams[cur], window, staged=True)
+        for f in feeds:  # every feed closed before any wait: an open feed's launch holds the device
+            if f is not None:
+                f.close()
         for i in (cur ^ 1, cur):
             if feeds[i] is not None:
                 flush(i)
