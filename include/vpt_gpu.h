@@ -339,10 +339,11 @@ int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* ctx, float* film_device, float* film
 /* Feeds: one launch of the production kernel that renders job ids pushed by the host while it runs --
  * the drop-in's way of handing the GPU a TileProvider's tokens as they are taken, with a bounded queue and
  * no per-batch launch drain (a launch lasts as long as its longest job; a feed's lanes keep taking pushed
- * jobs instead).  vpt_gpu_feed_open launches it on hip_stream (a stream of this context,
- * vpt_gpu_stream_create) into film_device (NULL = the context's own film); `window` (rounded up to a power
- * of two, >= 1024) bounds the jobs pushed and not yet started: vpt_gpu_feed_push blocks while the window is
- * full (VPT_E_STATE if the launch stops taking jobs for 120 s).  Job ids are any jids (< 2^62), e.g.
+ * jobs instead).  vpt_gpu_feed_open prepares it on hip_stream (a stream of this context,
+ * vpt_gpu_stream_create) into film_device (NULL = the context's own film); it is launched once as many jobs
+ * are pushed as it has lanes (C3: 458 752), when the window fills, or at close.  `window` (rounded up to a
+ * power of two, >= 1024 and >= twice the lanes) bounds the jobs pushed and not yet started:
+ * vpt_gpu_feed_push blocks while the window is full (VPT_E_STATE if the launch stops taking jobs for 120 s).  Job ids are any jids (< 2^62), e.g.
  * token.jid(); their samples equal vpt_gpu_render_jobs's.  vpt_gpu_feed_close publishes the end: the
  * launch ends once every pushed job is rendered, then adds their sample counts to the film (asynchronous,
  * on the feed's stream).  vpt_gpu_feed_query: whether a closed feed's work is complete (non-blocking) and
@@ -365,8 +366,7 @@ int vpt_gpu_feed_destroy(vpt_gpu_feed* feed);
  * it, so retiring the feed needs no GPU work queued after the launch (work queued while another feed is
  * open may wait for the CUs that feed's launch holds).  vpt_gpu_feed_collect closes if needed, waits, adds
  * the copy and the pushed jobs' sample counts into film_host (film_count floats; the caller serialises
- * writers of film_host) and frees the feed like destroy.  The ring of a feed holds at least twice the
- * launch's lanes (window rounded up). */
+ * writers of film_host) and frees the feed like destroy. */
 int vpt_gpu_feed_open_staged(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t window,
                              vpt_gpu_feed** out);
 int vpt_gpu_feed_collect(vpt_gpu_feed* feed, float* film_host);

@@ -1347,6 +1347,9 @@ struct vpt_gpu_feed {
   uint64_t published = 0;
   hipEvent_t closed_ev = nullptr;
   bool closed = false;
+  bool launched = false;     // the launch starts once launch_at items are published, or at close
+  uint64_t launch_at = 0;
+  vpt::FeedLaunch fl{};
 };
 
 namespace {
@@ -1435,11 +1438,22 @@ int feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t w
   ring_dev = word_dev + 8;
   float* staged_dev = nullptr;
   if (stage) VPT_HIP(hipHostGetDevicePointer((void**)&staged_dev, f->staged, 0));
-  const vpt::FeedLaunch fl{word_dev, ring_dev, cap - 1, reinterpret_cast<unsigned*>(word_dev + 1), staged_dev};
-  if ((rc = render(ctx, 0, ~0ULL >> 1, f->film, nullptr, hip_stream, nullptr, 0, nullptr, &fl))) return rc;
+  f->fl = vpt::FeedLaunch{word_dev, ring_dev, cap - 1, reinterpret_cast<unsigned*>(word_dev + 1), staged_dev};
+  // The launch is deferred until the ring holds as many items as it has lanes (or the feed is closed):
+  // launched at once, every lane would find the first few published items and reserve past them, and a
+  // lane holding an unpublished item pins its ring slot until its (gated) fetch block runs again.
+  f->launched = false;
+  f->launch_at = lanes;
   feed_trace(f.get(), stage ? "open_stg" : "open", (double)cap, (double)(uintptr_t)hip_stream);
   *out = f.release();
   return VPT_OK;
+}
+
+int feed_launch(vpt_gpu_feed* f) {
+  if (f->launched) return VPT_OK;
+  f->launched = true;
+  feed_trace(f, "launch", (double)f->published);
+  return render(f->ctx, 0, ~0ULL >> 1, f->film, nullptr, f->stream, nullptr, 0, nullptr, &f->fl);
 }
 
 // Waits for a closed feed's work; with film_host, adds its staged film there.  The feed goes back to the
@@ -1502,6 +1516,7 @@ int vpt_gpu_feed_push(vpt_gpu_feed* f, const uint64_t* jids, uint64_t n) {
       // spinning first (slots free at the GPU's job rate, tens of millions a second: a sleep between
       // checks would hold the lanes back), sleeping once the wait is long (a launch not yet started)
       feed_publish(f, false);
+      if (int rc = feed_launch(f)) return rc;
       const auto w0 = std::chrono::steady_clock::now();
       for (uint32_t spins = 0; __atomic_load_n(slot, __ATOMIC_ACQUIRE) != vpt::kFeedEmpty; ++spins) {
         if (spins < (1u << 16)) continue;
@@ -1517,6 +1532,8 @@ int vpt_gpu_feed_push(vpt_gpu_feed* f, const uint64_t* jids, uint64_t n) {
     ++f->published;
   }
   feed_publish(f, false);
+  if (f->published >= f->launch_at)
+    if (int rc = feed_launch(f)) return rc;
   return VPT_OK;
 }
 
@@ -1528,6 +1545,7 @@ int vpt_gpu_feed_close(vpt_gpu_feed* f) {
   f->closed = true;
   feed_publish(f, true);
   feed_trace(f, "close", (double)f->published);
+  if ((rc = feed_launch(f))) return rc;
   if (f->stage) {  // the launch retires its own film; the host adds the counts at collect
     VPT_HIP(hipEventRecord(f->closed_ev, f->stream));
     return VPT_OK;
