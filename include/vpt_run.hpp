@@ -196,10 +196,11 @@ class FeedPipeline {
 };
 
 namespace detail {
-// run()'s threads on one provider (main.cpp starts num_workers of them): each GPU is driven by the one
-// thread that claimed it; the others -- "helpers" -- take tokens too and push their job ids into a driving
-// thread's pipeline, because one thread takes ~50 M tokens/s (one 8x8 job each) and a GPU can render more
-// (C4: ~84 M jobs/s; several GPUs share one provider).
+// Threads on one provider: each GPU is driven by the one thread that claimed it; other threads may take
+// tokens too and push their job ids into a driving thread's pipeline (help()), since one thread takes ~26 M
+// tokens/s while a GPU can render more (C4: ~84 M jobs/s).  run() does not use it: with the restated
+// TileProvider, contended next() calls made it slower (see run_checked); a provider whose next() scales
+// across threads could.
 struct Helpers {
   std::mutex mu;
   std::condition_variable cv;
@@ -419,7 +420,10 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
     std::fprintf(stderr, "vpt_gpu::run: no HIP device (the integrator has no CPU fallback)\n");
     return VPT_E_HIP;
   }
-  if (device < 0) return help(tp, 4096);  // another worker thread drives each GPU: take tokens for them
+  // Another worker thread drives each GPU: return (as r03).  Taking tokens for the drivers (help()) was
+  // measured slower, not faster: with 3 helpers the C3 drain took 4 265 ms instead of 456, C4 1 682 instead
+  // of 316 -- every token is a next() on the one provider, and contended, those calls cost more than they add.
+  if (device < 0) return VPT_OK;
 
   const auto size = film.size();
   const int64_t W = (int64_t)size.x(), H = (int64_t)size.y();
@@ -487,7 +491,7 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   float* film_host = reinterpret_cast<float*>(film.data().data());  // H x W x (X, Y, Z, W)
   // the first batch is pushed first; then 4096 tokens per push (a token is one 8x8 job: 64 samples)
   (void)T;
-  return drain(ctx, tp, film_host, 4096, DrainOptions{}, &runs, true);
+  return drain(ctx, tp, film_host, 4096, DrainOptions{}, &runs);
 }
 
 template <class WorkerParameters, class Volume, class Camera, class TileProvider, class Image, class RNG>

@@ -920,12 +920,13 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
 #else
   const bool temp = ctx->scene.has_temperature != 0, dbg = records != nullptr || events != nullptr;
 #endif
-  // The latency kernel (lane cold state in VGPRs, VPT_WAVES_LAT waves per SIMD) for launches that fill at
-  // most its resident grid anyway: latency-bound ones (on its whole grid) and partly filled ones whose
-  // rule above gives <= lat_per_cu blocks per CU (C2: 2).  Same jobs, same samples.
+  // The latency kernel (lane cold state in VGPRs, VPT_WAVES_LAT waves per SIMD) for latency-bound launches,
+  // on its whole grid: C1 20.7-21.2 -> 19.2-19.5 ms (r04e).  Partly filled launches keep the throughput
+  // kernel: with it C2 100.1-101.2 ms vs 109.5-109.8, C3 shares of 16 / 32 waves 51.6 / 65.9-66.4 vs
+  // 56.1-56.4 / 75.5-76.1 (r04e, profiles/r04e_lat_ab.txt).  lat_mode 1 forces it.  Same jobs, same samples.
   const uint64_t lat_blocks = cus * (uint64_t)ctx->lat_per_cu;
   const bool use_lat = !dbg && !feed && ctx->lat_mode != 0 &&
-                       (ctx->lat_mode == 1 || (!ctx->grid_user && (latency || blocks <= lat_blocks)));
+                       (ctx->lat_mode == 1 || (!ctx->grid_user && latency));
   if (use_lat) blocks = (uint32_t)std::min<uint64_t>(latency ? lat_blocks : blocks, lat_blocks);
   const uint64_t T = ctx->scene.T;
   if (!feed && ctx->order_mode != VPT_ORDER_JID && jid_begin % T == 0 && jid_count % T == 0 && jid_count < (1ULL << 32)) {
