@@ -109,7 +109,7 @@ inline std::mutex& film_mutex() {  // the host film is shared by every caller
 }
 
 // Two streams, two device films and the feeds that render into them, for one drain() call.  push() and
-// tick() are called under mu() when other threads push into the same pipeline (run()'s helpers).
+// tick() are called under mu() when other threads push into the same pipeline (help()).
 class FeedPipeline {
  public:
   std::mutex& mu() { return mu_; }
@@ -251,7 +251,7 @@ int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs,
   return rc ? rc : frc;
 }
 
-// A helper thread of run(): takes tokens batch_jobs at a time and pushes their job ids into a driving
+// A helper thread (run() does not start any, see run_checked): takes tokens batch_jobs at a time and pushes their job ids into a driving
 // thread's pipeline, until the provider is exhausted (or no thread drives a GPU).
 template <class Provider>
 int help(Provider& tp, uint64_t batch_jobs) {
