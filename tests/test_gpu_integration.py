@@ -223,11 +223,15 @@ def test_library_before_torch_keeps_one_hip_runtime():
 
 
 @pytest.mark.gpu
-def test_feed_renders_pushed_jobs_in_any_order():
-    """vpt_gpu_feed_*: job ids pushed while the launch runs -- out of order, with gaps and past a full
-    window (1024 slots for ~2 000 jobs, so pushes wait for the GPU) -- render the oracle's samples; the
-    close adds exactly the pushed jobs' sample counts.  Two feeds of one context on two streams, the
-    second opened while the first runs (its lanes start as the first's leave, once it is closed)."""
+@pytest.mark.parametrize("mode", ["full_grid", "small_grid", "staged_small_grid"])
+def test_feed_renders_pushed_jobs_in_any_order(mode):
+    """vpt_gpu_feed_*: job ids pushed out of order and with gaps render the oracle's samples; the close (or,
+    for a staged feed, the collect) adds exactly the pushed jobs' sample counts.  Two feeds of one context on
+    two streams, the second opened while the first runs (its lanes start as the first's leave, once it is
+    closed).  full_grid: the ~2 000 jobs are fewer than the launch's lanes, so it starts at close.
+    small_grid (2 blocks, 512 lanes: a 1 024-slot ring): the launch starts after 512 pushes and renders
+    while the host pushes, and pushes wait on the full ring.  staged: the launch copies out its own film
+    (its last block) and vpt_gpu_feed_collect adds it and the counts into a host film."""
     import ctypes as C
 
     import torch
@@ -238,6 +242,9 @@ def test_feed_renders_pushed_jobs_in_any_order():
     wl = workload("c3", width=96, height=80, spp=24, grid_n=64)
     dens = SynthGrid(1, 64).grid()
     it = Integrator(wl.cfg, dens, None, device=0)
+    if mode != "full_grid":
+        it.set_tuning(grid_blocks=2)
+    staged = mode.startswith("staged")
     L = capi.lib()
     T = wl.cfg.jobs_per_wave()
     rng = np.random.default_rng(3)
@@ -248,20 +255,30 @@ def test_feed_renders_pushed_jobs_in_any_order():
         capi.check(L.vpt_gpu_stream_create(it.h, C.byref(s)), "stream")
     feeds = []
     halves = np.array_split(jids, 2)
+    open_fn = L.vpt_gpu_feed_open_staged if staged else L.vpt_gpu_feed_open
     for k in range(2):
         f = C.c_void_p()
-        capi.check(L.vpt_gpu_feed_open(it.h, C.c_void_p(films[k].data_ptr()), streams[k], 1000, C.byref(f)), "open")
+        capi.check(open_fn(it.h, C.c_void_p(films[k].data_ptr()), streams[k], 1000, C.byref(f)), "open")
         feeds.append(f)
     for part in np.array_split(halves[0], 7):
         capi.check(L.vpt_gpu_feed_push(feeds[0], part.ctypes.data_as(C.POINTER(C.c_uint64)), part.size), "push")
     capi.check(L.vpt_gpu_feed_close(feeds[0]), "close")  # the first launch holds the CUs until then
     capi.check(L.vpt_gpu_feed_push(feeds[1], halves[1].ctypes.data_as(C.POINTER(C.c_uint64)), halves[1].size), "push")
     capi.check(L.vpt_gpu_feed_close(feeds[1]), "close")
+    host = np.zeros((wl.cfg.height, wl.cfg.width, 4), np.float32)
     for f in feeds:
-        capi.check(L.vpt_gpu_feed_destroy(f), "destroy")
+        if staged:
+            capi.check(L.vpt_gpu_feed_collect(f, host.ctypes.data_as(C.POINTER(C.c_float))), "collect")
+        else:
+            capi.check(L.vpt_gpu_feed_destroy(f), "destroy")
     for s in streams:
         capi.check(L.vpt_gpu_stream_destroy(it.h, s), "stream destroy")
-    total = (films[0] + films[1]).cpu().numpy()
+    if staged:
+        total = host
+        # the launches cleared their device films after copying them out
+        assert not films[0].any().item() and not films[1].any().item()
+    else:
+        total = (films[0] + films[1]).cpu().numpy()
     od = O.OracleGrid(dens, fix_majorants=True)
     ref = np.zeros_like(total)
     # the oracle renders the pushed jobs (contiguous runs of the sorted ids)
@@ -289,4 +306,28 @@ def test_python_run_switches_feeds_every_batch():
     film = run(wl.cfg, it, tp, batch_jobs=7, flush_seconds=0.0, window=1024)
     np.testing.assert_array_equal(film[..., 3], waves)
     ref = _oracle_film("c3", w, h, waves)
+    np.testing.assert_allclose(film[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_python_run_single_pixel():
+    """render.run with the reference's single-pixel mode (worker.cpp:113-116): only that pixel gains samples
+    and counts -- the counts a staged feed's collect adds on the host follow the same rule as the count
+    kernel's."""
+    from volume_path_tracer_amd.render import Integrator, TileProvider, run
+
+    w, h, waves = 40, 24, 4
+    wl = workload("c3", width=w, height=h, spp=waves, grid_n=64)
+    wp = wl.cfg.worker_parameters
+    wp.single_pixel_enabled = 1
+    wp.single_pixel_coord[0], wp.single_pixel_coord[1] = 13, 9
+    dens = SynthGrid(1, 64).grid()
+    it = Integrator(wl.cfg, dens, None, device=0)
+    tp = TileProvider(wl.cfg.output_size, waves, wl.cfg.tile_size)
+    film = run(wl.cfg, it, tp, batch_jobs=11, flush_seconds=0.0)
+    want = np.zeros((h, w), np.float32)
+    want[9, 13] = waves
+    np.testing.assert_array_equal(film[..., 3], want)
+    od = O.OracleGrid(dens, fix_majorants=True)
+    ref, _, _ = O.render_jobs(wl.cfg, od, None, 0, wl.cfg.jobs_per_wave() * waves)
     np.testing.assert_allclose(film[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
