@@ -68,20 +68,25 @@ namespace vpt_gpu {
 // production kernel takes them as they are pushed, batch_jobs at a time, so
 //   * the launch never drains between batches (a launch lasts as long as its longest job; a feed's lanes
 //     keep taking the jobs pushed after it);
-//   * token run-ahead is bounded: a push blocks while window_jobs pushed jobs have not started, so the
-//     provider's job counter (progress(), eta(), what stop_at_next_wave() cuts) leads the GPU by at most
-//     the window plus the jobs in flight -- as the reference's workers each hold the token they render;
+//   * token run-ahead is bounded: a push blocks while window_jobs pushed jobs have not started (the ring
+//     is at least twice the launch's lanes), so the provider's job counter (progress(), eta(), what
+//     stop_at_next_wave() cuts) leads the GPU by at most the ring, the cost_batch jobs held to be pushed
+//     costliest first, and the jobs in flight -- as the reference's workers each hold the token they render;
 //   * the film is progressive (main.cpp:101-132 shows it at 5 FPS): every flush_seconds the running feed
 //     is closed and a new one opened on the other stream and film (its lanes start as the old launch's
 //     drain frees the CUs); the old launch's last block copies its film to pinned memory and clears it,
 //     and once the launch has ended the copy is added into film_host (under a mutex shared by all
-//     callers).  film_host's sample counts thus rise during the run, by
-//     whole jobs, and the final film is the same sum.
+//     callers).  film_host's sample counts thus rise during the run, by whole jobs, and the final film is
+//     the same sum.
 using JobRuns = std::vector<std::pair<uint64_t, uint64_t>>;  // contiguous (jid_begin, count) runs
 
 struct DrainOptions {
   double flush_seconds = 0.2;     // progressive film period (main.cpp's window draws at 5 FPS)
   uint64_t window_jobs = 1 << 19;  // pushed jobs not yet started on the GPU (C3: 16 waves, ~25 ms of work)
+  // Jobs held on the host and pushed costliest tile first (vpt_gpu_tile_costs), cost_batch at a time; 0:
+  // pushed as taken.  The provider hands jobs out in jid order, so a frame's last waves would start their
+  // densest tiles last and the launch would drain on them; samples never depend on the order.
+  uint64_t cost_batch = 1 << 18;
 };
 
 // Takes up to max_jobs tokens; on_token(token&) sees each before it is released.  Returns the count.
@@ -122,8 +127,17 @@ class FeedPipeline {
     }
     if (films_[1]) (void)vpt_gpu_film_free(ctx_, films_[1]);
   }
-  int init(uint64_t window) {
+  int init(uint64_t window, uint64_t cost_batch = 0) {
     window_ = window;
+    if (cost_batch) {  // cost classes per tile, before any feed holds the device (the cost pass syncs)
+      uint64_t T = 0, total = 0;
+      if (int rc = vpt_gpu_job_space(ctx_, &T, &total)) return rc;
+      std::vector<uint32_t> rank(T);
+      if (int rc = vpt_gpu_tile_costs(ctx_, nullptr, rank.data())) return rc;
+      cls_.assign(T, 0);
+      for (uint64_t i = 0; i < T; ++i) cls_[rank[i]] = (uint8_t)((i * kClasses) / T);  // 0: costliest
+      hold_ = cost_batch;
+    }
     for (void*& s : streams_)
       if (int rc = vpt_gpu_stream_create(ctx_, &s)) return rc;
     if (int rc = vpt_gpu_film_alloc(ctx_, &films_[1])) return rc;
@@ -131,9 +145,27 @@ class FeedPipeline {
     return vpt_gpu_feed_open_staged(ctx_, films_[0], streams_[0], window_, &feeds_[0]);
   }
   int push(const JobRuns& runs) {
+    if (hold_) {
+      for (const auto& r : runs)
+        for (uint64_t i = 0; i < r.second; ++i) held_.push_back(r.first + i);
+      return held_.size() >= hold_ ? release() : VPT_OK;
+    }
     ids_.clear();
     for (const auto& r : runs)
       for (uint64_t i = 0; i < r.second; ++i) ids_.push_back(r.first + i);
+    return vpt_gpu_feed_push(feeds_[cur_], ids_.data(), ids_.size());
+  }
+  // Pushes the held jobs into the running feed, costliest tile class first (a counting sort; within a
+  // class in the order taken).
+  int release() {
+    if (held_.empty()) return VPT_OK;
+    uint64_t start[kClasses + 1] = {};
+    const uint64_t T = cls_.size();
+    for (uint64_t j : held_) ++start[cls_[j % T] + 1];
+    for (int c = 0; c < kClasses; ++c) start[c + 1] += start[c];
+    ids_.resize(held_.size());
+    for (uint64_t j : held_) ids_[start[cls_[j % T]]++] = j;
+    held_.clear();
     return vpt_gpu_feed_push(feeds_[cur_], ids_.data(), ids_.size());
   }
   // Adds the retired feed's film to film_host once its launch has ended; every flush_seconds retires the
@@ -156,6 +188,7 @@ class FeedPipeline {
     return VPT_OK;
   }
   int finish(float* film_host) {
+    if (int rc = release()) return rc;
     for (vpt_gpu_feed* f : feeds_)  // every feed closed before any wait: an open one holds the device
       if (f)
         if (int rc = vpt_gpu_feed_close(f)) return rc;
@@ -191,6 +224,10 @@ class FeedPipeline {
   vpt_gpu_feed* feeds_[2] = {nullptr, nullptr};
   int cur_ = 0;
   std::vector<uint64_t> ids_;
+  static constexpr int kClasses = 256;
+  std::vector<uint8_t> cls_;     // per tile: cost class (0 = costliest), with cost_batch
+  std::vector<uint64_t> held_;   // jobs taken, not yet pushed
+  uint64_t hold_ = 0;
   std::chrono::steady_clock::time_point last_switch_;
   std::mutex mu_;
 };
@@ -221,7 +258,7 @@ template <class Provider>
 int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs, const DrainOptions& opt = {},
           const JobRuns* first = nullptr, bool share = false) {
   FeedPipeline pipe(ctx);
-  if (int rc = pipe.init(opt.window_jobs)) return rc;
+  if (int rc = pipe.init(opt.window_jobs, opt.cost_batch)) return rc;
   if (first)
     if (int rc = pipe.push(*first)) return rc;
   detail::Helpers& hub = detail::Helpers::get();

@@ -74,6 +74,16 @@ int vpt_gpu_stream_destroy(vpt_gpu_ctx*, void* s) {
   return VPT_OK;
 }
 int vpt_gpu_stream_sync(vpt_gpu_ctx*, void*) { return VPT_OK; }
+int vpt_gpu_job_space(const vpt_gpu_ctx*, uint64_t* per_wave, uint64_t* total) {
+  *per_wave = (uint64_t)(g_ntx * ((g_h + g_th - 1) / g_th));
+  *total = 0;
+  return VPT_OK;
+}
+int vpt_gpu_tile_costs(vpt_gpu_ctx*, float*, uint32_t* rank) {  // the last tile costliest: a real reorder
+  const uint64_t T = (uint64_t)(g_ntx * ((g_h + g_th - 1) / g_th));
+  for (uint64_t i = 0; i < T; ++i) rank[i] = (uint32_t)(T - 1 - i);
+  return VPT_OK;
+}
 int vpt_gpu_film_alloc(vpt_gpu_ctx*, float** f) {
   *f = new float[(size_t)(g_w * g_h * 4)]();
   return VPT_OK;
@@ -163,7 +173,8 @@ int vpt_gpu_feed_collect(vpt_gpu_feed* f, float* host) {
 
 int main(int argc, char** argv) {
   std::map<std::string, long long> a{{"drivers", 1}, {"helpers", 0}, {"w", 72}, {"h", 40}, {"waves", 5},
-                                     {"batch", 7}, {"flush_ms", 0}, {"window", 1024}, {"stop_after", 0}};
+                                     {"batch", 7}, {"flush_ms", 0}, {"window", 1024}, {"stop_after", 0},
+                                     {"cost_batch", 0}};
   for (int i = 1; i < argc; ++i) {
     const char* eq = std::strchr(argv[i], '=');
     if (eq) a[std::string(argv[i], eq - argv[i])] = std::atoll(eq + 1);
@@ -191,6 +202,7 @@ int main(int argc, char** argv) {
   vpt_gpu::DrainOptions opt;
   opt.flush_seconds = (double)a["flush_ms"] / 1000.0;
   opt.window_jobs = (uint64_t)a["window"];
+  opt.cost_batch = (uint64_t)a["cost_batch"];
   {
     std::lock_guard<std::mutex> l(vpt_gpu::detail::Helpers::get().mu);
     vpt_gpu::detail::Helpers::get().drivers += drivers;  // (run() counts them when they claim a device)

@@ -15,6 +15,9 @@ run() {
   rm -f $O/film_$tag.f32
 }
 run default "$@"
+run cb0 cost_batch=0 "$@"
+run cb20 cost_batch=1048576 "$@"
+run nof_cb0 flush_ms=100000 cost_batch=0 "$@"
 run w18 window=262144 "$@"
 run w20 window=1048576 "$@"
 run f1000 flush_ms=1000 "$@"
