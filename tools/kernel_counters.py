@@ -7,12 +7,15 @@ line's width x height x spp (one step at N = 1, which bench.py checks against th
 Usage: python tools/kernel_counters.py <outdir> <config>"""
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
 from pathlib import Path
 
 d, config = Path(sys.argv[1]), sys.argv[2]
 bench_args = sys.argv[3:]  # extra bench.py arguments of the passes (e.g. --grid-n 384: not the config's workload)
+if os.environ.get("VPT_LIB"):  # a variant library (an experiment): not the production kernel's counters
+    bench_args = bench_args + ["VPT_LIB=" + os.path.basename(os.environ["VPT_LIB"])]
 vals = defaultdict(list)
 ms = []
 samples = None
