@@ -70,8 +70,8 @@ namespace vpt_gpu {
 //     keep taking the jobs pushed after it);
 //   * token run-ahead is bounded: a push blocks while window_jobs pushed jobs have not started (the ring
 //     is at least twice the launch's lanes), so the provider's job counter (progress(), eta(), what
-//     stop_at_next_wave() cuts) leads the GPU by at most the ring, the cost_batch jobs held to be pushed
-//     costliest first, and the jobs in flight -- as the reference's workers each hold the token they render;
+//     stop_at_next_wave() cuts) leads the GPU by at most the ring, the push_batch jobs held for the next
+//     push, and the jobs in flight -- as the reference's workers each hold the token they render;
 //   * the film is progressive (main.cpp:101-132 shows it at 5 FPS): every flush_seconds the running feed
 //     is closed and a new one opened on the other stream and film (its lanes start as the old launch's
 //     drain frees the CUs); the old launch's last block copies its film to pinned memory and clears it,
@@ -83,10 +83,13 @@ using JobRuns = std::vector<std::pair<uint64_t, uint64_t>>;  // contiguous (jid_
 struct DrainOptions {
   double flush_seconds = 0.2;     // progressive film period (main.cpp's window draws at 5 FPS)
   uint64_t window_jobs = 1 << 19;  // pushed jobs not yet started on the GPU (C3: 16 waves, ~25 ms of work)
-  // Jobs held on the host and pushed costliest tile first (vpt_gpu_tile_costs), cost_batch at a time; 0:
-  // pushed as taken.  The provider hands jobs out in jid order, so a frame's last waves would start their
-  // densest tiles last and the launch would drain on them; samples never depend on the order.
-  uint64_t cost_batch = 1 << 18;
+  // Jobs taken are held and pushed push_batch at a time (0: every batch_jobs): when the host is the bound
+  // (C4: the GPU renders faster than one thread takes tokens) a large push publishes work in one step
+  // instead of lanes polling for each small one -- C4 drain 316 -> 222 ms (r04z).
+  uint64_t push_batch = 1 << 18;
+  // Held jobs pushed costliest tile first (vpt_gpu_tile_costs; the provider's jid order ends a frame on
+  // its densest tiles).  Measured slower with the progressive film (C3 496 vs 458 ms, r04z): off.
+  bool cost_order = false;
 };
 
 // Takes up to max_jobs tokens; on_token(token&) sees each before it is released.  Returns the count.
@@ -127,16 +130,16 @@ class FeedPipeline {
     }
     if (films_[1]) (void)vpt_gpu_film_free(ctx_, films_[1]);
   }
-  int init(uint64_t window, uint64_t cost_batch = 0) {
+  int init(uint64_t window, uint64_t push_batch = 0, bool cost_order = false) {
     window_ = window;
-    if (cost_batch) {  // cost classes per tile, before any feed holds the device (the cost pass syncs)
+    hold_ = push_batch;
+    if (push_batch && cost_order) {  // cost classes per tile, before any feed holds the device (the cost pass syncs)
       uint64_t T = 0, total = 0;
       if (int rc = vpt_gpu_job_space(ctx_, &T, &total)) return rc;
       std::vector<uint32_t> rank(T);
       if (int rc = vpt_gpu_tile_costs(ctx_, nullptr, rank.data())) return rc;
       cls_.assign(T, 0);
       for (uint64_t i = 0; i < T; ++i) cls_[rank[i]] = (uint8_t)((i * kClasses) / T);  // 0: costliest
-      hold_ = cost_batch;
     }
     for (void*& s : streams_)
       if (int rc = vpt_gpu_stream_create(ctx_, &s)) return rc;
@@ -155,10 +158,15 @@ class FeedPipeline {
       for (uint64_t i = 0; i < r.second; ++i) ids_.push_back(r.first + i);
     return vpt_gpu_feed_push(feeds_[cur_], ids_.data(), ids_.size());
   }
-  // Pushes the held jobs into the running feed, costliest tile class first (a counting sort; within a
-  // class in the order taken).
+  // Pushes the held jobs into the running feed: as taken, or (cost_order) costliest tile class first (a
+  // counting sort; within a class in the order taken).
   int release() {
     if (held_.empty()) return VPT_OK;
+    if (cls_.empty()) {
+      const int rc = vpt_gpu_feed_push(feeds_[cur_], held_.data(), held_.size());
+      held_.clear();
+      return rc;
+    }
     uint64_t start[kClasses + 1] = {};
     const uint64_t T = cls_.size();
     for (uint64_t j : held_) ++start[cls_[j % T] + 1];
@@ -225,7 +233,7 @@ class FeedPipeline {
   int cur_ = 0;
   std::vector<uint64_t> ids_;
   static constexpr int kClasses = 256;
-  std::vector<uint8_t> cls_;     // per tile: cost class (0 = costliest), with cost_batch
+  std::vector<uint8_t> cls_;     // per tile: cost class (0 = costliest), with cost_order
   std::vector<uint64_t> held_;   // jobs taken, not yet pushed
   uint64_t hold_ = 0;
   std::chrono::steady_clock::time_point last_switch_;
@@ -258,7 +266,7 @@ template <class Provider>
 int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs, const DrainOptions& opt = {},
           const JobRuns* first = nullptr, bool share = false) {
   FeedPipeline pipe(ctx);
-  if (int rc = pipe.init(opt.window_jobs, opt.cost_batch)) return rc;
+  if (int rc = pipe.init(opt.window_jobs, opt.push_batch, opt.cost_order)) return rc;
   if (first)
     if (int rc = pipe.push(*first)) return rc;
   detail::Helpers& hub = detail::Helpers::get();

@@ -174,7 +174,7 @@ int vpt_gpu_feed_collect(vpt_gpu_feed* f, float* host) {
 int main(int argc, char** argv) {
   std::map<std::string, long long> a{{"drivers", 1}, {"helpers", 0}, {"w", 72}, {"h", 40}, {"waves", 5},
                                      {"batch", 7}, {"flush_ms", 0}, {"window", 1024}, {"stop_after", 0},
-                                     {"cost_batch", 0}};
+                                     {"push_batch", 0}, {"cost_order", 0}};
   for (int i = 1; i < argc; ++i) {
     const char* eq = std::strchr(argv[i], '=');
     if (eq) a[std::string(argv[i], eq - argv[i])] = std::atoll(eq + 1);
@@ -202,7 +202,8 @@ int main(int argc, char** argv) {
   vpt_gpu::DrainOptions opt;
   opt.flush_seconds = (double)a["flush_ms"] / 1000.0;
   opt.window_jobs = (uint64_t)a["window"];
-  opt.cost_batch = (uint64_t)a["cost_batch"];
+  opt.push_batch = (uint64_t)a["push_batch"];
+  opt.cost_order = a["cost_order"] != 0;
   {
     std::lock_guard<std::mutex> l(vpt_gpu::detail::Helpers::get().mu);
     vpt_gpu::detail::Helpers::get().drivers += drivers;  // (run() counts them when they claim a device)

@@ -5,7 +5,7 @@
 //
 //   run_gpu_harness config=<scene.json> out=<film.f32> [mode=drain|run w= h= waves= threads= batch=
 //                   grid_n= dist= temperature=0|1 stop_after=<jobs> nvdb=<file.nvdb> gridbuf=<file>
-//                   tempbuf=<file> window= flush_ms= cost_batch= helpers= grid_blocks= sample_ms=]
+//                   tempbuf=<file> window= flush_ms= push_batch= cost_order= helpers= grid_blocks= sample_ms=]
 //
 // mode=drain (default): each thread owns a context made with vpt_gpu_create and calls
 //   vpt_gpu::drain(ctx, tp, film, batch).  The volume is nvdb= (vpt_grid_read_nvdb: "density", and
@@ -17,7 +17,7 @@
 //   to the RandomNumberGenerator.
 // The camera looks at the volume from (0, 0, -dist) unless dist=0 (then the scene file's camera).
 // stop_after: after that many jobs thread 0 calls tp.stop_at_next_wave() (tile_provider.cpp:107-110).
-// window / flush_ms / cost_batch: vpt_gpu::DrainOptions of mode=drain; helpers: threads that take tokens for the drain
+// window / flush_ms / push_batch / cost_order: vpt_gpu::DrainOptions of mode=drain; helpers: threads that take tokens for the drain
 // threads (vpt_gpu::help, as run()'s threads that find every GPU driven); grid_blocks: vpt_gpu_set_tuning's grid override.
 // sample_ms: a thread samples, every sample_ms, the jobs handed out and the samples in the host film (what
 // main.cpp's 5-FPS window shows: film_to_image(film) and provider.progress(), main.cpp:101-132) and prints
@@ -184,7 +184,8 @@ int main(int argc, char** argv) {
     float* fh = reinterpret_cast<float*>(film.data().data());
     vpt_gpu::DrainOptions opt;
     opt.window_jobs = (uint64_t)num("window", (long long)opt.window_jobs);
-    opt.cost_batch = (uint64_t)num("cost_batch", (long long)opt.cost_batch);
+    opt.push_batch = (uint64_t)num("push_batch", (long long)opt.push_batch);
+    opt.cost_order = num("cost_order", opt.cost_order ? 1 : 0) != 0;
     opt.flush_seconds = (double)num("flush_ms", (long long)(opt.flush_seconds * 1000)) / 1000.0;
     if (num("grid_blocks", 0) > 0)
       for (auto* c : ctx)

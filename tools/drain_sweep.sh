@@ -15,9 +15,9 @@ run() {
   rm -f $O/film_$tag.f32
 }
 run default "$@"
-run cb0 cost_batch=0 "$@"
-run cb20 cost_batch=1048576 "$@"
-run nof_cb0 flush_ms=100000 cost_batch=0 "$@"
+run pb0 push_batch=0 "$@"
+run cost cost_order=1 "$@"
+run nof_pb0 flush_ms=100000 push_batch=0 "$@"
 run w18 window=262144 "$@"
 run w20 window=1048576 "$@"
 run f1000 flush_ms=1000 "$@"
@@ -29,6 +29,8 @@ grep "^sample" $O/s50.log | head -40
 run h3 helpers=3 "$@"
 timeout -k 10 120 $H config=volume_path_tracer_amd/scenes/fire.json out=$O/film_c4.f32 w=1920 h=1080 waves=256 grid_n=512 \
   threads=1 batch=4096 temperature=1 > $O/c4_h0.log 2>&1 && echo "c4 helpers=0 $(grep render_ms $O/c4_h0.log)"
+timeout -k 10 120 $H config=volume_path_tracer_amd/scenes/fire.json out=$O/film_c4.f32 w=1920 h=1080 waves=256 grid_n=512 \
+  threads=1 batch=4096 temperature=1 push_batch=0 > $O/c4_pb0.log 2>&1 && echo "c4 push_batch=0 $(grep render_ms $O/c4_pb0.log)"
 timeout -k 10 120 $H config=volume_path_tracer_amd/scenes/fire.json out=$O/film_c4.f32 w=1920 h=1080 waves=256 grid_n=512 \
   threads=1 batch=4096 temperature=1 helpers=3 > $O/c4_h3.log 2>&1 && echo "c4 helpers=3 $(grep render_ms $O/c4_h3.log)"
 rm -f $O/film_c4.f32
