@@ -82,7 +82,7 @@ using JobRuns = std::vector<std::pair<uint64_t, uint64_t>>;  // contiguous (jid_
 
 struct DrainOptions {
   double flush_seconds = 0.2;     // progressive film period (main.cpp's window draws at 5 FPS)
-  uint64_t window_jobs = 1 << 19;  // pushed jobs not yet started on the GPU (C3: 16 waves, ~25 ms of work)
+  uint64_t window_jobs = 1 << 19;  // pushed jobs not yet started (rounded up to >= 2x the lanes: C3 2^20)
   // Jobs taken are held and pushed push_batch at a time (0: every batch_jobs): when the host is the bound
   // (C4: the GPU renders faster than one thread takes tokens) a large push publishes work in one step
   // instead of lanes polling for each small one -- C4 drain 316 -> 222 ms (r04z).
