@@ -1,5 +1,6 @@
 set -u
-# Live-path compaction (VPT_EXP_COMPACT) measured: its production parity, then C3 frames of the production
+# Live-path compaction (tools/experiments/r04_compaction.patch applied, built with -DVPT_EXP_COMPACT=8 / 32 as
+# libvpt_cmp8.so / libvpt_cmp32.so, and a 5-wave production build libvpt_w5.so) measured: its production parity, then C3 frames of the production
 # binary (7 waves), the same kernel at 5 waves (the compaction build's occupancy) and compaction every 8 / 32
 # outer iterations at 5 waves; then SQ / memory counters of the 5-wave baseline and compaction every 8.
 L=$PWD/volume_path_tracer_amd/lib

@@ -172,22 +172,11 @@ struct KernelEnvT {
   // The lane's cold state: its LDS slot, or (RegCold, the latency kernel) a kernel local the compiler
   // keeps in VGPRs.
   LaneCold* reg_cold;
-#ifdef VPT_EXP_COMPACT
-  // experiment (tools/experiments/r04_compaction.patch's measurement): paths move between the threads of a
-  // block, so a path's LDS slot travels with it
-  uint4* xbuf;         // [block][kBlockThreads][kXWords / 4]: the exchange of the paths' hot state
-  int32_t cold_slot;
-#endif
   __device__ __forceinline__ LaneCold& cold() {
     if constexpr (RegCold)
       return *reg_cold;
-#ifdef VPT_EXP_COMPACT
-    else
-      return g_lane_cold[cold_slot];
-#else
     else
       return g_lane_cold[threadIdx.x];
-#endif
   }
   const float* bb_lds;  // the temperature kernel's LDS copy of S.bb's first kBbLdsRows rows
   __device__ __forceinline__ const double (*logf_table() const)[2] { return g_logf_tab; }
@@ -310,94 +299,6 @@ struct KernelEnvT {
 };
 using KernelEnv = KernelEnvT<false>;
 
-#ifdef VPT_EXP_COMPACT
-// Live-path compaction across the 4 wavefronts of a block (north_star's "ballot/prefix-sum to compact live
-// rays"; measured and not kept): every VPT_EXP_COMPACT outer iterations the block's waves meet at
-// a barrier, count their walking / other live / done paths (ballots, LDS), and move every path's hot state
-// (the Lane registers and its LDS cold-slot index) through a global exchange buffer so that the walking
-// paths fill the block's first wavefronts.  A path's operations and draws never change (bit-exact); only
-// which thread runs it.  The block ends when no live path is left.
-constexpr int kXWords = 36;  // the density-only production kernel's hot state (pack_hot) + the cold slot
-__device__ __forceinline__ uint32_t fb(float f) { return __builtin_bit_cast(uint32_t, f); }
-__device__ __forceinline__ float bf(uint32_t u) { return __builtin_bit_cast(float, u); }
-// The Lane fields the density-only production kernel uses (jid_local, n_events: Debug; temp_cell: HasTemp).
-__device__ __forceinline__ void pack_hot(const Lane& ln, int32_t slot, uint32_t x[kXWords]) {
-  int n = 0;
-  x[n++] = (uint32_t)ln.state; x[n++] = (uint32_t)ln.sm; x[n++] = (uint32_t)ln.shadow;
-  x[n++] = (uint32_t)ln.rng; x[n++] = (uint32_t)(ln.rng >> 32);
-  for (int i = 0; i < 3; ++i) { x[n++] = fb(ln.e[i]); x[n++] = fb(ln.d[i]); x[n++] = fb(ln.nxt[i]);
-                                x[n++] = (uint32_t)ln.vox[i]; x[n++] = fb(ln.finc[i]); x[n++] = (uint32_t)ln.vinc[i]; }
-  x[n++] = fb(ln.scale); x[n++] = fb(ln.rscale); x[n++] = fb(ln.maj); x[n++] = (uint32_t)ln.dim;
-  x[n++] = fb(ln.Tn); x[n++] = fb(ln.T1); x[n++] = ln.pw; x[n++] = fb(ln.s_t0); x[n++] = fb(ln.s_t1);
-  x[n++] = fb(ln.s_dmaj); x[n++] = ln.n_dda; x[n++] = (uint32_t)slot;
-  while (n < kXWords) x[n++] = 0;
-}
-__device__ __forceinline__ int32_t unpack_hot(Lane& ln, const uint32_t x[kXWords]) {
-  int n = 0;
-  ln.state = (int32_t)x[n++]; ln.sm = (int32_t)x[n++]; ln.shadow = (int32_t)x[n++];
-  ln.rng = (uint64_t)x[n] | ((uint64_t)x[n + 1] << 32); n += 2;
-  for (int i = 0; i < 3; ++i) { ln.e[i] = bf(x[n++]); ln.d[i] = bf(x[n++]); ln.nxt[i] = bf(x[n++]);
-                                ln.vox[i] = (int32_t)x[n++]; ln.finc[i] = bf(x[n++]); ln.vinc[i] = (int32_t)x[n++]; }
-  ln.scale = bf(x[n++]); ln.rscale = bf(x[n++]); ln.maj = bf(x[n++]); ln.dim = (int32_t)x[n++];
-  ln.Tn = bf(x[n++]); ln.T1 = bf(x[n++]); ln.pw = x[n++]; ln.s_t0 = bf(x[n++]); ln.s_t1 = bf(x[n++]);
-  ln.s_dmaj = bf(x[n++]); ln.n_dda = x[n++];
-  return (int32_t)x[n];
-}
-template <bool Runs, class Env>
-__device__ __forceinline__ void compact_loop(ScenePtr sp, Lane& ln, Env& env) {
-  __shared__ int32_t cnt[12];
-  env.cold_slot = (int32_t)threadIdx.x;
-  uint4* xb = env.xbuf + (size_t)blockIdx.x * kBlockThreads * (kXWords / 4);
-  const uint32_t w = threadIdx.x / 64, l = threadIdx.x % 64;
-  const uint64_t below = (l == 0) ? 0ULL : (~0ULL >> (64 - l));
-  for (uint32_t it = 1;; ++it) {
-    if (ln.state != ST_DONE) lane_iteration<false, false, Runs>(sp, ln, env);
-    if (it % VPT_EXP_COMPACT) continue;
-    const bool walking = ln.state == ST_SAMPLE && ln.sm != SM_EVAL, live = ln.state != ST_DONE;
-    const uint64_t mw = __builtin_amdgcn_ballot_w64(walking), ml = __builtin_amdgcn_ballot_w64(live && !walking);
-    if (l == 0) {
-      cnt[w] = __popcll(mw);
-      cnt[4 + w] = __popcll(ml);
-    }
-    __syncthreads();
-    int32_t nw = 0, no = 0, pw = 0, po = 0, pd = 0;
-#pragma unroll
-    for (uint32_t v = 0; v < 4; ++v) {
-      nw += cnt[v];
-      no += cnt[4 + v];
-      if (v < w) {
-        pw += cnt[v];
-        po += cnt[4 + v];
-        pd += 64 - cnt[v] - cnt[4 + v];
-      }
-    }
-    if (nw + no == 0) break;  // uniform over the block
-    int32_t dest;
-    if (walking)
-      dest = pw + __popcll(mw & below);
-    else if (live)
-      dest = nw + po + __popcll(ml & below);
-    else
-      dest = nw + no + pd + __popcll(~(mw | ml) & below);
-    uint32_t words[kXWords];
-    pack_hot(ln, env.cold_slot, words);
-#pragma unroll
-    for (int q = 0; q < kXWords / 4; ++q)
-      xb[(size_t)q * kBlockThreads + dest] = make_uint4(words[4 * q], words[4 * q + 1], words[4 * q + 2], words[4 * q + 3]);
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < kXWords / 4; ++q) {
-      const uint4 v = xb[(size_t)q * kBlockThreads + threadIdx.x];
-      words[4 * q] = v.x;
-      words[4 * q + 1] = v.y;
-      words[4 * q + 2] = v.z;
-      words[4 * q + 3] = v.w;
-    }
-    env.cold_slot = unpack_hot(ln, words);
-    __syncthreads();  // cnt is rewritten at the next meeting
-  }
-}
-#endif
 
 // counters[] order = vpt_counters field order
 // A staged feed's retirement, run by the launch's last block once every block has ended: the film is
@@ -449,11 +350,6 @@ __global__ __launch_bounds__(kBlockThreads, Lat ? VPT_WAVES_LAT : (Debug ? VPT_W
   if constexpr (Lat) env.reg_cold = &lc_reg;
   cold_init(env.cold());
   const ScenePtr sp = (ScenePtr)scene;
-#ifdef VPT_EXP_COMPACT
-  if constexpr (!Debug && !Lat && !HasTemp) {
-    compact_loop<Runs>(sp, ln, env);
-  } else
-#endif
   while (ln.state != ST_DONE) {
     lane_iteration<HasTemp, Debug, Runs>(sp, ln, env);
     // Feed mode: a wavefront whose every live lane waits for the host to publish its item sleeps between
@@ -705,9 +601,6 @@ struct vpt_gpu_ctx {
   // that launch -- i.e. until its lanes give up -- so a feed's memory is allocated once and freed with
   // the context.
   std::vector<vpt_gpu_feed*> feed_pool;
-#ifdef VPT_EXP_COMPACT
-  uint4* xbuf = nullptr;           // the compaction experiment's exchange buffer (grid_blocks blocks)
-#endif
   int lat_mode = -1;               // latency kernel: -1 auto (launches of <= lat_per_cu blocks per CU), 0 off, 1 on
   int lat_ungated = 1;             // its partly filled launches read the latency gates (1) or the context's (0)
   int lat_per_cu = 1;              // resident blocks per CU of the latency kernel
@@ -955,11 +848,6 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.feed_mask = feed ? feed->mask : 0;
   env.feed_error = feed ? feed->error : nullptr;
   env.feed_staged = feed ? feed->staged : nullptr;
-#ifdef VPT_EXP_COMPACT
-  if (!ctx->xbuf)
-    VPT_HIP(hipMalloc((void**)&ctx->xbuf, (size_t)ctx->grid_blocks * vpt::kBlockThreads * vpt::kXWords * 4));
-  env.xbuf = ctx->xbuf;
-#endif
   env.event_count = ctx->job_counter + 2 * slot + 1;
   env.event_cap = event_cap;
   if (slot_out) *slot_out = slot;
