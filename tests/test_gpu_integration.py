@@ -223,6 +223,24 @@ def test_library_before_torch_keeps_one_hip_runtime():
 
 
 @pytest.mark.gpu
+@pytest.mark.spawns
+def test_progressive_film_rises_during_the_drain(tmp_path):
+    """What main.cpp's 5-FPS window shows (main.cpp:101-132): while the drain renders a full C3 frame
+    (1920x1080, 256 waves, 512^3 stand-in), a thread samples the host film every 10 ms.  With a feed switch
+    every 50 ms the film's sample count rises monotonically through several intermediate values, never ahead
+    of the jobs handed out, and ends with every pixel at 256 samples."""
+    w, h, waves = 1920, 1080, 256
+    film, log = _harness(tmp_path, "wdas_cloud.json", w, h, waves, 1, 4096, grid_n=512, flush_ms=50, sample_ms=10)
+    samples = [tuple(float(v) for v in line.split()[1:4]) for line in log.splitlines() if line.startswith("sample ")]
+    assert len(samples) >= 10, log[-2000:]
+    in_film = [s[2] for s in samples]
+    assert all(b >= a for a, b in zip(in_film, in_film[1:])), in_film
+    assert all(s[2] <= s[1] + 1e-6 for s in samples), samples  # the film never shows jobs not yet handed out
+    assert len({v for v in in_film if 0.0 < v < waves}) >= 3, in_film
+    assert (film[..., 3] == waves).all()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["full_grid", "small_grid", "staged_small_grid"])
 def test_feed_renders_pushed_jobs_in_any_order(mode):
     """vpt_gpu_feed_*: job ids pushed out of order and with gaps render the oracle's samples; the close (or,
