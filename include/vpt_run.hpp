@@ -71,7 +71,7 @@ namespace vpt_gpu {
 //   * token run-ahead is bounded: a push blocks while window_jobs pushed jobs have not started (the ring
 //     is at least twice the launch's lanes), so the provider's job counter (progress(), eta(), what
 //     stop_at_next_wave() cuts) leads the GPU by at most the ring, the push_batch jobs held for the next
-//     push, and the jobs in flight -- as the reference's workers each hold the token they render;
+//     push (none by default), and the jobs in flight -- as the reference's workers each hold the token they render;
 //   * the film is progressive (main.cpp:101-132 shows it at 5 FPS): every flush_seconds the running feed
 //     is closed and a new one opened on the other stream and film (its lanes start as the old launch's
 //     drain frees the CUs); the old launch's last block copies its film to pinned memory and clears it,
@@ -83,12 +83,11 @@ using JobRuns = std::vector<std::pair<uint64_t, uint64_t>>;  // contiguous (jid_
 struct DrainOptions {
   double flush_seconds = 0.2;     // progressive film period (main.cpp's window draws at 5 FPS)
   uint64_t window_jobs = 1 << 19;  // pushed jobs not yet started (rounded up to >= 2x the lanes: C3 2^20)
-  // Jobs taken are held and pushed push_batch at a time (0: every batch_jobs): when the host is the bound
-  // (C4: the GPU renders faster than one thread takes tokens) a large push publishes work in one step
-  // instead of lanes polling for each small one -- C4 drain 316 -> 222 ms (r04z).
-  uint64_t push_batch = 1 << 18;
+  // Jobs taken are held and pushed push_batch at a time (0: every batch_jobs).  Measured without effect
+  // (r04i: C3 449.0 vs 450.6 ms, C4 193.9 vs 196.0 ms for 0 vs 2^18), so off: it only adds run-ahead.
+  uint64_t push_batch = 0;
   // Held jobs pushed costliest tile first (vpt_gpu_tile_costs; the provider's jid order ends a frame on
-  // its densest tiles).  Measured slower with the progressive film (C3 496 vs 458 ms, r04z): off.
+  // its densest tiles; needs push_batch).  Measured without gain (r04z / r04i: C3 457-496 vs 449-458 ms): off.
   bool cost_order = false;
 };
 
