@@ -370,8 +370,9 @@ def main():
     ap.add_argument("--rng-mode", choices=["reference", "pixel"], default="reference",
                     help="pixel = throughput mode (per-pixel streams; not the reference's samples)")
     ap.add_argument("--latency-kernel", choices=["auto", "off", "on", "gated"], default="auto",
-                    help="the latency kernel (cold lane state in VGPRs): auto = for latency-bound launches (C1); "
-                         "off / on force it (A/B runs); gated = forced, with the context's gates")
+                    help="the latency kernel (cold lane state in VGPRs): auto = latency-bound launches (C1, latency "
+                         "gates) and partly filled ones (C2, small shares; the context's gates); off never; on / gated "
+                         "force it with the latency / the context's gates on partly filled launches (A/B runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work (3 runs)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
@@ -408,7 +409,7 @@ def main():
     from volume_path_tracer_amd import capi as _capi
     lat_info = None
     if hasattr(_capi.lib(), "vpt_gpu_set_latency_kernel"):  # (A/B runs against older library builds lack it)
-        mode, ungated = {"auto": (-1, 1), "off": (0, 1), "on": (1, 1), "gated": (1, 0)}[args.latency_kernel]
+        mode, ungated = {"auto": (-1, -1), "off": (0, -1), "on": (1, 1), "gated": (1, 0)}[args.latency_kernel]
         it.set_latency_kernel(mode, ungated)
         lat_info = it.latency_kernel_info()
     log(f"[rank {rank}] grids ready in {time.time() - t0:.1f}s: {dens.leaf_count} leaves, "

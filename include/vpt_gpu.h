@@ -397,12 +397,13 @@ int vpt_gpu_set_tuning(vpt_gpu_ctx* ctx, int gate_min, int gate_idle, int grid_b
 int vpt_gpu_set_latency_tuning(vpt_gpu_ctx* ctx, int wave_lanes, int gate_min, int gate_idle, int gate_eval,
                                int gate_walk);
 /* The latency kernel: the same state machine with the lane's cold state in VGPRs instead of LDS and a
- * larger register budget (4 waves per SIMD instead of 7).  mode -1 (default): used for latency-bound
- * launches (C1: 20.7-21.2 -> 19.2-19.5 ms); partly filled ones (C2, a GPU's small share of a frame) measured
- * slower with it and keep the throughput kernel; 0: never; 1: always (tests, A/B).  ungated 1 (default):
- * forced onto a partly filled launch it uses the latency gates (every block runs for one waiting lane,
- * vpt_gpu_set_latency_tuning); 0: the context's gates; -1: keep.  Samples never depend on it.  Takes
- * effect at the next launch. */
+ * larger register budget (4-5 waves per SIMD instead of 7), for launches that occupy at most that many
+ * anyway.  mode -1 (default): latency-bound launches (C1: 20.7-21.2 -> 19.2-19.7 ms) and partly filled ones
+ * whose grid rule gives <= its resident blocks per CU (C2: 100-101 -> 95.7-96.6 ms; a GPU's small share of a
+ * frame); 0: never; 1: always (tests, A/B).  ungated 0 (default): partly filled launches on it use the
+ * context's gates; 1: the latency gates (every block runs for one waiting lane, vpt_gpu_set_latency_tuning;
+ * measured slower there: C2 109 ms); -1: keep.  Latency-bound launches always use the latency gates.
+ * Samples never depend on it.  Takes effect at the next launch. */
 int vpt_gpu_set_latency_kernel(vpt_gpu_ctx* ctx, int mode, int ungated);
 /* The mode and the latency kernel's resident blocks per CU. */
 int vpt_gpu_latency_kernel_info(const vpt_gpu_ctx* ctx, int* mode, int* resident_blocks_per_cu);

@@ -10,7 +10,7 @@ therefore gives a bit-exact comparison with the oracle's per-sample records, for
                                on the 128^3 cube and on a 64^3 cloud)
   <HasTemp=true,  Runs=false>  C4 (fire: blackbody emission from the temperature grid)
 each as the throughput kernel and as the latency kernel (Lat: the lane's cold state in VGPRs; latency-bound
-launches such as C1 select it), forced with vpt_gpu_set_latency_kernel.
+and partly filled launches -- C1, C2, small shares -- select it), forced with vpt_gpu_set_latency_kernel.
 
 The production kernel's own event counters (samples, HDDA steps, density and temperature stencil
 refreshes -- the terms of the algorithmic bytes) must equal the oracle's.

@@ -602,7 +602,7 @@ struct vpt_gpu_ctx {
   // the context.
   std::vector<vpt_gpu_feed*> feed_pool;
   int lat_mode = -1;               // latency kernel: -1 auto (launches of <= lat_per_cu blocks per CU), 0 off, 1 on
-  int lat_ungated = 1;             // its partly filled launches read the latency gates (1) or the context's (0)
+  int lat_ungated = 0;             // its partly filled launches read the latency gates (1) or the context's (0)
   int lat_per_cu = 1;              // resident blocks per CU of the latency kernel
 };
 
@@ -813,13 +813,16 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
 #else
   const bool temp = ctx->scene.has_temperature != 0, dbg = records != nullptr || events != nullptr;
 #endif
-  // The latency kernel (lane cold state in VGPRs, VPT_WAVES_LAT waves per SIMD) for latency-bound launches,
-  // on its whole grid: C1 20.7-21.2 -> 19.2-19.5 ms (r04e).  Partly filled launches keep the throughput
-  // kernel: with it C2 100.1-101.2 ms vs 109.5-109.8, C3 shares of 16 / 32 waves 51.6 / 65.9-66.4 vs
-  // 56.1-56.4 / 75.5-76.1 (r04e, profiles/r04e_lat_ab.txt).  lat_mode 1 forces it.  Same jobs, same samples.
+  // The latency kernel (lane cold state in VGPRs, VPT_WAVES_LAT waves per SIMD) for launches that fill at
+  // most its resident grid anyway: latency-bound ones on its whole grid with the latency gates (C1 20.7-21.2
+  // -> 19.2-19.7 ms, r04e / r04z), and partly filled ones whose rule above gives <= lat_per_cu blocks per CU
+  // with the context's gates (C2 100.0-101.3 -> 95.7-96.6 ms, the 8-GPU C3 share of 32 waves 66.1-66.6 ->
+  // 65.1-65.3; with the latency gates they ran slower, 108.3-109.8 / 75.2-76.1 ms: its one-lane blocks add
+  // wave instructions to launches that are issue-bound; r04k, profiles/r04k_lat_gated_ab.txt).  lat_mode 1
+  // forces it.  Same jobs, same samples.
   const uint64_t lat_blocks = cus * (uint64_t)ctx->lat_per_cu;
   const bool use_lat = !dbg && !feed && ctx->lat_mode != 0 &&
-                       (ctx->lat_mode == 1 || (!ctx->grid_user && latency));
+                       (ctx->lat_mode == 1 || (!ctx->grid_user && (latency || blocks <= lat_blocks)));
   if (use_lat) blocks = (uint32_t)std::min<uint64_t>(latency ? lat_blocks : blocks, lat_blocks);
   const uint64_t T = ctx->scene.T;
   if (!feed && ctx->order_mode != VPT_ORDER_JID && jid_begin % T == 0 && jid_count % T == 0 && jid_count < (1ULL << 32)) {

@@ -193,9 +193,9 @@ class Integrator:
         capi.check(capi.lib().vpt_gpu_set_run_skipping(self.h, int(mode)), "vpt_gpu_set_run_skipping")
 
     def set_latency_kernel(self, mode: int, ungated: int = -1) -> None:
-        """The latency kernel (lane cold state in VGPRs, 4-5 waves per SIMD): -1 auto (latency-bound launches:
-        C1), 0 never, 1 always; `ungated` 1 / 0: partly filled launches forced onto it use the latency gates /
-        the context's (-1 keeps).  Samples never depend on it."""
+        """The latency kernel (lane cold state in VGPRs, 4-5 waves per SIMD): -1 auto (latency-bound launches,
+        C1, and partly filled ones, C2 and small shares), 0 never, 1 always; `ungated` 1 / 0: partly filled
+        launches on it use the latency gates / the context's (-1 keeps; default 0).  Samples never depend on it."""
         capi.check(capi.lib().vpt_gpu_set_latency_kernel(self.h, int(mode), int(ungated)), "vpt_gpu_set_latency_kernel")
 
     def latency_kernel_info(self) -> dict:
