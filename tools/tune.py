@@ -36,6 +36,10 @@ PRESETS = {
     "small-launch": [["--config", "c2", "--spp", "64", "--gates", "6:8:36:4", "--blocks", "512,640,768,1024,1280", "--reps", "2"],
                      ["--config", "c1", "--spp", "4", "--gates", "6:8:36:4", "--blocks", "1792",
                       "--lat", "0:1:65:1:1,0:1:65:2:1,0:1:65:1:2,0:1:65:4:1,0:1:65:1:4,0:2:65:1:1", "--reps", "3"]],
+    # C2 on the latency kernel with the context's gates (r04): gates and blocks per CU
+    "c2-lat": [["--config", "c2", "--spp", "64", "--lat-kernel", "1", "--lat-ungated", "0", "--blocks", "512,768,1024",
+                "--gates", "6:8:36:4,4:8:36:4,8:8:36:4,6:4:36:4,6:16:36:4,6:8:24:4,6:8:48:4,6:8:36:2,6:8:36:8", "--reps", "3"],
+               ["--config", "c2", "--spp", "64", "--lat-kernel", "0", "--blocks", "512", "--gates", "6:8:36:4", "--reps", "3"]],
     # the full-occupancy gates of the C3 / C4 frames
     "gates": [["--config", c, "--spp", "32", "--gates", "6:8:36:4,4:8:36:4,8:8:36:4,6:12:36:4,6:8:32:4,6:8:40:4,6:8:36:2,6:8:36:8",
                "--reps", "2"] for c in ("c3", "c4")],
@@ -51,6 +55,8 @@ def parser():
     ap.add_argument("--blocks", default="0")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--lat", default="", help="latency-launch knobs wave_lanes:gate_min:gate_idle:gate_eval:gate_walk, comma-separated")
+    ap.add_argument("--lat-kernel", type=int, default=-1, help="vpt_gpu_set_latency_kernel mode (-1 auto, 0 off, 1 on)")
+    ap.add_argument("--lat-ungated", type=int, default=-1, help="its ungated flag (-1 keep)")
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--rng-mode", default="reference")
     ap.add_argument("--order", type=int, default=-1, help="job order mode (-1: library default)")
@@ -72,6 +78,7 @@ def sweep(a):
     tg = SynthGrid(2, wl.grid_n) if wl.temperature else None
     it = Integrator(wl.cfg, dg.grid(copy=False), tg.grid(copy=False) if tg else None)
     base_blocks = it.launch_info()[0]
+    it.set_latency_kernel(a.lat_kernel, a.lat_ungated)
     if a.rng_mode == "pixel":
         from volume_path_tracer_amd import capi
         it.set_rng_mode(capi.VPT_RNG_PIXEL)
@@ -110,7 +117,7 @@ def sweep(a):
             if a.profile:
                 print(json.dumps({"gate": g, "profile": it.profile(reset=True)}), flush=True)
             print(json.dumps({"lib": os.environ.get("VPT_LIB", "default"), "config": a.config, "order": a.order, "tail": a.tail, "perm": a.perm,
-                              "gate": g, "lat": lat, "blocks": b or base_blocks, "spp": a.spp, "ms": round(best * 1e3, 2),
+                              "gate": g, "lat": lat, "lat_kernel": [a.lat_kernel, a.lat_ungated], "blocks": b or base_blocks, "spp": a.spp, "ms": round(best * 1e3, 2),
                               "Msps": round(wl.cfg.width * wl.cfg.height * a.spp / best / 1e6, 2)}), flush=True)
     del it
 
