@@ -127,6 +127,49 @@ def cpu_baseline(wl, dens, temp, budget_s: float = 15.0, runs: int = 3):
                                   "kind": "linear extrapolation of per_thread, not a measurement"}}
 
 
+HARNESS = ROOT / "tests" / "native" / "build" / "run_gpu_harness"
+
+
+def dropin_frames(wl, frames: int = 3, timeout_s: int = 300):
+    """The reference-API path, timed: main.cpp:46-87 made headless -- the restated
+    TileProvider and one worker thread calling vpt_gpu::drain (include/vpt_run.hpp: one staged feed, the
+    pusher and film threads, the 0.2-s progressive film) -- through tests/native/run_gpu_harness, on this
+    config's frame: `frames` frames on one context (setup -- grid upload, tile costs, the feed's memory --
+    outside the timed drains, as the harness and run_checked do it).  Then the provider alone (mode=tokens: one
+    thread taking every token of the frame), the drop-in's host-side floor.  A child process, started before
+    this process touches the GPU.  None for configs the harness does not run (C2's constant cube, C5)."""
+    import subprocess
+    import tempfile
+
+    if wl.density_kind != 1 or wl.name not in ("c1", "c3", "c4") or not HARNESS.exists():
+        return None
+    scene = ROOT / "volume_path_tracer_amd" / "scenes" / ("fire.json" if wl.temperature else "wdas_cloud.json")
+    W, H, spp = wl.cfg.width, wl.cfg.height, wl.spp
+    base = [str(HARNESS), f"config={scene}", f"w={W}", f"h={H}", f"waves={spp}", f"grid_n={wl.grid_n}", "threads=1",
+            "batch=4096", f"temperature={1 if wl.temperature else 0}"]
+    with tempfile.TemporaryDirectory() as tmp:
+        r = subprocess.run(base + [f"out={tmp}/film.f32", f"frames={frames}"], capture_output=True, text=True,
+                           timeout=timeout_s)
+        if r.returncode != 0:
+            log(f"bench: drop-in harness failed ({r.returncode}): {r.stderr[-500:]}")
+            return {"error": r.returncode}
+        film = __import__("numpy").fromfile(f"{tmp}/film.f32", "float32").reshape(H, W, 4)
+        counts_ok = bool((film[..., 3] == spp).all())
+        t = subprocess.run(base + [f"out={tmp}/x", "mode=tokens"], capture_output=True, text=True, timeout=60)
+    ms = [float(l.split()[-1]) for l in r.stdout.splitlines() if "render_ms" in l]
+    med = sorted(ms)[len(ms) // 2]
+    rec = {"path": "vpt_gpu::drain (include/vpt_run.hpp) behind the restated TileProvider, main.cpp:46-87 headless "
+                   "(tests/native/run_gpu_harness), 1 worker thread, 0.2-s progressive film",
+           "workload": f"{wl.name}: {W}x{H}, {spp} spp", "frames": len(ms), "ms_frames": ms, "ms_per_frame": med,
+           "value": round(W * H * spp / (med / 1e3) / 1e6, 3), "unit": "Msamples/s", "film_counts_exact": counts_ok}
+    for line in t.stdout.splitlines():
+        if "tokens_ms" in line:  # "tokens_ms 125.5, 8294400 tokens, 66.1 M tokens/s, 1 threads"
+            parts = line.replace(",", "").split()
+            rec["provider_alone_ms"] = float(parts[parts.index("tokens_ms") + 1])
+            rec["provider_alone_Mtokens_per_s"] = float(parts[parts.index("M") - 1])
+    return rec
+
+
 def spawn_ranks(args) -> int:
     """--gpus N without torchrun's environment: start N fresh ranks (this process has not touched the
     GPU) through torch.distributed.run on 127.0.0.1, and return their exit code."""
@@ -374,6 +417,8 @@ def main():
                          "gates) and partly filled ones (C2, small shares; the context's gates); off never; on / gated "
                          "force it with the latency / the context's gates on partly filled launches (A/B runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the reference-API (drop-in) frame timing")
+    ap.add_argument("--dropin-frames", type=int, default=3)
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work (3 runs)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI)")
@@ -390,6 +435,15 @@ def main():
 
     import torch
     import torch.distributed as dist
+
+    dropin = None
+    if world == 1 and not args.no_dropin and args.rng_mode == "reference" and args.spp is None and args.grid_n is None:
+        # the drop-in runs in a child process, before this one touches the GPU
+        from volume_path_tracer_amd.scenes import workload as _workload
+
+        t0 = time.time()
+        dropin = dropin_frames(_workload(args.config), args.dropin_frames)
+        log(f"bench: drop-in frames in {time.time() - t0:.1f}s: {dropin}")
 
     rank, world, dev, sdev = init_rank(args)
 
@@ -486,6 +540,10 @@ def main():
         }
         if strong is not None:
             out["scaling_strong"] = strong
+        if dropin is not None:
+            if "ms_per_frame" in dropin:
+                dropin["vs_one_launch"] = round(out["ms_per_step"] / dropin["ms_per_frame"], 4)
+            out["dropin"] = dropin
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(wl, dens, temp, args.cpu_budget)
             out["cpu_baseline"] = cb

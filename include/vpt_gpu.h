@@ -353,23 +353,40 @@ int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* ctx, float* film_device, float* film
  * is closed -- a second feed opened meanwhile starts as the first one's lanes leave -- so push to a feed
  * only after the feeds opened before it have been closed; and a call that waits for the whole device
  * (hipDeviceSynchronize, and hipFree / hipHostMalloc / hipHostFree may) waits for an open feed's lanes to
- * give up: wait for streams instead.  A destroyed feed's memory is kept by the context for the next
- * vpt_gpu_feed_open (freed by vpt_gpu_destroy).  Feeds use a host-pinned ring (8 bytes per
- * window slot) and run the reference RNG mode. */
+ * give up: wait for streams instead.  The context's own calls that wait for its launches (vpt_gpu_sync,
+ * vpt_gpu_film_clear, vpt_gpu_film_add_to_host, vpt_gpu_counters, vpt_gpu_profile, vpt_gpu_set_tuning,
+ * vpt_gpu_set_latency_tuning, vpt_gpu_set_rng_mode, vpt_gpu_set_tile_costs, vpt_gpu_set_job_permutation,
+ * and vpt_gpu_tile_costs before its first cost pass) return VPT_E_STATE while a feed of the context is
+ * launched and not closed, instead of waiting 30 s for its lanes to give up.  A destroyed feed's memory is
+ * kept by the context for the next vpt_gpu_feed_open (freed by vpt_gpu_destroy).  Feeds use a host-pinned
+ * ring (8 bytes per window slot) and run the reference RNG mode. */
 typedef struct vpt_gpu_feed vpt_gpu_feed;
 int vpt_gpu_feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t window, vpt_gpu_feed** out);
 int vpt_gpu_feed_push(vpt_gpu_feed* feed, const uint64_t* jids, uint64_t n);
 int vpt_gpu_feed_close(vpt_gpu_feed* feed);
 int vpt_gpu_feed_query(vpt_gpu_feed* feed, int* done, uint64_t* pushed);
 int vpt_gpu_feed_destroy(vpt_gpu_feed* feed);
-/* A staged feed: its launch's last block copies the film into a pinned host buffer of the feed and clears
- * it, so retiring the feed needs no GPU work queued after the launch (work queued while another feed is
- * open may wait for the CUs that feed's launch holds).  vpt_gpu_feed_collect closes if needed, waits, adds
- * the copy and the pushed jobs' sample counts into film_host (film_count floats; the caller serialises
- * writers of film_host) and frees the feed like destroy. */
+/* Jobs pushed and not yet taken by a lane (an estimate: the lanes report every 1 024th job they take;
+ * before the launch, every pushed job).  Cheap: one read of the pinned block. */
+int vpt_gpu_feed_backlog(vpt_gpu_feed* feed, uint64_t* backlog);
+/* A staged feed renders into film_device (NULL = the context's own film), which must be zero, on hip_stream
+ * (NULL = a stream of the feed's own), and counts the jobs it completes per tile; its film reaches the host through the copy engines, which run beside a launch
+ * that holds every CU (r05), so nothing in its life waits for CUs another feed's launch holds.
+ *   vpt_gpu_feed_snapshot -- at any time, also while the launch runs: adds into film_host (film_count
+ *     floats, the reference's [H][W][4] layout) what the launch has rendered since the previous snapshot --
+ *     the completed jobs' sample counts and the film's radiance as copied (~2 ms for a 1080p film).  A
+ *     progressive film (main.cpp:101-132's 5-FPS window): every snapshot's additions telescope to the final
+ *     film.  The caller serialises writers of film_host.
+ *   vpt_gpu_feed_collect -- closes if needed, waits for the launch, adds the rest (exact: the whole film
+ *     then equals the launch's), clears film_device and frees the feed like destroy.
+ * vpt_gpu_feed_prepare allocates a feed's memory (the ring, and with staged != 0 the copy buffers) into the
+ * context's pool ahead of the first open, e.g. right after vpt_gpu_create, so that no allocation runs while a
+ * launch holds the device. */
 int vpt_gpu_feed_open_staged(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t window,
                              vpt_gpu_feed** out);
+int vpt_gpu_feed_snapshot(vpt_gpu_feed* feed, float* film_host);
 int vpt_gpu_feed_collect(vpt_gpu_feed* feed, float* film_host);
+int vpt_gpu_feed_prepare(vpt_gpu_ctx* ctx, uint64_t window, int staged);
 
 /* Zero the context's own film. */
 int vpt_gpu_film_clear(vpt_gpu_ctx* ctx);

@@ -52,43 +52,20 @@
 
 namespace vpt_gpu {
 
-// Renders every job `tp` hands out on `ctx` and adds it into the caller's reference-layout film
-// (float[H][W][4], Image<float,4>) as it goes.  Returns VPT_OK or the first error code
-// (vpt_last_error() has the message).  Several threads may call it with one `tp` and one `film_host`,
-// each with its own context.
-//
-// TileProvider::next() blocks until the same tile's previous wave has been released
-// (src/tile_provider.cpp:40-60), so a thread that holds a token while calling next() deadlocks on
-// itself as soon as the job counter has moved one wave past that token -- which, with other threads
-// taking jobs, can happen at any batch size.  drain() therefore holds no token across next(): each
-// token is released as soon as its job id is recorded.  Every recorded job is rendered (no token is
-// dropped), and the GPU film needs no tile exclusivity: its adds are fp32 atomics.
-//
-// The tokens' job ids go to the GPU through a feed (vpt_gpu_feed_*): one running launch of the
-// production kernel takes them as they are pushed, batch_jobs at a time, so
-//   * the launch never drains between batches (a launch lasts as long as its longest job; a feed's lanes
-//     keep taking the jobs pushed after it);
-//   * token run-ahead is bounded: a push blocks while window_jobs pushed jobs have not started (the ring
-//     is at least twice the launch's lanes), so the provider's job counter (progress(), eta(), what
-//     stop_at_next_wave() cuts) leads the GPU by at most the ring, the push_batch jobs held for the next
-//     push (none by default), and the jobs in flight -- as the reference's workers each hold the token they render;
-//   * the film is progressive (main.cpp:101-132 shows it at 5 FPS): every flush_seconds the running feed
-//     is closed and a new one opened on the other stream and film (its lanes start as the old launch's
-//     drain frees the CUs); the old launch's last block copies its film to pinned memory and clears it,
-//     and once the launch has ended the copy is added into film_host (under a mutex shared by all
-//     callers).  film_host's sample counts thus rise during the run, by whole jobs, and the final film is
-//     the same sum.
 using JobRuns = std::vector<std::pair<uint64_t, uint64_t>>;  // contiguous (jid_begin, count) runs
 
 struct DrainOptions {
-  double flush_seconds = 0.2;     // progressive film period (main.cpp's window draws at 5 FPS)
-  uint64_t window_jobs = 1 << 19;  // pushed jobs not yet started (rounded up to >= 2x the lanes: C3 2^20)
-  // Jobs taken are held and pushed push_batch at a time (0: every batch_jobs).  Measured without effect
-  // (r04i: C3 449.0 vs 450.6 ms, C4 193.9 vs 196.0 ms for 0 vs 2^18), so off: it only adds run-ahead.
-  uint64_t push_batch = 0;
-  // Held jobs pushed costliest tile first (vpt_gpu_tile_costs; the provider's jid order ends a frame on
-  // its densest tiles; needs push_batch).  Measured without gain (r04z / r04i: C3 457-496 vs 449-458 ms): off.
-  bool cost_order = false;
+  double flush_seconds = 0.2;  // progressive film period (main.cpp's window draws at 5 FPS); <= 0: at the end only
+  // Run-ahead: the jobs taken from the provider and not yet started on the GPU are at most hold_jobs (held on
+  // the host, in the order taken) + backlog_jobs (pushed into the feed's ring, which the pusher keeps at least
+  // that full so the lanes never wait for the host).  0 = auto: hold 2 x the launch's lanes (C3: 917 504 jobs,
+  // 28 of 256 waves), backlog 1 x (C3: 458 752).  The C3 frame measured flat over hold 2 / 4 / 6 x and backlog
+  // 1 / 0.5 x (366-372 ms, r05d), and 390 ms without the cost tail.
+  uint64_t hold_jobs = 0;
+  uint64_t backlog_jobs = 0;
+  // When the provider runs dry the held jobs are pushed costliest tile first (vpt_gpu_tile_costs), so the launch
+  // ends on cheap jobs -- the one-launch frame's cost tail (VPT_ORDER_COST_TAIL), over the jobs still held.
+  bool cost_tail = true;
 };
 
 // Takes up to max_jobs tokens; on_token(token&) sees each before it is released.  Returns the count.
@@ -115,24 +92,30 @@ inline std::mutex& film_mutex() {  // the host film is shared by every caller
   return mu;
 }
 
-// Two streams, two device films and the feeds that render into them, for one drain() call.  push() and
-// tick() are called under mu() when other threads push into the same pipeline (help()).
+// One drain() call's pipeline: one staged feed (one launch of the production kernel for the whole drain, no
+// launch drain between batches), a pusher thread that feeds it from the jobs the takers queue, and a film
+// thread that adds the launch's progress into the caller's film every flush_seconds.  The takers (the driving
+// thread and help() threads) only take tokens and queue their job ids: the provider's next() is the drop-in's
+// host-side bound (C4: ~40 M tokens/s on one thread vs ~84 M jobs/s the GPU renders), so nothing else runs on
+// that thread.
 class FeedPipeline {
  public:
-  std::mutex& mu() { return mu_; }
-  std::atomic<int> helpers{0};  // helper threads attached (see detail::Helpers)
+  std::atomic<int> helpers{0};  // help() threads attached (see detail::Helpers)
   explicit FeedPipeline(vpt_gpu_ctx* ctx) : ctx_(ctx) {}
   ~FeedPipeline() {
-    for (int i = 0; i < 2; ++i) {
-      if (feeds_[i]) (void)vpt_gpu_feed_destroy(feeds_[i]);
-      if (streams_[i]) (void)vpt_gpu_stream_destroy(ctx_, streams_[i]);
-    }
-    if (films_[1]) (void)vpt_gpu_film_free(ctx_, films_[1]);
+    stop_threads();
+    if (feed_) (void)vpt_gpu_feed_destroy(feed_);
   }
-  int init(uint64_t window, uint64_t push_batch = 0, bool cost_order = false) {
-    window_ = window;
-    hold_ = push_batch;
-    if (push_batch && cost_order) {  // cost classes per tile, before any feed holds the device (the cost pass syncs)
+  int start(float* film_host, const DrainOptions& opt) {
+    film_host_ = film_host;
+    flush_ = opt.flush_seconds;
+    int blocks = 0, threads = 0;
+    if (int rc = vpt_gpu_launch_info(ctx_, &blocks, &threads)) return rc;
+    const uint64_t lanes = (uint64_t)blocks * (uint64_t)threads;
+    lanes_ = lanes;
+    hold_max_ = opt.hold_jobs ? opt.hold_jobs : 2 * lanes;
+    backlog_ = opt.backlog_jobs ? opt.backlog_jobs : lanes;
+    if (opt.cost_tail) {  // cost classes per tile, before the feed holds the device (the cost pass syncs)
       uint64_t T = 0, total = 0;
       if (int rc = vpt_gpu_job_space(ctx_, &T, &total)) return rc;
       std::vector<uint32_t> rank(T);
@@ -140,111 +123,178 @@ class FeedPipeline {
       cls_.assign(T, 0);
       for (uint64_t i = 0; i < T; ++i) cls_[rank[i]] = (uint8_t)((i * kClasses) / T);  // 0: costliest
     }
-    for (void*& s : streams_)
-      if (int rc = vpt_gpu_stream_create(ctx_, &s)) return rc;
-    if (int rc = vpt_gpu_film_alloc(ctx_, &films_[1])) return rc;
-    last_switch_ = std::chrono::steady_clock::now();
-    return vpt_gpu_feed_open_staged(ctx_, films_[0], streams_[0], window_, &feeds_[0]);
-  }
-  int push(const JobRuns& runs) {
-    if (hold_) {
-      for (const auto& r : runs)
-        for (uint64_t i = 0; i < r.second; ++i) held_.push_back(r.first + i);
-      return held_.size() >= hold_ ? release() : VPT_OK;
-    }
-    ids_.clear();
-    for (const auto& r : runs)
-      for (uint64_t i = 0; i < r.second; ++i) ids_.push_back(r.first + i);
-    return vpt_gpu_feed_push(feeds_[cur_], ids_.data(), ids_.size());
-  }
-  // Pushes the held jobs into the running feed: as taken, or (cost_order) costliest tile class first (a
-  // counting sort; within a class in the order taken).
-  int release() {
-    if (held_.empty()) return VPT_OK;
-    if (cls_.empty()) {
-      const int rc = vpt_gpu_feed_push(feeds_[cur_], held_.data(), held_.size());
-      held_.clear();
-      return rc;
-    }
-    uint64_t start[kClasses + 1] = {};
-    const uint64_t T = cls_.size();
-    for (uint64_t j : held_) ++start[cls_[j % T] + 1];
-    for (int c = 0; c < kClasses; ++c) start[c + 1] += start[c];
-    ids_.resize(held_.size());
-    for (uint64_t j : held_) ids_[start[cls_[j % T]]++] = j;
-    held_.clear();
-    return vpt_gpu_feed_push(feeds_[cur_], ids_.data(), ids_.size());
-  }
-  // Adds the retired feed's film to film_host once its launch has ended; every flush_seconds retires the
-  // current feed (the other one must have been flushed) and opens the next on the other stream and film.
-  int tick(double flush_seconds, float* film_host) {
-    const int old = cur_ ^ 1;
-    if (feeds_[old]) {
-      int done = 0;
-      if (int rc = vpt_gpu_feed_query(feeds_[old], &done, nullptr)) return rc;
-      if (done)
-        if (int rc = flush(old, film_host)) return rc;
-    }
-    const auto now = std::chrono::steady_clock::now();
-    if (!feeds_[old] && std::chrono::duration<double>(now - last_switch_).count() >= flush_seconds) {
-      if (int rc = vpt_gpu_feed_close(feeds_[cur_])) return rc;
-      cur_ = old;
-      last_switch_ = now;
-      return vpt_gpu_feed_open_staged(ctx_, films_[cur_], streams_[cur_], window_, &feeds_[cur_]);
-    }
+    // the ring holds the backlog plus the lanes' reservations; the feed's own stream
+    if (int rc = vpt_gpu_feed_open_staged(ctx_, nullptr, nullptr, backlog_ + lanes, &feed_)) return rc;
+    pusher_ = std::thread([this] { pusher_main(); });
+    if (flush_ > 0) film_ = std::thread([this] { film_main(); });
     return VPT_OK;
   }
-  int finish(float* film_host) {
-    if (int rc = release()) return rc;
-    for (vpt_gpu_feed* f : feeds_)  // every feed closed before any wait: an open one holds the device
-      if (f)
-        if (int rc = vpt_gpu_feed_close(f)) return rc;
-    for (int i : {cur_ ^ 1, cur_})
-      if (feeds_[i])
-        if (int rc = flush(i, film_host)) return rc;
+  // A taker's batch of job ids: queued for the pusher.  Blocks while the run-ahead bound is reached.
+  int add(const JobRuns& runs) {
+    uint64_t n = 0;
+    for (const auto& r : runs) n += r.second;
+    std::unique_lock<std::mutex> l(mu_);
+    taker_cv_.wait(l, [&] { return err_ != VPT_OK || queued_ + held_ < hold_max_; });
+    if (err_ != VPT_OK) return err_;
+    queue_.insert(queue_.end(), runs.begin(), runs.end());
+    queued_ += n;
     return VPT_OK;
+  }
+  // No more jobs: the pusher pushes what it holds and closes the feed; then the rest of the film is added.
+  int finish() {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      no_more_ = true;
+    }
+    if (pusher_.joinable()) pusher_.join();
+    stop_threads();  // no snapshot starts once the feed is closed: the collect adds the rest
+    int rc = err_;
+    if (feed_) {
+      vpt_gpu_feed* f = feed_;
+      feed_ = nullptr;
+      // The wait happens before the film lock: another caller's launch may be waiting for this device's CUs,
+      // which this feed's launch holds until that caller -- maybe blocked on the lock -- closes its feed.
+      int frc = vpt_gpu_feed_close(f);
+      for (int done = 0; frc == VPT_OK && !done;)
+        if ((frc = vpt_gpu_feed_query(f, &done, nullptr)) == VPT_OK && !done)
+          std::this_thread::sleep_for(std::chrono::microseconds(100));
+      if (frc == VPT_OK) {
+        std::lock_guard<std::mutex> lock(film_mutex());
+        frc = vpt_gpu_feed_collect(f, film_host_);
+      } else {
+        (void)vpt_gpu_feed_destroy(f);
+      }
+      if (rc == VPT_OK) rc = frc;
+    }
+    return rc;
   }
 
  private:
-  // A staged feed's launch copies out and clears its own film (nothing is queued on the GPU while the
-  // other feed's launch runs); collect adds the copy into film_host once the launch has ended.  The
-  // wait happens before the film lock: another caller's launch may be waiting for this device's CUs,
-  // which this feed's launch holds until that caller -- maybe blocked on the lock -- closes its feed.
-  int flush(int i, float* film_host) {
-    int rc = vpt_gpu_feed_close(feeds_[i]);
-    for (int done = 0; rc == VPT_OK && !done;)
-      if ((rc = vpt_gpu_feed_query(feeds_[i], &done, nullptr)) == VPT_OK && !done)
-        std::this_thread::sleep_for(std::chrono::microseconds(100));
-    if (rc == VPT_OK) {
-      std::lock_guard<std::mutex> lock(film_mutex());
-      rc = vpt_gpu_feed_collect(feeds_[i], film_host);
-    } else {
-      (void)vpt_gpu_feed_destroy(feeds_[i]);
-    }
-    feeds_[i] = nullptr;
-    return rc;
-  }
-  vpt_gpu_ctx* ctx_;
-  uint64_t window_ = 0;
-  void* streams_[2] = {nullptr, nullptr};
-  float* films_[2] = {nullptr, nullptr};  // [0]: the context's own film (NULL), [1]: allocated
-  vpt_gpu_feed* feeds_[2] = {nullptr, nullptr};
-  int cur_ = 0;
-  std::vector<uint64_t> ids_;
   static constexpr int kClasses = 256;
-  std::vector<uint8_t> cls_;     // per tile: cost class (0 = costliest), with cost_order
-  std::vector<uint64_t> held_;   // jobs taken, not yet pushed
-  uint64_t hold_ = 0;
-  std::chrono::steady_clock::time_point last_switch_;
-  std::mutex mu_;
+  static constexpr uint64_t kChunk = 16384;  // jobs per push
+
+  void fail(int rc) {
+    std::lock_guard<std::mutex> l(mu_);
+    if (err_ == VPT_OK) err_ = rc;
+    taker_cv_.notify_all();
+  }
+  int push(const uint64_t* ids, uint64_t n) { return n ? vpt_gpu_feed_push(feed_, ids, n) : VPT_OK; }
+  // Pushes held jobs, oldest first, while the feed's backlog is below its mark -- and, until the launch has
+  // started (it starts once a lane's worth of jobs is pushed, vpt_gpu_feed_push), below the lanes.
+  int top_up(std::vector<uint64_t>& hold, size_t& head) {
+    uint64_t b = 0;
+    if (int rc = vpt_gpu_feed_backlog(feed_, &b)) return rc;
+    const uint64_t mark = pushed_ < lanes_ ? std::max(backlog_, lanes_) : backlog_;
+    while (head < hold.size() && b < mark) {
+      const uint64_t n = std::min<uint64_t>(kChunk, hold.size() - head);
+      if (int rc = push(hold.data() + head, n)) return rc;
+      head += n;
+      b += n;
+      pushed_ += n;
+    }
+    if (head == hold.size()) {
+      hold.clear();
+      head = 0;
+    } else if (head > (1u << 20) && head * 2 > hold.size()) {
+      hold.erase(hold.begin(), hold.begin() + (ptrdiff_t)head);
+      head = 0;
+    }
+    return VPT_OK;
+  }
+  void pusher_main() {
+    std::vector<uint64_t> hold;  // taken, not pushed: hold[head..] in the order taken
+    size_t head = 0;
+    JobRuns batch;
+    for (;;) {
+      bool last;
+      {
+        std::lock_guard<std::mutex> l(mu_);
+        batch.swap(queue_);
+        queue_.clear();
+        held_ += queued_;
+        queued_ = 0;
+        last = no_more_;  // (set after the takers' last add: everything is in batch now)
+      }
+      // nothing new: the lanes take jobs meanwhile (the backlog check below); a timed condition-variable wait
+      // would do the same, but ThreadSanitizer (gcc 11) does not model pthread_cond_clockwait
+      if (batch.empty() && !last) std::this_thread::sleep_for(std::chrono::microseconds(50));
+      for (const auto& r : batch)
+        for (uint64_t i = 0; i < r.second; ++i) hold.push_back(r.first + i);
+      batch.clear();
+      if (last) break;
+      const size_t before = hold.size() - head;
+      if (int rc = top_up(hold, head)) return fail(rc);
+      if (hold.size() - head != before) {
+        std::lock_guard<std::mutex> l(mu_);
+        held_ = hold.size() - head;
+        taker_cv_.notify_all();
+      }
+    }
+    // The provider is dry: the held jobs, costliest tile class first (jid order within a class: consecutive
+    // items are different tiles of one wave), then the end of the feed.
+    std::vector<uint64_t> rest(hold.begin() + (ptrdiff_t)head, hold.end());
+    if (!cls_.empty() && !rest.empty()) {
+      const uint64_t T = cls_.size();
+      uint64_t start[kClasses + 1] = {};
+      for (uint64_t j : rest) ++start[cls_[j % T] + 1];
+      for (int c = 0; c < kClasses; ++c) start[c + 1] += start[c];
+      std::vector<uint64_t> sorted(rest.size());
+      for (uint64_t j : rest) sorted[start[cls_[j % T]]++] = j;
+      rest.swap(sorted);
+    }
+    for (size_t i = 0; i < rest.size(); i += kChunk)
+      if (int rc = push(rest.data() + i, std::min<uint64_t>(kChunk, rest.size() - i))) return fail(rc);
+    if (int rc = vpt_gpu_feed_close(feed_)) return fail(rc);
+    std::lock_guard<std::mutex> l(mu_);
+    held_ = 0;
+  }
+  void film_main() {
+    auto next = std::chrono::steady_clock::now() + std::chrono::duration<double>(flush_);
+    while (!film_stop_.load()) {
+      if (std::chrono::steady_clock::now() < next) {  // (slices of 1 ms: stop_threads() ends the wait)
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        continue;
+      }
+      next += std::chrono::duration_cast<std::chrono::steady_clock::duration>(std::chrono::duration<double>(flush_));
+      std::lock_guard<std::mutex> lock(film_mutex());
+      if (int rc = vpt_gpu_feed_snapshot(feed_, film_host_)) return fail(rc);
+    }
+  }
+  void stop_threads() {
+    film_stop_.store(true);
+    if (film_.joinable()) film_.join();
+    if (pusher_.joinable()) {  // (an error path: let the pusher end)
+      {
+        std::lock_guard<std::mutex> l(mu_);
+        no_more_ = true;
+      }
+      pusher_.join();
+    }
+  }
+
+  vpt_gpu_ctx* ctx_;
+  float* film_host_ = nullptr;
+  double flush_ = 0.2;
+  uint64_t hold_max_ = 0, backlog_ = 0, lanes_ = 0;
+  uint64_t pushed_ = 0;  // (the pusher's)
+  vpt_gpu_feed* feed_ = nullptr;
+  std::vector<uint8_t> cls_;  // per tile: cost class (0 = costliest)
+  std::thread pusher_, film_;
+  std::mutex mu_;  // queue_, queued_, held_, no_more_, err_
+  std::condition_variable taker_cv_;
+  JobRuns queue_;
+  uint64_t queued_ = 0, held_ = 0;
+  bool no_more_ = false;
+  int err_ = VPT_OK;
+  std::atomic<bool> film_stop_{false};
 };
 
 namespace detail {
 // Threads on one provider: each GPU is driven by the one thread that claimed it; other threads may take
-// tokens too and push their job ids into a driving thread's pipeline (help()), since one thread takes ~26 M
-// tokens/s while a GPU can render more (C4: ~84 M jobs/s).  run() does not use it: with the restated
-// TileProvider, contended next() calls made it slower (see run_checked); a provider whose next() scales
-// across threads could.
+// tokens too and queue their job ids into a driving thread's pipeline (help()).  run() does not use it: with
+// the restated TileProvider, contended next() calls are slower than one thread's (r05: 1 thread 36 M tokens/s,
+// 2 threads 23 M/s, 4 threads 20 M/s on an 8-core Xeon: the provider's one job counter); a provider whose
+// next() scales across threads could.
 struct Helpers {
   std::mutex mu;
   std::condition_variable cv;
@@ -259,44 +309,58 @@ struct Helpers {
 
 }  // namespace detail
 
-// `first`: job runs already taken by the caller (pushed first).  `share`: other threads of run() may
-// push into this pipeline while it drains (detail::Helpers); drain returns once they have detached.
+// Renders every job `tp` hands out on `ctx` and adds it into the caller's reference-layout film
+// (float[H][W][4], Image<float,4>) as it goes.  Returns VPT_OK or the first error code (vpt_last_error() has
+// the message).  Several threads may call it with one `tp` and one `film_host`, each with its own context.
+//
+// TileProvider::next() blocks until the same tile's previous wave has been released
+// (src/tile_provider.cpp:40-60), so a thread that holds a token while calling next() deadlocks on itself as
+// soon as the job counter has moved one wave past that token -- which, with other threads taking jobs, can
+// happen at any batch size.  drain() therefore holds no token across next(): each token is released as soon
+// as its job id is recorded.  Every recorded job is rendered (no token is dropped), and the GPU film needs no
+// tile exclusivity: its adds are fp32 atomics.
+//
+// The job ids reach the GPU through one staged feed (vpt_gpu_feed_*): one running launch of the production
+// kernel takes them as they are pushed, so
+//   * nothing drains until the provider is dry (a launch lasts as long as its longest job);
+//   * run-ahead is bounded: the takers wait while opt.hold_jobs taken jobs are held, and the pusher keeps
+//     opt.backlog_jobs in the ring, so the provider's job counter (progress(), eta(), what
+//     stop_at_next_wave() cuts) leads the GPU by at most those plus the jobs in flight -- as the reference's
+//     workers each hold the token they render;
+//   * the launch ends on cheap jobs: the jobs held when the provider runs dry go costliest tile first;
+//   * the film is progressive (main.cpp:101-132 shows it at 5 FPS): every flush_seconds the film thread adds
+//     what the launch has completed into film_host (the copy engines read the device film beside the launch),
+//     under a mutex shared by all callers; the final film is the launch's.
+// `first`: job runs already taken by the caller (queued first).  `share`: other threads of run() may queue
+// into this pipeline while it drains (detail::Helpers); drain returns once they have detached.
 template <class Provider>
 int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs, const DrainOptions& opt = {},
           const JobRuns* first = nullptr, bool share = false) {
   FeedPipeline pipe(ctx);
-  if (int rc = pipe.init(opt.window_jobs, opt.push_batch, opt.cost_order)) return rc;
-  if (first)
-    if (int rc = pipe.push(*first)) return rc;
+  int rc = pipe.start(film_host, opt);
+  if (rc == VPT_OK && first) rc = pipe.add(*first);
   detail::Helpers& hub = detail::Helpers::get();
-  if (share) {
+  if (share && rc == VPT_OK) {
     std::lock_guard<std::mutex> l(hub.mu);
     hub.pipes.push_back(&pipe);
     hub.cv.notify_all();
   }
-  int rc = VPT_OK;
   JobRuns runs;
-  while (rc == VPT_OK && take_jobs(tp, std::max<uint64_t>(1, batch_jobs), runs, [](auto&) {})) {
-    std::lock_guard<std::mutex> l(pipe.mu());
-    if ((rc = pipe.push(runs)) == VPT_OK) rc = pipe.tick(opt.flush_seconds, film_host);
-  }
-  if (share) {  // no new helper attaches; the attached ones push their last jobs, then detach
+  while (rc == VPT_OK && take_jobs(tp, std::max<uint64_t>(1, batch_jobs), runs, [](auto&) {})) rc = pipe.add(runs);
+  if (share) {  // no new helper attaches; the attached ones queue their last jobs, then detach
     {
       std::lock_guard<std::mutex> l(hub.mu);
-      hub.pipes.erase(std::find(hub.pipes.begin(), hub.pipes.end(), &pipe));
+      auto it = std::find(hub.pipes.begin(), hub.pipes.end(), &pipe);
+      if (it != hub.pipes.end()) hub.pipes.erase(it);
     }
-    while (pipe.helpers.load() > 0) {
-      std::this_thread::sleep_for(std::chrono::milliseconds(2));
-      std::lock_guard<std::mutex> l(pipe.mu());
-      if (rc == VPT_OK) rc = pipe.tick(opt.flush_seconds, film_host);
-    }
+    while (pipe.helpers.load() > 0) std::this_thread::sleep_for(std::chrono::milliseconds(1));
   }
-  const int frc = pipe.finish(film_host);
+  const int frc = pipe.finish();
   return rc ? rc : frc;
 }
 
-// A helper thread (run() does not start any, see run_checked): takes tokens batch_jobs at a time and pushes their job ids into a driving
-// thread's pipeline, until the provider is exhausted (or no thread drives a GPU).
+// A helper thread (run() does not start any, see run_checked): takes tokens batch_jobs at a time and queues
+// their job ids into a driving thread's pipeline, until the provider is exhausted (or no thread drives a GPU).
 template <class Provider>
 int help(Provider& tp, uint64_t batch_jobs) {
   detail::Helpers& hub = detail::Helpers::get();
@@ -310,10 +374,7 @@ int help(Provider& tp, uint64_t batch_jobs) {
   }
   int rc = VPT_OK;
   JobRuns runs;
-  while (rc == VPT_OK && take_jobs(tp, std::max<uint64_t>(1, batch_jobs), runs, [](auto&) {})) {
-    std::lock_guard<std::mutex> l(pipe->mu());
-    rc = pipe->push(runs);
-  }
+  while (rc == VPT_OK && take_jobs(tp, std::max<uint64_t>(1, batch_jobs), runs, [](auto&) {})) rc = pipe->add(runs);
   --pipe->helpers;  // the last touch: its driver may finish and destroy the pipeline from here on
   return rc;
 }
@@ -532,8 +593,11 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
     vpt_gpu_ctx* c;
     ~Ctx() { vpt_gpu_destroy(c); }
   } guard{ctx};
+  // setup, like the grid upload: the feed's pinned ring and copy buffers, and the tile costs of its cost tail
+  if (int rc = vpt_gpu_feed_prepare(ctx, 0, 1)) return rc;
+  if (int rc = vpt_gpu_tile_costs(ctx, nullptr, nullptr)) return rc;
   float* film_host = reinterpret_cast<float*>(film.data().data());  // H x W x (X, Y, Z, W)
-  // the first batch is pushed first; then 4096 tokens per push (a token is one 8x8 job: 64 samples)
+  // the first batch is queued first; then 4096 tokens per batch (a token is one 8x8 job: 64 samples)
   (void)T;
   return drain(ctx, tp, film_host, 4096, DrainOptions{}, &runs);
 }

@@ -1,13 +1,13 @@
 // dropin_mock.cpp -- TEST HARNESS (CPU only): include/vpt_run.hpp's drain / help threads over a mock of the
-// C ABI's stream, film and feed calls, so the host-side protocol -- tokens taken by drivers and helpers,
-// pushes under the pipeline's lock, feed switches, the progressive film, helpers detaching before the
-// driver's final flush -- is checked without a GPU: every job id the provider hands out must be "rendered"
+// C ABI's stream, film and feed calls, so the host-side protocol -- tokens taken by drivers and helpers and
+// queued for the pusher thread, the run-ahead bound, the held jobs' cost tail, the film thread's snapshots,
+// helpers detaching before the driver's final collect -- is checked without a GPU: every job id the provider hands out must be "rendered"
 // (pushed into some open feed) exactly once, and the host film must count every sample once.  The mock
 // keeps the GPU's one blocking rule: a feed's launch holds the device (every context shares one here) until
 // it is closed, so a feed's work completes only once it and every feed opened before it are closed; a wait
 // that cannot end that way within 5 s is reported as a deadlock.
 //
-//   dropin_mock drivers=<n> helpers=<n> w= h= waves= batch= flush_ms= window= stop_after=
+//   dropin_mock drivers=<n> helpers=<n> w= h= waves= batch= flush_ms= hold= backlog= cost_tail= stop_after=
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
@@ -39,7 +39,10 @@ struct vpt_gpu_feed {
   float* film;
   bool closed = false;
   bool staged = false;
-  std::vector<float> copy;  // a staged feed's film, copied out at close
+  std::mutex mu;              // film / shown: the pusher "renders" (push), the film thread snapshots
+  std::vector<float> shown;   // a staged feed's film as already added to the host film
+  uint64_t published = 0;
+  std::atomic<uint64_t> backlog_calls{0};
 };
 
 namespace {
@@ -61,6 +64,13 @@ void dev_remove(vpt_gpu_feed* f) {
   std::lock_guard<std::mutex> l(g_dev_mu);
   g_dev_feeds.erase(std::find(g_dev_feeds.begin(), g_dev_feeds.end(), f));
 }
+void add_delta(vpt_gpu_feed* f, float* host) {  // host += film - shown; shown = film
+  std::lock_guard<std::mutex> l(f->mu);
+  for (int64_t i = 0; i < g_w * g_h * 4; ++i) {
+    host[i] += f->film[i] - f->shown[i];
+    f->shown[i] = f->film[i];
+  }
+}
 }  // namespace
 
 extern "C" {
@@ -73,7 +83,11 @@ int vpt_gpu_stream_destroy(vpt_gpu_ctx*, void* s) {
   delete static_cast<int*>(s);
   return VPT_OK;
 }
-int vpt_gpu_stream_sync(vpt_gpu_ctx*, void*) { return VPT_OK; }
+int vpt_gpu_launch_info(const vpt_gpu_ctx*, int* blocks, int* threads) {  // a small "GPU": 3 x 7 lanes
+  *blocks = 3;
+  *threads = 7;
+  return VPT_OK;
+}
 int vpt_gpu_job_space(const vpt_gpu_ctx*, uint64_t* per_wave, uint64_t* total) {
   *per_wave = (uint64_t)(g_ntx * ((g_h + g_th - 1) / g_th));
   *total = 0;
@@ -81,30 +95,17 @@ int vpt_gpu_job_space(const vpt_gpu_ctx*, uint64_t* per_wave, uint64_t* total) {
 }
 int vpt_gpu_tile_costs(vpt_gpu_ctx*, float*, uint32_t* rank) {  // the last tile costliest: a real reorder
   const uint64_t T = (uint64_t)(g_ntx * ((g_h + g_th - 1) / g_th));
-  for (uint64_t i = 0; i < T; ++i) rank[i] = (uint32_t)(T - 1 - i);
+  if (rank)
+    for (uint64_t i = 0; i < T; ++i) rank[i] = (uint32_t)(T - 1 - i);
   return VPT_OK;
 }
-int vpt_gpu_film_alloc(vpt_gpu_ctx*, float** f) {
-  *f = new float[(size_t)(g_w * g_h * 4)]();
-  return VPT_OK;
-}
-int vpt_gpu_film_free(vpt_gpu_ctx*, float* f) {
-  delete[] f;
-  return VPT_OK;
-}
-int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* c, float* f, float* host) {
-  float* src = f ? f : c->own.data();
-  for (int64_t i = 0; i < g_w * g_h * 4; ++i) {
-    host[i] += src[i];
-    src[i] = 0.0f;
-  }
-  return VPT_OK;
-}
+int vpt_gpu_feed_prepare(vpt_gpu_ctx*, uint64_t, int) { return VPT_OK; }
 int vpt_gpu_feed_open(vpt_gpu_ctx* c, float* film, void* stream, uint64_t, vpt_gpu_feed** out) {
   if (!stream) return VPT_E_INVALID;
   *out = new vpt_gpu_feed();
   (*out)->ctx = c;
   (*out)->film = film ? film : c->own.data();
+  (*out)->shown.assign((size_t)(g_w * g_h * 4), 0.0f);
   {
     std::lock_guard<std::mutex> l(g_dev_mu);
     g_dev_feeds.push_back(*out);
@@ -125,25 +126,27 @@ int vpt_gpu_feed_push(vpt_gpu_feed* f, const uint64_t* jids, uint64_t n) {
       ++g_rendered[jids[i]];
     }
     const int64_t tile = (int64_t)(jids[i] % (uint64_t)T), x0 = (tile % g_ntx) * g_tw, y0 = (tile / g_ntx) * g_th;
+    std::lock_guard<std::mutex> l(f->mu);
     for (int64_t y = y0; y < std::min(g_h, y0 + g_th); ++y)
       for (int64_t x = x0; x < std::min(g_w, x0 + g_tw); ++x) f->film[(y * g_w + x) * 4 + 3] += 1.0f;  // the count
   }
+  f->published += n;
   if (n % 3 == 0) std::this_thread::yield();  // let other threads interleave
   return VPT_OK;
 }
+int vpt_gpu_feed_backlog(vpt_gpu_feed* f, uint64_t* b) {  // alternately "starved" and "full": both pusher branches
+  *b = (f->backlog_calls++ % 4 == 0) ? 0 : f->published;
+  return VPT_OK;
+}
 int vpt_gpu_feed_open_staged(vpt_gpu_ctx* c, float* film, void* stream, uint64_t w, vpt_gpu_feed** out) {
-  const int rc = vpt_gpu_feed_open(c, film, stream, w, out);
+  int own = 0;  // (a staged feed without a stream uses its own)
+  const int rc = vpt_gpu_feed_open(c, film, stream ? stream : &own, w, out);
   if (rc == VPT_OK) (*out)->staged = true;
   return rc;
 }
 int vpt_gpu_feed_close(vpt_gpu_feed* f) {
   std::lock_guard<std::mutex> l(g_dev_mu);
-  if (f->closed) return VPT_OK;
   f->closed = true;
-  if (f->staged) {
-    f->copy.assign(f->film, f->film + g_w * g_h * 4);
-    std::fill(f->film, f->film + g_w * g_h * 4, 0.0f);
-  }
   return VPT_OK;
 }
 int vpt_gpu_feed_query(vpt_gpu_feed* f, int* done, uint64_t*) {
@@ -158,12 +161,20 @@ int vpt_gpu_feed_destroy(vpt_gpu_feed* f) {
   delete f;
   return rc;
 }
+int vpt_gpu_feed_snapshot(vpt_gpu_feed* f, float* host) {
+  if (!f->staged) return VPT_E_INVALID;
+  add_delta(f, host);
+  return VPT_OK;
+}
 int vpt_gpu_feed_collect(vpt_gpu_feed* f, float* host) {
   if (!f->staged) return VPT_E_INVALID;
   vpt_gpu_feed_close(f);
   int rc = wait_complete(f);
-  if (rc == VPT_OK)
-    for (int64_t i = 0; i < g_w * g_h * 4; ++i) host[i] += f->copy[i];
+  if (rc == VPT_OK) {
+    add_delta(f, host);
+    std::lock_guard<std::mutex> l(f->mu);
+    std::fill(f->film, f->film + g_w * g_h * 4, 0.0f);
+  }
   dev_remove(f);
   --g_open_feeds;
   delete f;
@@ -173,8 +184,8 @@ int vpt_gpu_feed_collect(vpt_gpu_feed* f, float* host) {
 
 int main(int argc, char** argv) {
   std::map<std::string, long long> a{{"drivers", 1}, {"helpers", 0}, {"w", 72}, {"h", 40}, {"waves", 5},
-                                     {"batch", 7}, {"flush_ms", 0}, {"window", 1024}, {"stop_after", 0},
-                                     {"push_batch", 0}, {"cost_order", 0}};
+                                     {"batch", 7}, {"flush_ms", 0}, {"hold", 0}, {"backlog", 0}, {"stop_after", 0},
+                                     {"cost_tail", 1}};
   for (int i = 1; i < argc; ++i) {
     const char* eq = std::strchr(argv[i], '=');
     if (eq) a[std::string(argv[i], eq - argv[i])] = std::atoll(eq + 1);
@@ -201,9 +212,9 @@ int main(int argc, char** argv) {
   for (auto& c : ctx) c.own.assign(film.size(), 0.0f);
   vpt_gpu::DrainOptions opt;
   opt.flush_seconds = (double)a["flush_ms"] / 1000.0;
-  opt.window_jobs = (uint64_t)a["window"];
-  opt.push_batch = (uint64_t)a["push_batch"];
-  opt.cost_order = a["cost_order"] != 0;
+  opt.hold_jobs = (uint64_t)a["hold"];
+  opt.backlog_jobs = (uint64_t)a["backlog"];
+  opt.cost_tail = a["cost_tail"] != 0;
   {
     std::lock_guard<std::mutex> l(vpt_gpu::detail::Helpers::get().mu);
     vpt_gpu::detail::Helpers::get().drivers += drivers;  // (run() counts them when they claim a device)

@@ -5,7 +5,7 @@
 //
 //   run_gpu_harness config=<scene.json> out=<film.f32> [mode=drain|run w= h= waves= threads= batch=
 //                   grid_n= dist= temperature=0|1 stop_after=<jobs> nvdb=<file.nvdb> gridbuf=<file>
-//                   tempbuf=<file> window= flush_ms= push_batch= cost_order= helpers= grid_blocks= sample_ms=]
+//                   tempbuf=<file> hold= backlog= flush_ms= cost_tail= helpers= grid_blocks= sample_ms= frames=]
 //
 // mode=drain (default): each thread owns a context made with vpt_gpu_create and calls
 //   vpt_gpu::drain(ctx, tp, film, batch).  The volume is nvdb= (vpt_grid_read_nvdb: "density", and
@@ -17,8 +17,10 @@
 //   to the RandomNumberGenerator.
 // The camera looks at the volume from (0, 0, -dist) unless dist=0 (then the scene file's camera).
 // stop_after: after that many jobs thread 0 calls tp.stop_at_next_wave() (tile_provider.cpp:107-110).
-// window / flush_ms / push_batch / cost_order: vpt_gpu::DrainOptions of mode=drain; helpers: threads that take tokens for the drain
+// hold / backlog / flush_ms / cost_tail: vpt_gpu::DrainOptions of mode=drain; helpers: threads that take tokens for the drain
 // threads (vpt_gpu::help, as run()'s threads that find every GPU driven); grid_blocks: vpt_gpu_set_tuning's grid override.
+// mode=tokens (no GPU): the provider alone -- `threads` threads take every token of the frame and release it at once, the
+// drop-in's host-side floor (r05) -- printed as tokens_ms and M tokens/s.
 // sample_ms: a thread samples, every sample_ms, the jobs handed out and the samples in the host film (what
 // main.cpp's 5-FPS window shows: film_to_image(film) and provider.progress(), main.cpp:101-132) and prints
 // them as "sample <ms> <waves handed out> <waves in the film>".  The render time is printed as render_ms.
@@ -141,6 +143,23 @@ int main(int argc, char** argv) {
     std::printf("run_gpu_harness: tiles %d %lld %lld %zu\n", ok ? 1 : 0, (long long)tw, (long long)th, runs.size());
     return 0;
   }
+  if (mode == "tokens") {
+    std::vector<std::thread> pool;
+    std::vector<uint64_t> got(threads, 0);
+    const auto r0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < threads; ++i)
+      pool.emplace_back([&, i] {
+        vpt_gpu::JobRuns runs;
+        while (uint64_t n = vpt_gpu::take_jobs(sp, 4096, runs, [](auto&) {})) got[i] += n;
+      });
+    for (auto& t : pool) t.join();
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count();
+    uint64_t n = 0;
+    for (uint64_t g : got) n += g;
+    std::printf("run_gpu_harness: tokens_ms %.1f, %llu tokens, %.1f M tokens/s, %d threads\n", ms, (unsigned long long)n,
+                n / ms / 1e3, threads);
+    return 0;
+  }
   if (mode == "run") {
     // The reference's objects, built from the same configuration as main.cpp builds them.
     const std::vector<char> gbuf = slurp(a["gridbuf"]), tbuf = a.count("tempbuf") ? slurp(a["tempbuf"]) : std::vector<char>();
@@ -183,15 +202,30 @@ int main(int argc, char** argv) {
       if (vpt_gpu_create(&cfg, dens, temp, nullptr, i % ndev, &ctx[i])) return fail("vpt_gpu_create");
     float* fh = reinterpret_cast<float*>(film.data().data());
     vpt_gpu::DrainOptions opt;
-    opt.window_jobs = (uint64_t)num("window", (long long)opt.window_jobs);
-    opt.push_batch = (uint64_t)num("push_batch", (long long)opt.push_batch);
-    opt.cost_order = num("cost_order", opt.cost_order ? 1 : 0) != 0;
+    opt.hold_jobs = (uint64_t)num("hold", (long long)opt.hold_jobs);
+    opt.backlog_jobs = (uint64_t)num("backlog", (long long)opt.backlog_jobs);
+    opt.cost_tail = num("cost_tail", opt.cost_tail ? 1 : 0) != 0;
     opt.flush_seconds = (double)num("flush_ms", (long long)(opt.flush_seconds * 1000)) / 1000.0;
     if (num("grid_blocks", 0) > 0)
       for (auto* c : ctx)
         if (vpt_gpu_set_tuning(c, 0, -1, (int)num("grid_blocks", 0), 0, -1)) return fail("vpt_gpu_set_tuning");
-    for (auto* c : ctx)  // the context's one-time tile-cost pass, outside the timed render
-      if (vpt_gpu_tile_costs(c, nullptr, nullptr) || vpt_gpu_sync(c)) return fail("warm-up");
+    for (auto* c : ctx)  // setup outside the timed render, as run_checked does it: the tile-cost pass, the feed's memory
+      if (vpt_gpu_tile_costs(c, nullptr, nullptr) || vpt_gpu_feed_prepare(c, 0, 1) || vpt_gpu_sync(c)) return fail("warm-up");
+    // frames=N: N - 1 more frames first, each with a fresh provider and film (main.cpp renders one frame per
+    // process: these time the same drain again, on the contexts already built), one render_ms line each
+    for (long long fr = 1; fr < num("frames", 1); ++fr) {
+      vpt_headless::TileProvider tp2(cfg.output_size[0], cfg.output_size[1], cfg.num_waves, cfg.tile_size[0], cfg.tile_size[1]);
+      vpt_headless::Image<float, 4> film2(cfg.output_size[0], cfg.output_size[1]);
+      float* fh2 = reinterpret_cast<float*>(film2.data().data());
+      const auto r0 = std::chrono::steady_clock::now();
+      std::vector<std::thread> pool;
+      for (int i = 0; i < threads; ++i) pool.emplace_back([&, i] { rc[i] = vpt_gpu::drain(ctx[i], tp2, fh2, batch, opt); });
+      for (auto& t : pool) t.join();
+      for (int i = 0; i < threads; ++i)
+        if (rc[i]) return fail("vpt_gpu::drain");
+      std::printf("run_gpu_harness: render_ms %.1f\n",
+                  std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count());
+    }
     {
       const auto r0 = std::chrono::steady_clock::now();
       if (sample_ms > 0) sampler_thread = std::thread(sampler);

@@ -1,8 +1,9 @@
-"""The drop-in's host protocol (include/vpt_run.hpp: drain's feeds and film switches, run()'s helper threads)
-over a mock of the C ABI's stream / film / feed calls, built with ThreadSanitizer (tests/native/dropin_mock.cpp;
-no GPU): with 1-3 driving threads, 0-7 helpers, batches of 1-7 tokens, film switches every batch and
-stop_at_next_wave() mid-run, jobs held for larger pushes (push_batch), pushed costliest tile first (cost_order), every job id the TileProvider hands out is pushed into an open feed exactly
-once, the host film counts every sample once, and TSan reports no race."""
+"""The drop-in's host protocol (include/vpt_run.hpp: drain's taker / pusher / film threads around one staged feed,
+run()'s helper threads) over a mock of the C ABI's stream / feed calls, built with ThreadSanitizer
+(tests/native/dropin_mock.cpp; no GPU): with 1-3 driving threads, 0-7 helpers, batches of 1-7 tokens, film
+snapshots every millisecond, stop_at_next_wave() mid-run, tiny run-ahead bounds (hold / backlog) and the cost
+tail on and off, every job id the TileProvider hands out is pushed into an open feed exactly once, the host film
+counts every sample once, and TSan reports no race."""
 import os
 import subprocess
 from pathlib import Path
@@ -18,9 +19,9 @@ CASES = [
     "drivers=3 helpers=2 flush_ms=1 batch=1",
     "drivers=1 helpers=4 stop_after=50 batch=2",
     "drivers=2 helpers=7 batch=1 w=200 h=120 waves=4",
-    "drivers=1 helpers=0 push_batch=100 batch=7",
-    "drivers=1 helpers=0 push_batch=100 cost_order=1 batch=7",
-    "drivers=2 helpers=3 push_batch=37 cost_order=1 batch=5 stop_after=90",
+    "drivers=1 helpers=0 hold=100 cost_tail=0 batch=7",
+    "drivers=1 helpers=0 hold=5 backlog=3 batch=7 flush_ms=1",
+    "drivers=2 helpers=3 hold=37 backlog=11 batch=5 stop_after=90 flush_ms=1",
 ]
 
 

@@ -226,9 +226,10 @@ def test_library_before_torch_keeps_one_hip_runtime():
 @pytest.mark.spawns
 def test_progressive_film_rises_during_the_drain(tmp_path):
     """What main.cpp's 5-FPS window shows (main.cpp:101-132): while the drain renders a full C3 frame
-    (1920x1080, 256 waves, 512^3 stand-in), a thread samples the host film every 10 ms.  With a feed switch
+    (1920x1080, 256 waves, 512^3 stand-in), a thread samples the host film every 10 ms.  With a film snapshot
     every 50 ms the film's sample count rises monotonically through several intermediate values, never ahead
-    of the jobs handed out, and ends with every pixel at 256 samples."""
+    of the jobs handed out, and ends with every pixel at 256 samples.  (flush_ms: the film thread's snapshot
+    period.)"""
     w, h, waves = 1920, 1080, 256
     film, log = _harness(tmp_path, "wdas_cloud.json", w, h, waves, 1, 4096, grid_n=512, flush_ms=50, sample_ms=10)
     samples = [tuple(float(v) for v in line.split()[1:4]) for line in log.splitlines() if line.startswith("sample ")]
@@ -248,8 +249,9 @@ def test_feed_renders_pushed_jobs_in_any_order(mode):
     two streams, the second opened while the first runs (its lanes start as the first's leave, once it is
     closed).  full_grid: the ~2 000 jobs are fewer than the launch's lanes, so it starts at close.
     small_grid (2 blocks, 512 lanes: a 1 024-slot ring): the launch starts after 512 pushes and renders
-    while the host pushes, and pushes wait on the full ring.  staged: the launch copies out its own film
-    (its last block) and vpt_gpu_feed_collect adds it and the counts into a host film."""
+    while the host pushes, and pushes wait on the full ring.  staged: the launch counts its jobs per tile and
+    vpt_gpu_feed_collect adds the film (copied by the copy engines) and the counts into a host film, then
+    clears the device film."""
     import ctypes as C
 
     import torch
@@ -293,7 +295,7 @@ def test_feed_renders_pushed_jobs_in_any_order(mode):
         capi.check(L.vpt_gpu_stream_destroy(it.h, s), "stream destroy")
     if staged:
         total = host
-        # the launches cleared their device films after copying them out
+        # the collects cleared the device films after copying them out
         assert not films[0].any().item() and not films[1].any().item()
     else:
         total = (films[0] + films[1]).cpu().numpy()
@@ -311,10 +313,10 @@ def test_feed_renders_pushed_jobs_in_any_order(mode):
 
 
 @pytest.mark.gpu
-def test_python_run_switches_feeds_every_batch():
-    """render.run (the Python drop-in) with a feed switch after every batch of 7 tokens (flush_seconds 0):
-    many closed / reopened launches on two streams and films, each added into the host film once its
-    launch has ended -- the film equals the oracle's and every sample is counted once."""
+def test_python_run_snapshots_every_batch():
+    """render.run (the Python drop-in) with a progressive-film snapshot after every batch of 7 tokens
+    (flush_seconds 0): many copies of the running launch's film and counts added into the host film, then the
+    collect -- the film equals the oracle's and every sample is counted once."""
     from volume_path_tracer_amd.render import Integrator, TileProvider, run
 
     w, h, waves = 40, 24, 3
@@ -349,3 +351,93 @@ def test_python_run_single_pixel():
     od = O.OracleGrid(dens, fix_majorants=True)
     ref, _, _ = O.render_jobs(wl.cfg, od, None, 0, wl.cfg.jobs_per_wave() * waves)
     np.testing.assert_allclose(film[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_context_waits_refuse_while_a_feed_is_open():
+    """while a feed of the context is launched and not closed, the calls that wait for
+    the context's launches (vpt_gpu_sync, vpt_gpu_film_clear, vpt_gpu_counters, vpt_gpu_set_tuning) return
+    VPT_E_STATE at once instead of waiting for the feed's lanes to give up (30 s) and losing its work.  After
+    the close they succeed, and the feed's film holds every pushed job (oracle, exact counts)."""
+    import ctypes as C
+    import time
+
+    import torch
+
+    from volume_path_tracer_amd import capi
+    from volume_path_tracer_amd.render import Integrator
+
+    VPT_E_STATE = 6
+    wl = workload("c3", width=64, height=48, spp=16, grid_n=64)
+    dens = SynthGrid(1, 64).grid()
+    it = Integrator(wl.cfg, dens, None, device=0)
+    it.set_tuning(grid_blocks=2)  # 512 lanes: the feed launches once 512 of the 768 jobs are pushed
+    L = capi.lib()
+    T = wl.cfg.jobs_per_wave()
+    film = torch.zeros_like(it.film)
+    torch.cuda.synchronize()
+    s, f = C.c_void_p(), C.c_void_p()
+    capi.check(L.vpt_gpu_stream_create(it.h, C.byref(s)), "stream")
+    capi.check(L.vpt_gpu_feed_open(it.h, C.c_void_p(film.data_ptr()), s, 1024, C.byref(f)), "open")
+    jids = np.arange(16 * T, dtype=np.uint64)
+    capi.check(L.vpt_gpu_feed_push(f, jids.ctypes.data_as(C.POINTER(C.c_uint64)), jids.size), "push")  # launched
+    t0 = time.monotonic()
+    assert L.vpt_gpu_sync(it.h) == VPT_E_STATE
+    assert L.vpt_gpu_film_clear(it.h) == VPT_E_STATE
+    assert L.vpt_gpu_set_tuning(it.h, 6, 8, 0, 36, 4) == VPT_E_STATE
+    assert time.monotonic() - t0 < 5.0
+    capi.check(L.vpt_gpu_feed_close(f), "close")
+    capi.check(L.vpt_gpu_feed_destroy(f), "destroy")
+    capi.check(L.vpt_gpu_sync(it.h), "sync after the close")
+    capi.check(L.vpt_gpu_stream_destroy(it.h, s), "stream destroy")
+    out = film.cpu().numpy()
+    np.testing.assert_array_equal(out[..., 3], 16)
+    ref = _oracle_film("c3", 64, 48, 16)
+    np.testing.assert_allclose(out[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_staged_feed_snapshots_add_up_to_the_film():
+    """vpt_gpu_feed_snapshot while the launch renders (the drop-in's progressive film): several snapshots of a
+    running staged feed, then the collect.  The host film's sample counts never exceed the jobs pushed and end
+    exact; its radiance equals the oracle's (the snapshots' additions telescope to the launch's film)."""
+    import ctypes as C
+
+    import torch
+
+    from volume_path_tracer_amd import capi
+    from volume_path_tracer_amd.render import Integrator
+
+    w, h, waves = 96, 64, 48
+    wl = workload("c3", width=w, height=h, spp=waves, grid_n=64)
+    dens = SynthGrid(1, 64).grid()
+    it = Integrator(wl.cfg, dens, None, device=0)
+    it.set_tuning(grid_blocks=4)  # 1 024 lanes: the launch renders while the host pushes
+    L = capi.lib()
+    T = wl.cfg.jobs_per_wave()
+    capi.check(L.vpt_gpu_feed_prepare(it.h, 0, 1), "prepare")
+    s, f = C.c_void_p(), C.c_void_p()
+    capi.check(L.vpt_gpu_stream_create(it.h, C.byref(s)), "stream")
+    torch.cuda.synchronize()
+    capi.check(L.vpt_gpu_feed_open_staged(it.h, C.c_void_p(it.film.data_ptr()), s, 0, C.byref(f)), "open")
+    host = np.zeros((h, w, 4), np.float32)
+    hp = host.ctypes.data_as(C.POINTER(C.c_float))
+    seen = []
+    for wave in range(waves):
+        jids = np.arange(wave * T, (wave + 1) * T, dtype=np.uint64)
+        capi.check(L.vpt_gpu_feed_push(f, jids.ctypes.data_as(C.POINTER(C.c_uint64)), jids.size), "push")
+        b = C.c_uint64()
+        capi.check(L.vpt_gpu_feed_backlog(f, C.byref(b)), "backlog")
+        assert b.value <= (wave + 1) * T
+        if wave % 6 == 5:
+            capi.check(L.vpt_gpu_feed_snapshot(f, hp), "snapshot")
+            assert (host[..., 3] <= wave + 1).all()
+            seen.append(float(host[..., 3].mean()))
+    capi.check(L.vpt_gpu_feed_collect(f, hp), "collect")
+    capi.check(L.vpt_gpu_stream_destroy(it.h, s), "stream destroy")
+    assert all(b >= a for a, b in zip(seen, seen[1:])), seen
+    np.testing.assert_array_equal(host[..., 3], waves)
+    ref = _oracle_film("c3", w, h, waves)
+    np.testing.assert_allclose(host[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
+    # the collect left the feed's film zero
+    assert not it.film.any().item()

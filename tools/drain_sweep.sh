@@ -1,36 +1,35 @@
 #!/bin/bash
-# The drop-in's drain (include/vpt_run.hpp: feeds) on the full C3 frame (1920x1080, 256 waves, 512^3 stand-in),
-# one host thread, across feed windows and film periods; each line: the knobs and render_ms (bench.py's C3 frame
-# is the one-launch reference).  The last run samples what main.cpp's window would show every 50 ms.
+# The drop-in's drain (include/vpt_run.hpp: one staged feed, pusher and film threads) on the full C3 frame
+# (1920x1080, 256 waves, 512^3 stand-in) and the C4 frame, one host thread, across the run-ahead bounds (hold /
+# backlog), the cost tail and the film period; each line: the knobs and render_ms (bench.py's C3 frame is the
+# one-launch reference).  Then the provider alone (mode=tokens: the host-side floor) and a run sampling what
+# main.cpp's window would show every 50 ms.
 # Usage (GPU box): bash tools/drain_sweep.sh <out_dir> [extra harness args]
 set -u
 O=${1:-gpurun_out/drain}; shift || true
 mkdir -p $O
 H=tests/native/build/run_gpu_harness
 run() {
-  local tag=$1; shift
-  timeout -k 10 120 $H config=volume_path_tracer_amd/scenes/wdas_cloud.json out=$O/film_$tag.f32 w=1920 h=1080 waves=256 \
-    grid_n=512 threads=1 batch=4096 "$@" > $O/$tag.log 2>&1 || { echo "$tag failed rc=$?"; tail -3 $O/$tag.log; exit 1; }
-  echo "$tag $* $(grep render_ms $O/$tag.log)"
+  local tag=$1 scene=$2; shift 2
+  local t=0; [ "$scene" = fire ] && t=1
+  timeout -k 10 120 $H config=volume_path_tracer_amd/scenes/$scene.json out=$O/film_$tag.f32 w=1920 h=1080 waves=256 \
+    grid_n=512 threads=1 batch=4096 temperature=$t "$@" > $O/$tag.log 2>&1 || { echo "$tag failed rc=$?"; tail -3 $O/$tag.log; exit 1; }
+  echo "$tag $scene $* $(grep render_ms $O/$tag.log)"
   rm -f $O/film_$tag.f32
 }
-run default "$@"
-run pb0 push_batch=0 "$@"
-run cost cost_order=1 "$@"
-run nof_pb0 flush_ms=100000 push_batch=0 "$@"
-run w18 window=262144 "$@"
-run w20 window=1048576 "$@"
-run f1000 flush_ms=1000 "$@"
-run nof flush_ms=100000 "$@"
-run default2 "$@"
-run s50 sample_ms=50 "$@"
-grep "^sample" $O/s50.log | head -40
-# helper threads taking tokens for the driver (run()'s other worker threads), C3 and C4 (the token-bound one)
-run h3 helpers=3 "$@"
-timeout -k 10 120 $H config=volume_path_tracer_amd/scenes/fire.json out=$O/film_c4.f32 w=1920 h=1080 waves=256 grid_n=512 \
-  threads=1 batch=4096 temperature=1 > $O/c4_h0.log 2>&1 && echo "c4 helpers=0 $(grep render_ms $O/c4_h0.log)"
-timeout -k 10 120 $H config=volume_path_tracer_amd/scenes/fire.json out=$O/film_c4.f32 w=1920 h=1080 waves=256 grid_n=512 \
-  threads=1 batch=4096 temperature=1 push_batch=0 > $O/c4_pb0.log 2>&1 && echo "c4 push_batch=0 $(grep render_ms $O/c4_pb0.log)"
-timeout -k 10 120 $H config=volume_path_tracer_amd/scenes/fire.json out=$O/film_c4.f32 w=1920 h=1080 waves=256 grid_n=512 \
-  threads=1 batch=4096 temperature=1 helpers=3 > $O/c4_h3.log 2>&1 && echo "c4 helpers=3 $(grep render_ms $O/c4_h3.log)"
-rm -f $O/film_c4.f32
+run c3_default wdas_cloud "$@"
+run c3_nofilm wdas_cloud flush_ms=100000 "$@"
+run c3_notail wdas_cloud cost_tail=0 "$@"
+run c3_hold2 wdas_cloud hold=917504 "$@"
+run c3_hold6 wdas_cloud hold=2752512 "$@"
+run c3_backlog_half wdas_cloud backlog=229376 "$@"
+run c3_default2 wdas_cloud "$@"
+run c4_default fire "$@"
+run c4_nofilm fire flush_ms=100000 "$@"
+run c4_default2 fire "$@"
+for th in 1 2; do
+  timeout -k 10 60 $H config=volume_path_tracer_amd/scenes/wdas_cloud.json out=$O/x w=1920 h=1080 waves=256 mode=tokens \
+    threads=$th > $O/tokens_$th.log 2>&1 && echo "provider alone: $(grep tokens_ms $O/tokens_$th.log)"
+done
+run c3_s50 wdas_cloud sample_ms=50 "$@"
+grep "^sample" $O/c3_s50.log | head -40

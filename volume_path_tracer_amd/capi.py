@@ -276,6 +276,10 @@ def lib() -> C.CDLL:
     if hasattr(L, "vpt_gpu_feed_open_staged"):
         L.vpt_gpu_feed_open_staged.argtypes = [vp, vp, vp, C.c_uint64, C.POINTER(vp)]
         L.vpt_gpu_feed_collect.argtypes = [vp, fp]
+    if hasattr(L, "vpt_gpu_feed_snapshot"):
+        L.vpt_gpu_feed_snapshot.argtypes = [vp, fp]
+        L.vpt_gpu_feed_backlog.argtypes = [vp, C.POINTER(C.c_uint64)]
+        L.vpt_gpu_feed_prepare.argtypes = [vp, C.c_uint64, C.c_int]
     _lib = L
     return L
 

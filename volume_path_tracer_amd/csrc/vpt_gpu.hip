@@ -12,7 +12,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <chrono>
 #include <string>
@@ -70,6 +72,9 @@ constexpr uint64_t kFeedEmpty = ~0ULL;
 constexpr int32_t kFeedPending = -2;
 constexpr int32_t kFeedWait = -3;
 constexpr uint32_t kFeedDeadline = 3000000000u;
+// Every kStartedHint-th reserved item is reported to the host (the feed's backlog, vpt_gpu_feed_backlog):
+// one posted write per 1 024 jobs.
+constexpr uint64_t kStartedHint = 1024;
 // LDS copies of the small lookup tables the evaluation reads per lane (logf's 16 x 2 doubles; the
 // temperature kernel's 501 x 3 blackbody table): LDS reads instead of vector-memory loads, which
 // would count in vmcnt with the walk's loads.
@@ -97,14 +102,15 @@ struct KernelEnvT {
   unsigned long long* event_count;
   uint64_t event_cap;
   // Feed mode (vpt_gpu_feed_*: the launch takes job ids the host pushes while it runs): host-pinned
-  // coherent memory shared with the host -- the published word (items published | kFeedClosed) and
-  // the ring of job ids (kFeedEmpty once read) -- and an error word in device memory.  nullptr:
-  // items are job_counter values < jid_count (every other launch).
+  // coherent memory shared with the host -- the published word (items published | kFeedClosed), the
+  // ring of job ids (kFeedEmpty once read), the error word and the started hint.  nullptr: items are
+  // job_counter values < jid_count (every other launch).
   const uint64_t* feed_word;
   uint64_t* feed_ring;
   uint64_t feed_mask;                // ring slots - 1 (a power of two)
   unsigned* feed_error;
-  float* feed_staged;                // a staged feed: the film's host-pinned copy, written by the last block
+  uint64_t* feed_started;            // a lane that reserves item k, k % kStartedHint == 0, stores k here
+  uint32_t* tile_done;               // a staged feed: jobs completed per tile (device memory), else nullptr
 
   // Adds w for every active lane with w != 0 (w uniform per call site) to a workgroup counter.
   __device__ __forceinline__ void tally(int32_t k, int32_t w) {
@@ -233,8 +239,8 @@ struct KernelEnvT {
   __device__ int fetch_feed(uint64_t& j) {
     LaneCold& lc = cold();
     const uint32_t now = (uint32_t)__builtin_amdgcn_s_memrealtime();  // 100 MHz
-    // Relaxed system-scope loads of host memory go to the host every time; the slot is read only after
-    // the word has shown it published (a control dependency), and the host wrote it before the word.
+    // System-scope loads of host memory go to the host every time.  The host writes a slot before the word
+    // that publishes it (release); the slot is read after an acquire fence that follows the word's load.
     const uint64_t w = __hip_atomic_load(feed_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint64_t published = w & ~kFeedClosed;
     if (lc.pix != kFeedPending) {
@@ -250,6 +256,8 @@ struct KernelEnvT {
         return -1;
       }
       const uint64_t k = atomicAdd(job_counter, 1ULL);
+      // the host's backlog estimate (vpt_gpu_feed_backlog): a posted write every kStartedHint items
+      if ((k & (kStartedHint - 1)) == 0) __hip_atomic_store(feed_started, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       lc.item_lo = (uint32_t)k;
       lc.item_hi = (uint32_t)(k >> 32);
       if (lc.pix != kFeedWait) lc.x0 = (int32_t)now;  // wait start
@@ -258,7 +266,13 @@ struct KernelEnvT {
     const uint64_t k = ((uint64_t)lc.item_hi << 32) | lc.item_lo;
     if (k < published) {
       uint64_t* slot = feed_ring + (k & feed_mask);
+      // Acquire after the word's load: the slot's load cannot be satisfied before it (ADVICE / VERDICT r04).
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       j = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      // And by construction: a slot holds kFeedEmpty from the lane's mark until the host's next id, and the
+      // host writes that id only after it has seen the mark, so a slot read too early can only return
+      // kFeedEmpty -- never another job's id.  Such a lane keeps its item and asks again.
+      if (j == kFeedEmpty) return -1;
       // The empty mark is stored only once the id has arrived (a posted write may overtake a read on the
       // host link, and the host reuses the slot as soon as it sees the mark): the asm takes j as an input,
       // so the compiler waits for the load before it.
@@ -274,6 +288,12 @@ struct KernelEnvT {
       return 0;
     }
     return -1;
+  }
+  // A job's last pixel is done: a staged feed counts it for its tile (the film's sample counts are the host's
+  // per-tile job counts, vpt_gpu_feed_snapshot / _collect).  Once per job (64 samples); a uniform branch.
+  __device__ __forceinline__ void job_end(const DevScene& S, const LaneCold& lc) {
+    if (!RegCold && tile_done)
+      atomicAdd(tile_done + (uint32_t)(lc.y0 / S.th) * S.ntx + (uint32_t)(lc.x0 / S.tw), 1u);
   }
   __device__ __forceinline__ void film_add(const DevScene& S, const Lane& ln, int32_t px, int32_t py, int32_t rw) {
     float* f = film + ((int64_t)py * S.W + px) * 4;
@@ -301,28 +321,6 @@ using KernelEnv = KernelEnvT<false>;
 
 
 // counters[] order = vpt_counters field order
-// A staged feed's retirement, run by the launch's last block once every block has ended: the film is
-// copied into the feed's host-pinned buffer and cleared, inside the launch -- nothing is queued behind it,
-// where a copy or fill could wait for the CUs the next feed's launch holds (r04 fd: 34 s).  The host adds
-// the sample counts it kept per tile when it collects the copy (vpt_gpu_feed_collect).
-__device__ __forceinline__ void feed_retire(const KernelEnv& env, const DevScene& S) {
-  __shared__ int last;
-  __threadfence();  // this thread's film adds are done device-wide before its block counts as ended
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(env.event_count, 1ULL) == (unsigned long long)gridDim.x - 1;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();  // every block's adds are visible to this block's loads
-  float4* film = reinterpret_cast<float4*>(env.film);
-  float4* out = reinterpret_cast<float4*>(env.feed_staged);
-  const uint64_t n = (uint64_t)S.W * (uint64_t)S.H;
-  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const float4 v = film[i];
-    out[i] = v;
-    film[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  }
-}
-
 template <bool HasTemp, bool Debug, bool Runs, bool Lat = false>
 __global__ __launch_bounds__(kBlockThreads, Lat ? VPT_WAVES_LAT : (Debug ? VPT_WAVES_SLOW : (HasTemp ? VPT_WAVES_TEMP : VPT_WAVES_FAST))) void vpt_integrate_kernel(const DevScene* scene, KernelEnvT<Lat> env,
                                                                        unsigned long long* counters) {
@@ -367,8 +365,6 @@ __global__ __launch_bounds__(kBlockThreads, Lat ? VPT_WAVES_LAT : (Debug ? VPT_W
 #if defined(VPT_PROFILE) || defined(VPT_PROFILE_TIME)
   if (threadIdx.x < PT_COUNT) atomicAdd(env.prof_buf + 2 * PB_COUNT + threadIdx.x, wg_prof[threadIdx.x]);
 #endif
-  if constexpr (!Debug && !Lat)
-    if (env.feed_staged) feed_retire(env, *scene);
 }
 
 // The film's sample-count channel for the job range [jid_begin, jid_begin + jid_count): a pixel of
@@ -551,7 +547,8 @@ struct FeedLaunch {
   uint64_t* ring;
   uint64_t mask;
   unsigned* error;
-  float* staged;  // nullptr unless a staged feed
+  uint64_t* started;
+  uint32_t* tile_done;  // nullptr unless a staged feed
 };
 }  // namespace vpt
 
@@ -601,7 +598,13 @@ struct vpt_gpu_ctx {
   // that launch -- i.e. until its lanes give up -- so a feed's memory is allocated once and freed with
   // the context.
   std::vector<vpt_gpu_feed*> feed_pool;
-  int lat_mode = -1;               // latency kernel: -1 auto (launches of <= lat_per_cu blocks per CU), 0 off, 1 on
+  // Feeds launched and not yet closed: a call that waits for the context's launches (wait_ctx) would wait
+  // for such a feed's lanes to give up (30 s) and lose its work, so those calls refuse while it is > 0.
+  std::atomic<int> open_feeds{0};
+  // Pinned zeros: staged feeds clear their film and tile counts with host-to-device copies, which the copy
+  // engines run beside a launch that holds every CU (a fill kernel would wait for it; r05a probe).
+  float* zeros = nullptr;
+  int lat_mode = -1;              // latency kernel: -1 auto (launches of <= lat_per_cu blocks per CU), 0 off, 1 on
   int lat_ungated = 0;             // its partly filled launches read the latency gates (1) or the context's (0)
   int lat_per_cu = 1;              // resident blocks per CU of the latency kernel
 };
@@ -660,6 +663,9 @@ int release_slot(vpt_gpu_ctx* ctx, hipStream_t s, uint32_t slot) {
 // The events are snapshotted under the lock and waited for after it is released, so a wait never
 // blocks another thread's take_slot.
 int wait_ctx(vpt_gpu_ctx* ctx) {
+  if (ctx->open_feeds.load() > 0)
+    return vpt::set_error(VPT_E_STATE, "a feed of this context is open: close it before calls that wait for the "
+                                       "context's launches (ADVICE r04)");
   hipEvent_t ev[kLaunchSlots];
   uint32_t n = 0;
   {
@@ -725,6 +731,8 @@ int rank_tiles(vpt_gpu_ctx* ctx) {
 // Tile costs (vpt_tile_cost_kernel) and the descending-cost tile ranks, once per context.
 int ensure_order(vpt_gpu_ctx* ctx) {
   if (ctx->order) return VPT_OK;
+  if (ctx->open_feeds.load() > 0)  // the cost pass and its copy would wait for the feed's launch
+    return vpt::set_error(VPT_E_STATE, "tile costs: a feed of this context is open (compute them before)");
   const uint64_t T = ctx->scene.T;
   float* cost = nullptr;
   VPT_HIP(hipMalloc((void**)&cost, T * sizeof(float)));
@@ -850,7 +858,8 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.feed_ring = feed ? feed->ring : nullptr;
   env.feed_mask = feed ? feed->mask : 0;
   env.feed_error = feed ? feed->error : nullptr;
-  env.feed_staged = feed ? feed->staged : nullptr;
+  env.feed_started = feed ? feed->started : nullptr;
+  env.tile_done = feed ? feed->tile_done : nullptr;
   env.event_count = ctx->job_counter + 2 * slot + 1;
   env.event_cap = event_cap;
   if (slot_out) *slot_out = slot;
@@ -1222,33 +1231,47 @@ int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* ctx, float* film_device, float* film
 }  // extern "C"
 
 // A feed: one launch of the production kernel that renders job ids as the host pushes them (see
-// include/vpt_gpu.h).  Its host-pinned, coherent block holds the published word, then the ring of
-// job ids, then the per-tile job counts the close adds to the film's sample-count channel.
+// include/vpt_gpu.h).  Its host-pinned, coherent block holds the published word, the error word and the
+// started hint, then the ring of job ids, then the per-tile job counts pushed.
 struct vpt_gpu_feed {
   vpt_gpu_ctx* ctx = nullptr;
   hipStream_t stream = nullptr;
   float* film = nullptr;
-  uint64_t* block = nullptr;  // hipHostMalloc'd: [8] word, error word, padding; [cap] ring; uint32 counts[T]
+  uint64_t* block = nullptr;  // hipHostMalloc'd: [8] word, error word, started hint, padding; [cap] ring; uint32 counts[T]
   uint64_t* word = nullptr;
-  uint32_t* error = nullptr;  // block[1]: a lane that gave up waiting stores 1 here
+  uint32_t* error = nullptr;    // block[1]: a lane that gave up waiting stores 1 here
+  uint64_t* started = nullptr;  // block[2]: the last reported reserved item (kStartedHint)
   uint64_t* ring = nullptr;
   uint32_t* counts = nullptr;
-  float* staged = nullptr;  // hipHostMalloc'd film_count floats: a staged feed's film, copied by its launch
   bool stage = false;
+  // Staged feeds: the launch counts the jobs it completes per tile in device memory; snapshots and the final
+  // collect copy that and the film into pinned memory with the copy engines (beside the launch, which holds
+  // every CU) and add what is new since the previous copy into the caller's film.
+  uint32_t* done_dev = nullptr;   // uint32[T]
+  float* pin_film = nullptr;      // film_count floats, pinned
+  uint32_t* pin_done = nullptr;   // uint32[T], pinned
+  std::vector<float> shown;       // the film as already added to the caller's film
+  std::vector<uint32_t> shown_done;
+  hipStream_t copy_stream = nullptr;
+  hipStream_t own_stream = nullptr;  // a staged feed's launch stream when the caller passes none
+  bool ring_clean = false;           // every slot holds kFeedEmpty (a completed feed's lanes marked them all)
   uint64_t cap = 0;
   uint64_t published = 0;
+  uint64_t started_seen = 0;
   hipEvent_t closed_ev = nullptr;
   bool closed = false;
   bool launched = false;     // the launch starts once launch_at items are published, or at close
+  bool counted = false;      // counted in ctx->open_feeds (launched, not closed)
   uint64_t launch_at = 0;
   vpt::FeedLaunch fl{};
 };
 
 namespace {
 constexpr double kFeedHostWaitS = 120.0;  // a push waiting this long for a ring slot gives up
+constexpr size_t kZeroBytes = 4u << 20;   // the context's pinned zeros (staged feeds' clears)
 
-// VPT_FEED_TRACE=1: one stderr line per feed event (open / close / a push's wait for a ring slot / the
-// end of its work), milliseconds since the first event -- for diagnosing a drop-in's host protocol.
+// VPT_FEED_TRACE=1: one stderr line per feed event (open / launch / close / a push's wait for a ring slot /
+// snapshots / the end of its work), milliseconds since the first event -- for diagnosing a drop-in's protocol.
 void feed_trace(const vpt_gpu_feed* f, const char* what, double a = 0, double b = 0) {
   static const bool on = std::getenv("VPT_FEED_TRACE") && std::atoi(std::getenv("VPT_FEED_TRACE")) > 0;
   if (!on) return;
@@ -1261,14 +1284,20 @@ void feed_free(vpt_gpu_feed* f) {
   if (!f) return;
   (void)hipSetDevice(f->ctx->device);
   if (f->closed_ev) (void)hipEventDestroy(f->closed_ev);
+  if (f->copy_stream) (void)hipStreamDestroy(f->copy_stream);
+  if (f->own_stream) (void)hipStreamDestroy(f->own_stream);
   (void)hipHostFree(f->block);
-  if (f->staged) (void)hipHostFree(f->staged);
+  if (f->pin_film) (void)hipHostFree(f->pin_film);
+  if (f->pin_done) (void)hipHostFree(f->pin_done);
+  (void)hipFree(f->done_dev);
   delete f;
 }
 
 void feed_pool_free(vpt_gpu_ctx* ctx) {
   for (vpt_gpu_feed* f : ctx->feed_pool) feed_free(f);
   ctx->feed_pool.clear();
+  if (ctx->zeros) (void)hipHostFree(ctx->zeros);
+  ctx->zeros = nullptr;
 }
 
 // Publishes items [0, published) and, with close, the end of the feed (release: the ring and count
@@ -1276,66 +1305,97 @@ void feed_pool_free(vpt_gpu_ctx* ctx) {
 void feed_publish(vpt_gpu_feed* f, bool close) {
   __atomic_store_n(f->word, f->published | (close ? vpt::kFeedClosed : 0), __ATOMIC_RELEASE);
 }
-}  // namespace
 
-extern "C" {
+// Zeroes `bytes` of device memory with host-to-device copies of the context's pinned zeros, enqueued on s:
+// copy-engine work, which runs while another launch holds every CU (a fill kernel would wait for it).
+int clear_by_copy(vpt_gpu_ctx* ctx, void* dev, size_t bytes, hipStream_t s) {
+  if (!ctx->zeros) {
+    VPT_HIP(hipHostMalloc((void**)&ctx->zeros, kZeroBytes, hipHostMallocDefault));
+    std::memset(ctx->zeros, 0, kZeroBytes);
+  }
+  for (size_t off = 0; off < bytes; off += kZeroBytes)
+    VPT_HIP(hipMemcpyAsync(static_cast<char*>(dev) + off, ctx->zeros, std::min(kZeroBytes, bytes - off),
+                           hipMemcpyHostToDevice, s));
+  return VPT_OK;
+}
 
-}  // extern "C"
+// The resources of a feed of ring size cap (and, staged, its copy-out buffers), from the context's pool or new.
+int feed_get(vpt_gpu_ctx* ctx, uint64_t cap, bool stage, std::unique_ptr<vpt_gpu_feed, void (*)(vpt_gpu_feed*)>& f) {
+  for (size_t i = 0; i < ctx->feed_pool.size(); ++i)
+    if (ctx->feed_pool[i]->cap == cap && (!stage || ctx->feed_pool[i]->done_dev)) {  // a pooled feed of this window
+      f.reset(ctx->feed_pool[i]);
+      ctx->feed_pool.erase(ctx->feed_pool.begin() + (ptrdiff_t)i);
+      return VPT_OK;
+    }
+  f.reset(new vpt_gpu_feed());
+  f->ctx = ctx;
+  f->cap = cap;
+  const uint64_t T = ctx->scene.T;
+  const size_t bytes = (8 + cap) * sizeof(uint64_t) + T * sizeof(uint32_t);
+  VPT_HIP(hipHostMalloc((void**)&f->block, bytes, hipHostMallocCoherent | hipHostMallocMapped));
+  f->word = f->block;
+  f->error = reinterpret_cast<uint32_t*>(f->block + 1);
+  f->started = f->block + 2;
+  f->ring = f->block + 8;  // its own cache lines, away from the words the waiting wavefronts poll
+  f->counts = reinterpret_cast<uint32_t*>(f->ring + cap);
+  VPT_HIP(hipEventCreateWithFlags(&f->closed_ev, hipEventDisableTiming));
+  if (stage) {
+    VPT_HIP(hipMalloc((void**)&f->done_dev, T * sizeof(uint32_t)));
+    VPT_HIP(hipHostMalloc((void**)&f->pin_film, ctx->film_count * sizeof(float), hipHostMallocDefault));
+    VPT_HIP(hipHostMalloc((void**)&f->pin_done, T * sizeof(uint32_t), hipHostMallocDefault));
+    VPT_HIP(hipStreamCreateWithFlags(&f->copy_stream, hipStreamNonBlocking));
+    VPT_HIP(hipStreamCreateWithFlags(&f->own_stream, hipStreamNonBlocking));
+    f->shown.assign(ctx->film_count, 0.0f);
+    f->shown_done.assign(T, 0u);
+    if (int rc = clear_by_copy(ctx, f->done_dev, T * sizeof(uint32_t), f->copy_stream)) return rc;
+    VPT_HIP(hipStreamSynchronize(f->copy_stream));
+  }
+  return VPT_OK;
+}
 
-namespace {
-int feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t window, bool stage, vpt_gpu_feed** out) {
-  if (!ctx || !out || !hip_stream) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_open: null argument");
-  *out = nullptr;
-  if (ctx->scene.pixel_mode) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_open: feeds run the reference RNG mode");
-  int rc = ctx_device(ctx);
-  if (rc) return rc;
+uint64_t feed_cap(const vpt_gpu_ctx* ctx, uint64_t window) {
   // The ring holds at least twice the launch's lanes: a lane reserves an item only while some are
   // published, so reservations lead the consumed items by at most the lanes, and the host keeps pushing
   // while the lanes it has already fed work (C3: 458 752 lanes, ring 2^20).
   const uint64_t lanes = (uint64_t)ctx->grid_blocks * vpt::kBlockThreads;
   uint64_t cap = 1024;
   while ((cap < window || cap < 2 * lanes) && cap < (1ULL << 26)) cap <<= 1;
+  return cap;
+}
+}  // namespace
+
+namespace {
+int feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t window, bool stage, vpt_gpu_feed** out) {
+  if (!ctx || !out || (!hip_stream && !stage)) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_open: null argument");
+  *out = nullptr;
+  if (ctx->scene.pixel_mode) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_open: feeds run the reference RNG mode");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  const uint64_t cap = feed_cap(ctx, window);
   std::unique_ptr<vpt_gpu_feed, void (*)(vpt_gpu_feed*)> f(nullptr, feed_free);
-  for (size_t i = 0; i < ctx->feed_pool.size(); ++i)
-    if (ctx->feed_pool[i]->cap == cap) {  // a pooled feed of this window
-      f.reset(ctx->feed_pool[i]);
-      ctx->feed_pool.erase(ctx->feed_pool.begin() + (ptrdiff_t)i);
-      break;
-    }
-  if (!f) {
-    f.reset(new vpt_gpu_feed());
-    f->ctx = ctx;
-    f->cap = cap;
-    const size_t bytes = (8 + cap) * sizeof(uint64_t) + ctx->scene.T * sizeof(uint32_t);
-    VPT_HIP(hipHostMalloc((void**)&f->block, bytes, hipHostMallocCoherent | hipHostMallocMapped));
-    f->word = f->block;
-    f->error = reinterpret_cast<uint32_t*>(f->block + 1);
-    f->ring = f->block + 8;  // its own cache lines, away from the word the waiting wavefronts poll
-    f->counts = reinterpret_cast<uint32_t*>(f->ring + cap);
-    VPT_HIP(hipEventCreateWithFlags(&f->closed_ev, hipEventDisableTiming));
-  }
-  if (stage && !f->staged)
-    VPT_HIP(hipHostMalloc((void**)&f->staged, ctx->film_count * sizeof(float), hipHostMallocDefault));
+  if ((rc = feed_get(ctx, cap, stage, f))) return rc;
   f->stage = stage;
-  f->stream = (hipStream_t)hip_stream;
+  f->stream = hip_stream ? (hipStream_t)hip_stream : f->own_stream;  // (staged: the feed's own stream if none)
   f->film = film_device ? film_device : ctx->film;
   f->published = 0;
+  f->started_seen = 0;
   f->closed = false;
-  for (uint64_t i = 0; i < cap; ++i) f->ring[i] = vpt::kFeedEmpty;
+  f->counted = false;
+  if (!f->ring_clean)
+    for (uint64_t i = 0; i < cap; ++i) f->ring[i] = vpt::kFeedEmpty;
+  f->ring_clean = false;
   std::memset(f->counts, 0, ctx->scene.T * sizeof(uint32_t));
   __atomic_store_n(f->error, 0u, __ATOMIC_RELAXED);
+  __atomic_store_n(f->started, 0ULL, __ATOMIC_RELAXED);
   __atomic_store_n(f->word, 0ULL, __ATOMIC_RELEASE);
-  uint64_t *word_dev = nullptr, *ring_dev = nullptr;
+  uint64_t* word_dev = nullptr;
   VPT_HIP(hipHostGetDevicePointer((void**)&word_dev, f->word, 0));
-  ring_dev = word_dev + 8;
-  float* staged_dev = nullptr;
-  if (stage) VPT_HIP(hipHostGetDevicePointer((void**)&staged_dev, f->staged, 0));
-  f->fl = vpt::FeedLaunch{word_dev, ring_dev, cap - 1, reinterpret_cast<unsigned*>(word_dev + 1), staged_dev};
+  f->fl = vpt::FeedLaunch{word_dev, word_dev + 8, cap - 1, reinterpret_cast<unsigned*>(word_dev + 1), word_dev + 2,
+                          stage ? f->done_dev : nullptr};
   // The launch is deferred until the ring holds as many items as it has lanes (or the feed is closed):
-  // launched at once, every lane would find the first few published items and reserve past them, and a
-  // lane holding an unpublished item pins its ring slot until its (gated) fetch block runs again.
+  // launched at once, its idle wavefronts would poll the host link for work (r04).
   f->launched = false;
-  f->launch_at = lanes;
+  f->launch_at = (uint64_t)ctx->grid_blocks * vpt::kBlockThreads;
   feed_trace(f.get(), stage ? "open_stg" : "open", (double)cap, (double)(uintptr_t)hip_stream);
   *out = f.release();
   return VPT_OK;
@@ -1344,12 +1404,83 @@ int feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t w
 int feed_launch(vpt_gpu_feed* f) {
   if (f->launched) return VPT_OK;
   f->launched = true;
+  if (!f->closed) {  // launched and open: it holds the device until it is closed
+    ++f->ctx->open_feeds;
+    f->counted = true;
+  }
   feed_trace(f, "launch", (double)f->published);
   return render(f->ctx, 0, ~0ULL >> 1, f->film, nullptr, f->stream, nullptr, 0, nullptr, &f->fl);
 }
 
-// Waits for a closed feed's work; with film_host, adds its staged film there.  The feed goes back to the
-// context's pool unless a HIP failure leaves its launch possibly still reading the block (then it leaks).
+// film_host += (the staged feed's film and per-tile counts as copied to pin_film / pin_done) - (what was added
+// before), rows split over a few threads; shown := the copy.  Counts are integers (exact); the radiance
+// channels telescope to the final film (the first add onto zero is exact).
+void add_delta(vpt_gpu_feed* f, float* film_host) {
+  const vpt::DevScene& S = f->ctx->scene;
+  const uint64_t T = S.T;
+  std::vector<uint32_t> dc(T);
+  for (uint64_t t = 0; t < T; ++t) {
+    // (a copy taken beside the launch reads memory, not the dirty L2 lines: it may lag, never lead; the max
+    // keeps the counts monotone should an older value be read after a newer one)
+    const uint32_t now = std::max(f->pin_done[t], f->shown_done[t]);
+    dc[t] = now - f->shown_done[t];
+    f->shown_done[t] = now;
+  }
+  auto rows = [&](int32_t y0, int32_t y1) {
+    for (int32_t y = y0; y < y1; ++y) {
+      const uint32_t* dct = dc.data() + (uint64_t)(y / S.th) * S.ntx;
+      for (int32_t x = 0; x < S.W; ++x) {
+        const uint64_t p = ((uint64_t)y * (uint64_t)S.W + (uint64_t)x) * 4;
+        const bool counted = !S.single_pixel_enabled || (x == S.sp_x && y == S.sp_y);
+        for (int c = 0; c < 3; ++c) {
+          const float v = f->pin_film[p + c];
+          film_host[p + c] += v - f->shown[p + c];
+          f->shown[p + c] = v;
+        }
+        if (counted) film_host[p + 3] += (float)dct[x / S.tw];
+      }
+    }
+  };
+  const int32_t H = S.H;
+  const unsigned hw = std::thread::hardware_concurrency();
+  const int nt = (int)std::max(1u, std::min(8u, hw ? hw : 1u));
+  if (nt == 1 || (uint64_t)S.W * (uint64_t)H < (1u << 16)) {
+    rows(0, H);
+    return;
+  }
+  std::vector<std::thread> pool;
+  for (int i = 1; i < nt; ++i) pool.emplace_back(rows, (int32_t)((int64_t)H * i / nt), (int32_t)((int64_t)H * (i + 1) / nt));
+  rows(0, (int32_t)((int64_t)H / nt));
+  for (auto& t : pool) t.join();
+}
+
+// Copies a staged feed's film and per-tile counts with the copy engines and adds what is new into film_host.
+// after_end: ordered after the feed's launch (exact); else beside it (what it has completed so far).
+int feed_snapshot(vpt_gpu_feed* f, float* film_host, bool after_end, const std::function<int()>& then = {}) {
+  vpt_gpu_ctx* ctx = f->ctx;
+  if (after_end) VPT_HIP(hipStreamWaitEvent(f->copy_stream, f->closed_ev, 0));
+  // counts first: a job counted here has added its samples before (in its lane's order)
+  feed_trace(f, after_end ? "final0" : "snap0");
+  VPT_HIP(hipMemcpyAsync(f->pin_done, f->done_dev, ctx->scene.T * sizeof(uint32_t), hipMemcpyDeviceToHost, f->copy_stream));
+  VPT_HIP(hipMemcpyAsync(f->pin_film, f->film, ctx->film_count * sizeof(float), hipMemcpyDeviceToHost, f->copy_stream));
+  hipEvent_t copied = nullptr;
+  VPT_HIP(hipEventCreateWithFlags(&copied, hipEventDisableTiming));
+  hipError_t e = hipEventRecord(copied, f->copy_stream);
+  int rc = VPT_OK;
+  if (e == hipSuccess && then) rc = then();  // queued after the copy: runs while the host adds it
+  if (e == hipSuccess) e = hipEventSynchronize(copied);
+  (void)hipEventDestroy(copied);
+  if (e != hipSuccess) return vpt::set_error(VPT_E_HIP, std::string("feed snapshot copy: ") + hipGetErrorString(e));
+  if (rc) return rc;
+  feed_trace(f, "copied");
+  add_delta(f, film_host);
+  feed_trace(f, after_end ? "final" : "snapshot");
+  return VPT_OK;
+}
+
+// Waits for a closed feed's work; a staged feed then adds its film into film_host (when given) and clears its
+// film and counts for the next use.  The feed goes back to the context's pool unless a HIP failure leaves its
+// launch possibly still reading the block (then it leaks).
 int feed_finish(vpt_gpu_feed* f, float* film_host) {
   bool complete = false;
   int rc = VPT_OK;
@@ -1362,22 +1493,28 @@ int feed_finish(vpt_gpu_feed* f, float* film_host) {
   feed_trace(f, "ended", (double)f->published, complete ? (double)__atomic_load_n(f->error, __ATOMIC_ACQUIRE) : -1.0);
   if (complete && __atomic_load_n(f->error, __ATOMIC_ACQUIRE))
     rc = vpt::set_error(VPT_E_STATE, "vpt_gpu_feed_destroy: lanes of the feed's launch gave up waiting for jobs");
-  if (rc == VPT_OK && film_host) {
-    // the launch's last block copied the film here; the sample counts are the jobs pushed per tile (the
-    // same integer sums as vpt_count_kernel's; single_pixel: that pixel only)
-    const vpt::DevScene& S = f->ctx->scene;
-    const float* src = f->staged;
-    for (int32_t y = 0; y < S.H; ++y)
-      for (int32_t x = 0; x < S.W; ++x) {
-        const uint64_t p = ((uint64_t)y * (uint64_t)S.W + (uint64_t)x) * 4;
-        const bool counted = !S.single_pixel_enabled || (x == S.sp_x && y == S.sp_y);
-        const uint32_t n = counted ? f->counts[(uint64_t)(y / S.th) * S.ntx + (uint64_t)(x / S.tw)] : 0u;
-        film_host[p] += src[p];
-        film_host[p + 1] += src[p + 1];
-        film_host[p + 2] += src[p + 2];
-        film_host[p + 3] += src[p + 3] + (float)n;
-      }
+  if (complete && f->stage) {
+    vpt_gpu_ctx* ctx = f->ctx;
+    // the final copy; then the film and counts back to zero (copy engines, queued behind the copy on the same
+    // stream) while the host adds the copy; nothing shown afterwards
+    auto clear = [&] {
+      int r = clear_by_copy(ctx, f->film, ctx->film_count * sizeof(float), f->copy_stream);
+      return r ? r : clear_by_copy(ctx, f->done_dev, ctx->scene.T * sizeof(uint32_t), f->copy_stream);
+    };
+    if (rc == VPT_OK && film_host) {
+      rc = feed_snapshot(f, film_host, true, clear);
+    } else {
+      const int r = clear();
+      if (rc == VPT_OK) rc = r;
+    }
+    if (hipStreamSynchronize(f->copy_stream) != hipSuccess && rc == VPT_OK)
+      rc = vpt::set_error(VPT_E_HIP, "vpt_gpu_feed_collect: clearing the film failed");
+    std::fill(f->shown.begin(), f->shown.end(), 0.0f);
+    std::fill(f->shown_done.begin(), f->shown_done.end(), 0u);
+    feed_trace(f, "cleared");
   }
+  // a completed feed's lanes marked every published slot empty (unpublished ones still are)
+  f->ring_clean = complete && rc == VPT_OK;
   if (complete) f->ctx->feed_pool.push_back(f);
   return rc;
 }
@@ -1394,38 +1531,62 @@ int vpt_gpu_feed_open_staged(vpt_gpu_ctx* ctx, float* film_device, void* hip_str
   return feed_open(ctx, film_device, hip_stream, window, true, out);
 }
 
+int vpt_gpu_feed_prepare(vpt_gpu_ctx* ctx, uint64_t window, int staged) {
+  if (!ctx) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_prepare: null context");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  std::unique_ptr<vpt_gpu_feed, void (*)(vpt_gpu_feed*)> f(nullptr, feed_free);
+  if ((rc = feed_get(ctx, feed_cap(ctx, window), staged != 0, f))) return rc;
+  if (staged && (rc = clear_by_copy(ctx, ctx->zeros, 0, f->copy_stream))) return rc;  // (allocates the zeros)
+  ctx->feed_pool.push_back(f.release());
+  return VPT_OK;
+}
+
 int vpt_gpu_feed_push(vpt_gpu_feed* f, const uint64_t* jids, uint64_t n) {
   if (!f || (n && !jids)) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_push: null argument");
   if (f->closed) return vpt::set_error(VPT_E_STATE, "vpt_gpu_feed_push: the feed is closed");
-  const uint64_t T = f->ctx->scene.T;
-  const auto t0 = std::chrono::steady_clock::now();
+  const uint64_t T = f->ctx->scene.T, mask = f->cap - 1;
+  const bool count = !f->stage;  // (a staged feed's launch counts its completed jobs itself)
   for (uint64_t i = 0; i < n; ++i) {
     const uint64_t jid = jids[i];
     if (jid >> 62) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_push: job id out of range");
-    uint64_t* slot = f->ring + (f->published & (f->cap - 1));
+    // The ring's lines were last written by the lanes (their empty marks): each is a miss in the host's
+    // caches, so they are fetched 32 lines ahead (r05: the pusher, not the provider, bounded C4's drain).
+    if ((f->published & 7) == 0) __builtin_prefetch(f->ring + ((f->published + 256) & mask), 1);
+    uint64_t* slot = f->ring + (f->published & mask);
     if (__atomic_load_n(slot, __ATOMIC_ACQUIRE) != vpt::kFeedEmpty) {
       // the window is full (cap items published and not yet started): publish what we have, then wait --
       // spinning first (slots free at the GPU's job rate, tens of millions a second: a sleep between
-      // checks would hold the lanes back), sleeping once the wait is long (a launch not yet started)
+      // checks would hold the lanes back), sleeping once the wait is long (a launch not yet started).  The
+      // limit counts from the start of this wait, not of the call.
       feed_publish(f, false);
       if (int rc = feed_launch(f)) return rc;
       const auto w0 = std::chrono::steady_clock::now();
       for (uint32_t spins = 0; __atomic_load_n(slot, __ATOMIC_ACQUIRE) != vpt::kFeedEmpty; ++spins) {
         if (spins < (1u << 16)) continue;
         std::this_thread::sleep_for(std::chrono::microseconds(20));
-        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kFeedHostWaitS)
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count() > kFeedHostWaitS)
           return vpt::set_error(VPT_E_STATE, "vpt_gpu_feed_push: the feed's launch stopped taking jobs");
       }
       const double waited = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
       if (waited > 1.0) feed_trace(f, "slotwait", (double)f->published, waited);
     }
     *slot = jid;
-    ++f->counts[jid % T];
+    if (count) ++f->counts[jid % T];
     ++f->published;
   }
   feed_publish(f, false);
   if (f->published >= f->launch_at)
     if (int rc = feed_launch(f)) return rc;
+  return VPT_OK;
+}
+
+int vpt_gpu_feed_backlog(vpt_gpu_feed* f, uint64_t* backlog) {
+  if (!f || !backlog) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_backlog: null argument");
+  // the newest reported reservation (the lanes' posted writes may land out of order: keep the largest)
+  const uint64_t s = __atomic_load_n(f->started, __ATOMIC_RELAXED);
+  if (s > f->started_seen) f->started_seen = s;
+  *backlog = f->published > f->started_seen ? f->published - f->started_seen : 0;
   return VPT_OK;
 }
 
@@ -1437,8 +1598,13 @@ int vpt_gpu_feed_close(vpt_gpu_feed* f) {
   f->closed = true;
   feed_publish(f, true);
   feed_trace(f, "close", (double)f->published);
-  if ((rc = feed_launch(f))) return rc;
-  if (f->stage) {  // the launch retires its own film; the host adds the counts at collect
+  rc = feed_launch(f);
+  if (f->counted) {  // closed: its launch ends once its jobs are done
+    --f->ctx->open_feeds;
+    f->counted = false;
+  }
+  if (rc) return rc;
+  if (f->stage) {  // the host adds the film and the counts at collect (copy engines)
     VPT_HIP(hipEventRecord(f->closed_ev, f->stream));
     return VPT_OK;
   }
@@ -1473,6 +1639,14 @@ int vpt_gpu_feed_destroy(vpt_gpu_feed* f) {
   if (!f) return VPT_OK;
   const int rc = vpt_gpu_feed_close(f);
   return rc ? rc : feed_finish(f, nullptr);
+}
+
+int vpt_gpu_feed_snapshot(vpt_gpu_feed* f, float* film_host) {
+  if (!f || !film_host) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_snapshot: null argument");
+  if (!f->stage) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_snapshot: not a staged feed (vpt_gpu_feed_open_staged)");
+  int rc = ctx_device(f->ctx);
+  if (rc) return rc;
+  return feed_snapshot(f, film_host, false);
 }
 
 int vpt_gpu_feed_collect(vpt_gpu_feed* f, float* film_host) {

@@ -219,35 +219,8 @@ __host__ __device__ __forceinline__ void fetch_stencil(const DevGrid& g, Cell c,
 
 // TrilinearSampler::sample: lerp(a, b, w) = a + w * (b - a), z then y then x.
 __host__ __device__ __forceinline__ float lerpf(float a, float b, float w) { return a + w * (b - a); }
-// The corner cell of the stencil at (x, y, z): the leaf-slot lookup is skipped while the corner stays
-// in the previous stencil's 8^3 leaf cell (`last` is only read).
-__host__ __device__ __forceinline__ Cell stencil_corner(const DevGrid& g, const StencilCell& last, float x, float y, float z) {
-  const int32_t i = (int32_t)floorf(x), j = (int32_t)floorf(y), k = (int32_t)floorf(z);
-  const int32_t dx = (i ^ last.i) | (j ^ last.j) | (k ^ last.k);
-  if (last.code >= 0 && dx >= 0 && dx < 8) return Cell{last.code, 0.0f};  // value only read for non-leaf cells
-  return cell_at(g, i, j, k);
-}
-// TrilinearSampler::sample at (x, y, z) whose corner cell is c (stencil_corner): returns true when the
-// cell differs from the previous evaluation (a NanoVDB stencil refresh).
-__host__ __device__ __forceinline__ bool trilinear_in(const DevGrid& g, StencilCell& last, float x, float y, float z, Cell c,
-                                                      float& out) {
-  float fi = floorf(x), fj = floorf(y), fk = floorf(z);
-  float u = x - fi, v = y - fj, w = z - fk;
-  int32_t i = (int32_t)fi, j = (int32_t)fj, k = (int32_t)fk;
-  bool refresh = i != last.i || j != last.j || k != last.k;
-  last.i = i;
-  last.j = j;
-  last.k = k;
-  last.code = c.code;
-  float s[8];
-  fetch_stencil(g, c, i, j, k, s);
-  out = lerpf(lerpf(lerpf(s[0], s[1], w), lerpf(s[2], s[3], w), v), lerpf(lerpf(s[4], s[5], w), lerpf(s[6], s[7], w), v), u);
-  return refresh;
-}
 // Returns true when the cell differs from the previous evaluation (a NanoVDB stencil refresh).
-// The leaf-slot lookup is skipped while the corner cell stays in the previous one's 8^3 cell.  (The
-// same as trilinear_in at stencil_corner, written out: the composed form costs the temperature kernel
-// 12 B more scratch.)
+// The leaf-slot lookup is skipped while the corner cell stays in the previous one's 8^3 cell.
 __host__ __device__ __forceinline__ bool trilinear(const DevGrid& g, StencilCell& last, float x, float y, float z,
                                                    float& out) {
   float fi = floorf(x), fj = floorf(y), fk = floorf(z);
@@ -930,22 +903,11 @@ __host__ __device__ inline void scene_finalize(DevScene& S) {
 // dens: emission (HasTemp), then sample_discrete({Null, Absorption, Scatter}, u) with
 // p_a = sigma_a*dens/sigma_maj, p_s = sigma_s*dens/sigma_maj.  u < 0: draw the event's uniform here
 // (after the emission, as the reference); else u is that draw, taken by the caller.
-// The temperature sampler's point of a primary ray's tentative collision and its stencil's corner cell,
-// looked up before the density's stencil arrives (VPT_TEMP_PREFETCH): the temperature grid's leaf-slot load
-// leaves the emitting collision's chain of four dependent loads (density slot, density stencil,
-// temperature slot, temperature stencil).
-struct TempPre {
-  float x, y, z;
-  Cell c;
-};
-#ifndef VPT_TEMP_PREFETCH
-#define VPT_TEMP_PREFETCH 0
-#endif
-
+// (r04's temperature-corner prefetch, measured 2.5 % slower on C4: tools/experiments/r04_temp_prefetch.patch.)
 template <bool HasTemp, bool Debug, class Env>
 __host__ __device__ __forceinline__ void primary_event(const DevScene& S, const DevGrid& G, Lane& ln, LaneCold& lc, Env& env,
                                                        float pi_x, float pi_y, float pi_z, float dens, float p_a,
-                                                       float p_s, float u, const TempPre* tpre = nullptr) {
+                                                       float p_s, float u) {
   env.prof(PB_EVENT);
   float cp[3];
   map_fwd(G, pi_x, pi_y, pi_z, cp[0], cp[1], cp[2]);
@@ -953,17 +915,13 @@ __host__ __device__ __forceinline__ void primary_event(const DevScene& S, const 
   const float p_n = fmaxf(1.0f - p_a - p_s, 0.0f);
   if (HasTemp) {
     float tx, ty, tz, tadim, X, Y, Z;
-    if (tpre) {
-      env.tally(CNT_TEMP_STENCILS, trilinear_in(S.temperature, ln.temp_cell, tpre->x, tpre->y, tpre->z, tpre->c, tadim) ? 1 : 0);
-    } else {
-      map_inv(S.temperature, cp[0], cp[1], cp[2], tx, ty, tz);
+    map_inv(S.temperature, cp[0], cp[1], cp[2], tx, ty, tz);
 #ifdef VPT_EXP_TEMP_NOCACHE
-      StencilCell tc{kNoCell, 0, 0, -1};
-      env.tally(CNT_TEMP_STENCILS, trilinear(S.temperature, tc, tx, ty, tz, tadim) ? 1 : 0);
+    StencilCell tc{kNoCell, 0, 0, -1};
+    env.tally(CNT_TEMP_STENCILS, trilinear(S.temperature, tc, tx, ty, tz, tadim) ? 1 : 0);
 #else
-      env.tally(CNT_TEMP_STENCILS, trilinear(S.temperature, ln.temp_cell, tx, ty, tz, tadim) ? 1 : 0);
+    env.tally(CNT_TEMP_STENCILS, trilinear(S.temperature, ln.temp_cell, tx, ty, tz, tadim) ? 1 : 0);
 #endif
-    }
     float tK = tadim * S.temp_scale + S.temp_offset;
     env.blackbody(S, tK, X, Y, Z);
     float sc = p_a * S.le_scale;
@@ -1034,15 +992,6 @@ __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const
   const float t = ln.s_t0;
   float pi_x = ln.e[0] + ln.d[0] * t, pi_y = ln.e[1] + ln.d[1] * t, pi_z = ln.e[2] + ln.d[2] * t;
   float dens;
-  TempPre tpre;
-  if (HasTemp && VPT_TEMP_PREFETCH && !ln.shadow) {
-    // the temperature point (world point of the collision, then the temperature grid's map) and its corner
-    // cell: the cell load is in flight with the density's
-    float cx, cy, cz;
-    map_fwd(G, pi_x, pi_y, pi_z, cx, cy, cz);
-    map_inv(S.temperature, cx, cy, cz, tpre.x, tpre.y, tpre.z);
-    tpre.c = stencil_corner(S.temperature, ln.temp_cell, tpre.x, tpre.y, tpre.z);
-  }
   if (Debug) env.tally(CNT_DENSITY_EVALS, 1);
   env.tally(CNT_STENCILS, trilinear(G, lc.dens_cell, pi_x, pi_y, pi_z, dens) ? 1 : 0);
   ln.sm = SM_DRAW;  // density <= 0, a null event or an unkilled shadow ray: keep drawing
@@ -1081,8 +1030,7 @@ __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const
       // worker.cpp:148-188
       const float p_a = (S.sigma_a * dens) / sigma_maj;
       const float p_s = (S.sigma_s * dens) / sigma_maj;
-      primary_event<HasTemp, Debug>(S, G, ln, lc, env, pi_x, pi_y, pi_z, dens, p_a, p_s, -1.0f,
-                                    VPT_TEMP_PREFETCH ? &tpre : nullptr);
+      primary_event<HasTemp, Debug>(S, G, ln, lc, env, pi_x, pi_y, pi_z, dens, p_a, p_s, -1.0f);
     } else {
       env.prof(PB_SHADOW_HIT);
       // Ratio tracking with Russian roulette (worker.cpp:68-85)
@@ -1313,6 +1261,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
 #ifdef VPT_JOB_LOG
           env.job_done(lc.job, (uint32_t)((lc.x0 / S.tw) + (lc.y0 / S.th) * S.ntx), lc.t_start);
 #endif
+          env.job_end(S, lc);
           ln.state = ST_FETCH;
           return;
         }

@@ -292,9 +292,10 @@ class Integrator:
 
 class Feed:
     """A running launch that renders job ids as they are pushed (vpt_gpu_feed_*, include/vpt_gpu.h) into
-    `film` (a device tensor of the context's film shape) on `stream` (a torch stream of the device).  A
-    staged feed's launch copies out and clears its own film at its end; collect() adds that copy and the
-    sample counts to a host film."""
+    `film` (a zeroed device tensor of the context's film shape) on `stream` (a torch stream of the device).  A
+    staged feed counts its completed jobs per tile: snapshot() adds what it has rendered so far into a host
+    film (also while it runs: the copy engines read the device film beside the launch), collect() the rest
+    once it has ended (then it clears `film`)."""
 
     def __init__(self, integrator: "Integrator", film, stream, window: int = 1 << 19, staged: bool = False):
         self.it, self.film, self.stream = integrator, film, stream
@@ -317,13 +318,25 @@ class Feed:
         capi.check(capi.lib().vpt_gpu_feed_query(self.h, C.byref(d), None), "vpt_gpu_feed_query")
         return bool(d.value)
 
+    def backlog(self) -> int:
+        b = C.c_uint64()
+        capi.check(capi.lib().vpt_gpu_feed_backlog(self.h, C.byref(b)), "vpt_gpu_feed_backlog")
+        return int(b.value)
+
     def destroy(self) -> None:
         if self.h:
             h, self.h = self.h, None
             capi.check(capi.lib().vpt_gpu_feed_destroy(h), "vpt_gpu_feed_destroy")
 
+    def snapshot(self, film_host: np.ndarray) -> None:
+        """Adds what a staged feed has rendered since the previous snapshot into film_host (float32,
+        C-contiguous [H][W][4])."""
+        assert film_host.dtype == np.float32 and film_host.flags.c_contiguous
+        capi.check(capi.lib().vpt_gpu_feed_snapshot(self.h, film_host.ctypes.data_as(C.POINTER(C.c_float))),
+                   "vpt_gpu_feed_snapshot")
+
     def collect(self, film_host: np.ndarray) -> None:
-        """Waits for a staged feed and adds its film into film_host (float32, C-contiguous); frees it."""
+        """Waits for a staged feed and adds the rest of its film into film_host (float32, C-contiguous); frees it."""
         assert film_host.dtype == np.float32 and film_host.flags.c_contiguous
         h, self.h = self.h, None
         capi.check(capi.lib().vpt_gpu_feed_collect(h, film_host.ctypes.data_as(C.POINTER(C.c_float))),
@@ -333,49 +346,31 @@ class Feed:
 def run(cfg: capi.Configuration, integrator: Integrator, tp: TileProvider, film: Optional[np.ndarray] = None,
         batch_jobs: int = 4096, flush_seconds: float = 0.2, window: int = 1 << 19) -> np.ndarray:
     """Drop-in for vpt::run (worker.cpp:92-208): drain `tp` on the GPU into `film` (host float32 [H][W][4],
-    the reference's Image<float,4> layout), as include/vpt_run.hpp's drain does: job ids go to a running
-    launch through a feed (bounded window, no launch drain between batches), and every flush_seconds the
-    feed is closed and the next opened on the other stream and device film, the finished one being added
-    into `film` -- which therefore fills in during the run (main.cpp:101-132 shows it at 5 FPS)."""
+    the reference's Image<float,4> layout), as include/vpt_run.hpp's drain does it (without its threads): the
+    job ids go to one running launch through a staged feed (no launch drain between batches), every
+    flush_seconds what it has completed is added into `film` (vpt_gpu_feed_snapshot) -- which therefore fills
+    in during the run (main.cpp:101-132 shows it at 5 FPS) -- and the collect adds the rest."""
     torch = integrator.torch
     out = film if film is not None else np.zeros((integrator.cfg.height, integrator.cfg.width, 4), np.float32)
     if out.dtype != np.float32 or not out.flags.c_contiguous or out.size != integrator.film.numel():
         raise ValueError("run: film must be a C-contiguous float32 [H][W][4] array")
-    films = [torch.zeros_like(integrator.film) for _ in range(2)]
-    streams = [torch.cuda.Stream(device=integrator.dev) for _ in range(2)]
-    feeds = [Feed(integrator, films[0], streams[0], window, staged=True), None]
-    cur, last = 0, time.monotonic()
-
-    def flush(i):
-        # staged feeds (as vpt_run.hpp's drain): nothing is queued on the GPU while the other feed's launch
-        # runs -- it holds the device until closed, and work queued meanwhile (a film copy, a device-wide
-        # synchronize) could wait behind it until its lanes give up
-        f, feeds[i] = feeds[i], None
-        f.collect(out)
-
+    dev_film = torch.zeros_like(integrator.film)
+    torch.cuda.synchronize(integrator.dev)  # zeroed before the feed's launch (on its own stream) reads it
+    stream = torch.cuda.Stream(device=integrator.dev)
+    feed = Feed(integrator, dev_film, stream, window, staged=True)
+    last = time.monotonic()
     try:
         while True:
             begin, count = tp.next_batch(batch_jobs)
             if count == 0:
                 break
-            feeds[cur].push(np.arange(begin, begin + count, dtype=np.uint64))
-            old = cur ^ 1
-            if feeds[old] is not None and feeds[old].done():
-                flush(old)
-            if feeds[old] is None and time.monotonic() - last >= flush_seconds:
-                feeds[cur].close()
-                cur, last = old, time.monotonic()
-                feeds[cur] = Feed(integrator, films[cur], streams[cur], window, staged=True)
-        for f in feeds:  # every feed closed before any wait: an open feed's launch holds the device
-            if f is not None:
-                f.close()
-        for i in (cur ^ 1, cur):
-            if feeds[i] is not None:
-                flush(i)
+            feed.push(np.arange(begin, begin + count, dtype=np.uint64))
+            if time.monotonic() - last >= flush_seconds:
+                feed.snapshot(out)
+                last = time.monotonic()
+        feed.collect(out)
     finally:
-        for f in feeds:
-            if f is not None:
-                f.destroy()
+        feed.destroy()
     return out
 
 
