@@ -87,6 +87,18 @@ uint64_t take_jobs(Provider& tp, uint64_t max_jobs, JobRuns& runs, OnToken&& on_
   return taken;
 }
 
+namespace detail {
+// VPT_DRAIN_TRACE=1: one stderr line per pipeline event (taker done, the pusher's final hold, its close), in
+// milliseconds since the first event, next to the library's VPT_FEED_TRACE lines.
+inline void drain_trace(const char* what, double a = 0, double b = 0) {
+  static const bool on = std::getenv("VPT_DRAIN_TRACE") && std::atoi(std::getenv("VPT_DRAIN_TRACE")) > 0;
+  if (!on) return;
+  static const auto t0 = std::chrono::steady_clock::now();
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  std::fprintf(stderr, "drain %10.2f ms %-10s %.0f %.0f\n", ms, what, a, b);
+}
+}  // namespace detail
+
 inline std::mutex& film_mutex() {  // the host film is shared by every caller
   static std::mutex mu;
   return mu;
@@ -134,7 +146,11 @@ class FeedPipeline {
     uint64_t n = 0;
     for (const auto& r : runs) n += r.second;
     std::unique_lock<std::mutex> l(mu_);
-    taker_cv_.wait(l, [&] { return err_ != VPT_OK || queued_ + held_ < hold_max_; });
+    if (err_ == VPT_OK && queued_ + held_ >= hold_max_) {  // the run-ahead bound: wait for the lanes
+      const auto w0 = std::chrono::steady_clock::now();
+      taker_cv_.wait(l, [&] { return err_ != VPT_OK || queued_ + held_ < hold_max_; });
+      blocked_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
+    }
     if (err_ != VPT_OK) return err_;
     queue_.insert(queue_.end(), runs.begin(), runs.end());
     queued_ += n;
@@ -148,6 +164,7 @@ class FeedPipeline {
     }
     if (pusher_.joinable()) pusher_.join();
     stop_threads();  // no snapshot starts once the feed is closed: the collect adds the rest
+    detail::drain_trace("taker_blocked_ms", blocked_s_ * 1e3);
     int rc = err_;
     if (feed_) {
       vpt_gpu_feed* f = feed_;
@@ -233,6 +250,7 @@ class FeedPipeline {
     // The provider is dry: the held jobs, costliest tile class first (jid order within a class: consecutive
     // items are different tiles of one wave), then the end of the feed.
     std::vector<uint64_t> rest(hold.begin() + (ptrdiff_t)head, hold.end());
+    detail::drain_trace("final_hold", (double)rest.size(), (double)pushed_);
     if (!cls_.empty() && !rest.empty()) {
       const uint64_t T = cls_.size();
       uint64_t start[kClasses + 1] = {};
@@ -245,6 +263,7 @@ class FeedPipeline {
     for (size_t i = 0; i < rest.size(); i += kChunk)
       if (int rc = push(rest.data() + i, std::min<uint64_t>(kChunk, rest.size() - i))) return fail(rc);
     if (int rc = vpt_gpu_feed_close(feed_)) return fail(rc);
+    detail::drain_trace("closed");
     std::lock_guard<std::mutex> l(mu_);
     held_ = 0;
   }
@@ -284,6 +303,7 @@ class FeedPipeline {
   std::condition_variable taker_cv_;
   JobRuns queue_;
   uint64_t queued_ = 0, held_ = 0;
+  double blocked_s_ = 0;  // the takers' waits on the run-ahead bound (VPT_DRAIN_TRACE)
   bool no_more_ = false;
   int err_ = VPT_OK;
   std::atomic<bool> film_stop_{false};
@@ -346,7 +366,12 @@ int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs,
     hub.cv.notify_all();
   }
   JobRuns runs;
-  while (rc == VPT_OK && take_jobs(tp, std::max<uint64_t>(1, batch_jobs), runs, [](auto&) {})) rc = pipe.add(runs);
+  uint64_t taken = 0;
+  for (uint64_t n; rc == VPT_OK && (n = take_jobs(tp, std::max<uint64_t>(1, batch_jobs), runs, [](auto&) {}));) {
+    taken += n;
+    rc = pipe.add(runs);
+  }
+  detail::drain_trace("taker_done", (double)taken);
   if (share) {  // no new helper attaches; the attached ones queue their last jobs, then detach
     {
       std::lock_guard<std::mutex> l(hub.mu);

@@ -336,3 +336,87 @@ def single_scatter(o, w, wi, sigma_s, sub=48, npts=8, t_shadow0=1e-5):
     I = (wt * sigma_s * rho * np.exp(-sigma_s * (tau_cam + tau_sh))).sum(axis=1)
     tau = cube_od(np.broadcast_to(o, (n, 3)), w, t0, t1)
     return np.where(hit, I, 0.0), np.where(hit, tau, 0.0)
+
+
+# ---- multiple scattering: the survival probability of absorbing paths ----------------
+def max_scatters(max_depth):
+    """Scatters a path can make: the loop's depth moves twice per scatter (worker.cpp:130 and :169) and its
+    body runs while depth < max_depth, so at depths 0, 2, 4, ... -- ceil(max_depth / 2) iterations; the
+    scatter check `depth++ >= max_depth` (:169) never fires, since depth < max_depth in the body.  After the
+    last one's scatter the loop ends with `terminated` false, and the environment light is added."""
+    return (int(max_depth) + 1) // 2
+
+
+def hg_sample_dirs(d, g, u1, u2):
+    """sample_henyey_greenstein (random.hpp:56-84) about the incoming directions d [n, 3]: local z = d,
+    cos = (1 + g^2 - ((1 - g^2) / (1 + g - 2 g u1))^2) / (2 g), phi = 2 pi u2 (any frame about d: the law
+    is symmetric in phi)."""
+    cos = (1.0 + g * g - ((1.0 - g * g) / (1.0 + g - 2.0 * g * u1)) ** 2) / (2.0 * g)
+    cos = np.clip(cos, -1.0, 1.0)
+    sin = np.sqrt(np.maximum(0.0, 1.0 - cos * cos))
+    a = np.where(np.abs(d[:, :1]) < 0.9, [[1.0, 0.0, 0.0]], [[0.0, 1.0, 0.0]])
+    e1 = np.cross(d, a)
+    e1 /= np.linalg.norm(e1, axis=1, keepdims=True)
+    e2 = np.cross(d, e1)
+    phi = 2.0 * np.pi * u2
+    return (sin * np.cos(phi))[:, None] * e1 + (sin * np.sin(phi))[:, None] * e2 + cos[:, None] * d
+
+
+def survival_walk(o, w, sigma_s, sigma_a, g, max_depth, rng):
+    """Whether each camera path o + t w (index space, |w| = 1) through the cube survives -- is not absorbed
+    -- by an analog random walk in float64 written from the reference's semantics, not from the oracle:
+    delta tracking against the majorant sigma_t (the cube's density <= 1) inside the clip box [0, 128]^3
+    (Ray::clip, volume.cpp:83), a tentative collision real with probability rho(x) (null: same direction,
+    majorant_transmittance_sampler.cpp:59-61), a real one absorbing with probability sigma_a / sigma_t and
+    otherwise scattering along sample_henyey_greenstein's law (worker.cpp:148-179), the path ending without
+    absorption when it leaves the box or after max_scatters(max_depth) scatters.  Returns bool [n]."""
+    n = w.shape[0]
+    sigma_t = sigma_s + sigma_a
+    t0, t1 = cube_chord(np.broadcast_to(o, w.shape), w)
+    t0 = np.maximum(t0, 1e-5)
+    surv = np.ones(n, bool)
+    act = t1 > t0
+    p = np.where(act[:, None], o + t0[:, None] * w, 0.0)
+    d = w.copy()
+    k = np.zeros(n, np.int64)
+    kmax = max_scatters(max_depth)
+    idx = np.flatnonzero(act)
+    while idx.size:
+        pi, di = p[idx], d[idx]
+        _, te = cube_chord(pi, di)                                 # the box exit from the current point
+        dt = -np.log1p(-rng.random(idx.size)) / sigma_t
+        esc = dt >= te
+        pn = pi + dt[:, None] * di
+        real = ~esc & (rng.random(idx.size) < cube_density(pn))
+        absorb = real & (rng.random(idx.size) < sigma_a / sigma_t)
+        scat = real & ~absorb
+        surv[idx[absorb]] = False
+        k[idx[scat]] += 1
+        p[idx] = np.where(esc[:, None], pi, pn)
+        if scat.any():
+            s = idx[scat]
+            d[s] = hg_sample_dirs(d[s], g, rng.random(s.size), rng.random(s.size))
+        done = esc | absorb | (scat & (k[idx] >= kmax))
+        idx = idx[~done]
+    return surv
+
+
+def survival_probability(cfg, paths_per_pixel, seed=0, index_of_world=64.0, chunk=1 << 20):
+    """Per pixel [H, W]: the survival probability of its camera paths (pixel centres: no jitter) estimated
+    with paths_per_pixel walks of survival_walk (in chunks of ~`chunk` paths)."""
+    W, H = cfg.width, cfg.height
+    v, wp = cfg.volume_parameters, cfg.worker_parameters
+    ys, xs = np.mgrid[0:H, 0:W]
+    d = camera_dirs(cfg, xs.ravel() + 0.5, ys.ravel() + 0.5)
+    o = np.asarray(cfg.camera_parameters.position[:], np.float64) + index_of_world
+    rng = np.random.default_rng(seed)
+    hits = np.zeros(W * H)
+    reps = max(1, chunk // (W * H))
+    done = 0
+    while done < paths_per_pixel:
+        r = min(reps, paths_per_pixel - done)
+        surv = survival_walk(o, np.tile(d, (r, 1)), float(v.sigma_s), float(v.sigma_a),
+                             float(v.henyey_greenstein_g), int(wp.max_depth), rng)
+        hits += surv.reshape(r, W * H).sum(axis=0)
+        done += r
+    return (hits / paths_per_pixel).reshape(H, W)
