@@ -179,6 +179,7 @@ typedef struct vpt_counters {
   uint64_t scatters;       /* scatter events                                            */
   uint64_t shadow_rays;    /* sample_Ld calls that traced a ray                         */
   uint64_t rng_draws;      /* uniform<float>() calls                                    */
+  uint64_t exchanged;      /* paths moved by live-path compaction (vpt_gpu_set_compaction) */
 } vpt_counters;
 
 /* Create a context on HIP device `device`.  Copies everything it needs (the grids are
@@ -422,6 +423,12 @@ int vpt_gpu_set_latency_tuning(vpt_gpu_ctx* ctx, int wave_lanes, int gate_min, i
  * measured slower there: C2 109 ms); -1: keep.  Latency-bound launches always use the latency gates.
  * Samples never depend on it.  Takes effect at the next launch. */
 int vpt_gpu_set_latency_kernel(vpt_gpu_ctx* ctx, int mode, int ungated);
+/* Live-path compaction (north_star's "ballot/prefix-sum to compact live rays") on the latency kernel's partly
+ * filled launches (e.g. C2): every `every` outer iterations a block's four wavefronts meet and, when packing
+ * helps, move their paths through LDS so that walking paths fill the first wavefronts (a kernel variant with a
+ * 56 KiB LDS exchange: <= 2 blocks per CU; launches with more blocks per CU do not use it).  0 (default): off.
+ * Samples never depend on it (counters: `exchanged`).  Takes effect at the next launch. */
+int vpt_gpu_set_compaction(vpt_gpu_ctx* ctx, int every);
 /* The mode and the latency kernel's resident blocks per CU. */
 int vpt_gpu_latency_kernel_info(const vpt_gpu_ctx* ctx, int* mode, int* resident_blocks_per_cu);
 /* SIMT-utilisation profile of profiling builds (-DVPT_PROFILE): for each block of the lane state

@@ -411,3 +411,46 @@ def test_temperature_grid_of_another_map_or_topology(kind, lat):
     for k in COUNTERS:
         assert c[k] == tot[k], (k, c[k], tot[k])
     assert tot["temp_stencils"] > 100
+
+
+COMPACT_CASES = [
+    # (workload, width, height, grid_n, run_skipping)
+    ("c2", 96, 96, 128, 1),    # C2's cube with run skipping: the launch compaction targets
+    ("c2", 80, 80, 128, 0),
+    ("c3", 96, 80, 64, 0),     # the cloud
+    ("c4", 96, 72, 64, -1),    # the temperature kernel (its temperature cell travels with the path)
+]
+
+
+@pytest.mark.parametrize("every", [1, 4, 16])
+@pytest.mark.parametrize("name,w,h,n,runs", COMPACT_CASES)
+def test_compacting_latency_kernel_films_bit_exact(name, w, h, n, runs, every):
+    """Live-path compaction (vpt_gpu_set_compaction) on partly filled latency launches: a 4-block grid renders
+    each wave's >= 64 jobs (more than 6 per wavefront: not a latency-bound launch), its four wavefronts meeting
+    every 1 / 4 / 16 outer iterations to repack walking paths.  Each wave's film is the oracle's bit for bit,
+    the event counters equal the oracle's, and the exchange ran (`exchanged` > 0)."""
+    from volume_path_tracer_amd.render import Integrator
+
+    wl = workload(name, width=w, height=h, spp=3, grid_n=n)
+    dens, temp = _grids(wl)
+    it = Integrator(wl.cfg, dens, temp, device=0)
+    it.set_latency_kernel(1, 0)
+    it.set_tuning(grid_blocks=4)
+    it.set_compaction(every)
+    if runs >= 0:
+        it.set_run_skipping(runs)
+    od, ot = _oracle_grids(dens, temp)
+    T = wl.cfg.jobs_per_wave()
+    assert T > 6 * 4 * 4  # partly filled, not latency-bound (kSpreadLanes x wavefronts)
+    it.counters(reset=True)
+    tot = {k: 0 for k in COUNTERS}
+    for wave in (1, 2, 3):
+        f_g = _prod_film(it, (wave - 1) * T, T)
+        f_o, _, c_o = O.render_jobs(wl.cfg, od, ot, (wave - 1) * T, T)
+        _assert_bitwise(f_g, f_o, f"{name} compact {every} wave {wave}")
+        for k in COUNTERS:
+            tot[k] += c_o[k]
+    c = it.counters()
+    for k in COUNTERS:
+        assert c[k] == tot[k], (k, c[k], tot[k])
+    assert c["exchanged"] > 0, c

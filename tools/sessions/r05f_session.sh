@@ -16,3 +16,5 @@ rm -f $O/film.f32 $O/x
 VPT_LIB=$PWD/volume_path_tracer_amd/lib/libvpt_prof.so timeout -k 10 300 python tools/tune.py --config c2 --spp 64 \
   --gates 6:8:36:4 --blocks 512 --lat-kernel 1 --lat-ungated 0 --profile --reps 1 > $O/c2_profile.jsonl 2>$O/c2_profile.err
 cat $O/c2_profile.jsonl
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_analytic_multiscatter.py \
+  > $O/pytest_multiscatter.log 2>&1; grep -E "PASSED|FAILED|passed|failed|variant|{" $O/pytest_multiscatter.log | tail -12

@@ -58,6 +58,7 @@ def parser():
     ap.add_argument("--lat-kernel", type=int, default=-1, help="vpt_gpu_set_latency_kernel mode (-1 auto, 0 off, 1 on)")
     ap.add_argument("--lat-ungated", type=int, default=-1, help="its ungated flag (-1 keep)")
     ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--compact", default="0", help="live-path compaction periods to sweep (comma-separated; 0 = off)")
     ap.add_argument("--rng-mode", default="reference")
     ap.add_argument("--order", type=int, default=-1, help="job order mode (-1: library default)")
     ap.add_argument("--tail", type=int, default=0, help="VPT_ORDER_COST_TAIL tile-major waves (0: auto)")
@@ -102,8 +103,10 @@ def sweep(a):
         gm, gi = parts[0], parts[1]
         ge = parts[2] if len(parts) > 2 else 1
         gw = parts[3] if len(parts) > 3 else 0
-        for b, lat in [(b, l) for b in map(int, a.blocks.split(",")) for l in (a.lat.split(",") if a.lat else [""])]:
+        for b, lat, cmp in [(b, l, c) for b in map(int, a.blocks.split(",")) for l in (a.lat.split(",") if a.lat else [""])
+                            for c in map(int, a.compact.split(","))]:
             it.set_tuning(gm, gi, b if b > 0 else base_blocks, ge, gw)
+            it.set_compaction(cmp)
             if lat:
                 it.set_latency_tuning(*map(int, lat.split(":")))
             best = 1e9
@@ -117,7 +120,9 @@ def sweep(a):
             if a.profile:
                 print(json.dumps({"gate": g, "profile": it.profile(reset=True)}), flush=True)
             print(json.dumps({"lib": os.environ.get("VPT_LIB", "default"), "config": a.config, "order": a.order, "tail": a.tail, "perm": a.perm,
-                              "gate": g, "lat": lat, "lat_kernel": [a.lat_kernel, a.lat_ungated], "blocks": b or base_blocks, "spp": a.spp, "ms": round(best * 1e3, 2),
+                              "gate": g, "lat": lat, "lat_kernel": [a.lat_kernel, a.lat_ungated], "compact": cmp,
+                              "exchanged": it.counters(reset=True).get("exchanged", 0),
+                              "blocks": b or base_blocks, "spp": a.spp, "ms": round(best * 1e3, 2),
                               "Msps": round(wl.cfg.width * wl.cfg.height * a.spp / best / 1e6, 2)}), flush=True)
     del it
 

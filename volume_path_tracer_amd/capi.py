@@ -82,7 +82,7 @@ class GridDesc(C.Structure):
 class Counters(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("samples", "dda_steps", "segments", "draws", "stencils",
                                           "density_evals", "temp_stencils", "scatters", "shadow_rays",
-                                          "rng_draws")]
+                                          "rng_draws", "exchanged")]
 
     def as_dict(self) -> dict:
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
@@ -259,6 +259,8 @@ def lib() -> C.CDLL:
     L.vpt_gpu_set_job_permutation.argtypes = [vp, C.POINTER(C.c_uint32), C.c_uint64]
     if hasattr(L, "vpt_gpu_set_latency_kernel"):  # (A/B builds of older sources lack it; tests check the exports)
         L.vpt_gpu_set_latency_kernel.argtypes = [vp, C.c_int, C.c_int]
+    if hasattr(L, "vpt_gpu_set_compaction"):
+        L.vpt_gpu_set_compaction.argtypes = [vp, C.c_int]
         L.vpt_gpu_latency_kernel_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     if hasattr(L, "vpt_gpu_stream_create"):
         L.vpt_gpu_stream_create.argtypes = [vp, C.POINTER(vp)]

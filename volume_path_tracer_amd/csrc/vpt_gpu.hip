@@ -111,6 +111,7 @@ struct KernelEnvT {
   unsigned* feed_error;
   uint64_t* feed_started;            // a lane that reserves item k, k % kStartedHint == 0, stores k here
   uint32_t* tile_done;               // a staged feed: jobs completed per tile (device memory), else nullptr
+  uint32_t compact_every;            // the compacting latency kernel: outer iterations between two meetings
 
   // Adds w for every active lane with w != 0 (w uniform per call site) to a workgroup counter.
   __device__ __forceinline__ void tally(int32_t k, int32_t w) {
@@ -320,9 +321,133 @@ struct KernelEnvT {
 using KernelEnv = KernelEnvT<false>;
 
 
+// ---- live-path compaction (north_star: "wavefront ballot/prefix-sum to compact live rays") ----
+// The latency kernel's partly filled launches (C2: 2 blocks per CU, 2 jobs per lane) are issue-bound on
+// divergent wave instructions: the HDDA step takes 85 % of the wave time and runs at 32.5 of 64 lanes, and per
+// walk-loop iteration a wavefront holds 32.7 walking, 14.9 parked (a collision waiting for its batched
+// evaluation) and 12.5 finished paths (r05f census, profiles/r05f_c2_census.txt).  Every `compact_every` outer
+// iterations the block's four wavefronts meet (two barriers), count their walking / other live paths with
+// ballots, and -- when packing would leave fewer wavefronts holding walkers, or live paths -- move every path
+// (its hot Lane registers and its cold state, which this kernel keeps in VGPRs: kXWords words) through LDS so
+// that walkers fill the block's first wavefronts, the other live paths the next, finished ones the last.  A
+// wavefront without a live path skips its iterations until the next meeting; the block ends when none is left.
+// A path's operations and draws never depend on the thread that runs it (its RNG state and every value it reads
+// travel with it; the gates only choose when a block runs), so samples are bit-identical; only the order of the
+// film's fp32 atomics changes.  The HDDA step counter stays with the thread (it is summed per launch).
+constexpr int kXWords = 56;  // 53 state words, padded to uint4
+__device__ __forceinline__ uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
+__device__ __forceinline__ float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+template <bool HasTemp>
+__device__ __forceinline__ void xchg_pack(const Lane& ln, const LaneCold& lc, uint32_t x[kXWords]) {
+  int n = 0;
+  x[n++] = (uint32_t)ln.state; x[n++] = (uint32_t)ln.sm; x[n++] = (uint32_t)ln.shadow;
+  x[n++] = (uint32_t)ln.rng; x[n++] = (uint32_t)(ln.rng >> 32);
+  for (int i = 0; i < 3; ++i) {
+    x[n++] = f2u(ln.e[i]); x[n++] = f2u(ln.d[i]); x[n++] = f2u(ln.nxt[i]);
+    x[n++] = (uint32_t)ln.vox[i]; x[n++] = f2u(ln.finc[i]); x[n++] = (uint32_t)ln.vinc[i];
+  }
+  x[n++] = f2u(ln.scale); x[n++] = f2u(ln.rscale); x[n++] = f2u(ln.maj); x[n++] = (uint32_t)ln.dim;
+  x[n++] = f2u(ln.Tn); x[n++] = f2u(ln.T1); x[n++] = ln.pw; x[n++] = f2u(ln.s_t0); x[n++] = f2u(ln.s_t1);
+  x[n++] = f2u(ln.s_dmaj);
+  x[n++] = (uint32_t)lc.x0; x[n++] = (uint32_t)lc.y0; x[n++] = (uint32_t)lc.pix; x[n++] = lc.depth;
+  for (int i = 0; i < 3; ++i) { x[n++] = f2u(lc.L[i]); x[n++] = f2u(lc.ro[i]); x[n++] = f2u(lc.rd[i]); }
+  x[n++] = (uint32_t)lc.dens_cell.i; x[n++] = (uint32_t)lc.dens_cell.j; x[n++] = (uint32_t)lc.dens_cell.k;
+  x[n++] = (uint32_t)lc.dens_cell.code; x[n++] = f2u(lc.Tr); x[n++] = f2u(lc.y_draw); x[n++] = lc.item_lo;
+  x[n++] = lc.item_hi;
+  if (HasTemp) {
+    x[n++] = (uint32_t)ln.temp_cell.i; x[n++] = (uint32_t)ln.temp_cell.j; x[n++] = (uint32_t)ln.temp_cell.k;
+  }
+  x[n++] = HasTemp ? (uint32_t)ln.temp_cell.code : 0u;
+  while (n < kXWords) x[n++] = 0;
+}
+template <bool HasTemp>
+__device__ __forceinline__ void xchg_unpack(Lane& ln, LaneCold& lc, const uint32_t x[kXWords]) {
+  int n = 0;
+  ln.state = (int32_t)x[n++]; ln.sm = (int32_t)x[n++]; ln.shadow = (int32_t)x[n++];
+  ln.rng = (uint64_t)x[n] | ((uint64_t)x[n + 1] << 32);
+  n += 2;
+  for (int i = 0; i < 3; ++i) {
+    ln.e[i] = u2f(x[n++]); ln.d[i] = u2f(x[n++]); ln.nxt[i] = u2f(x[n++]);
+    ln.vox[i] = (int32_t)x[n++]; ln.finc[i] = u2f(x[n++]); ln.vinc[i] = (int32_t)x[n++];
+  }
+  ln.scale = u2f(x[n++]); ln.rscale = u2f(x[n++]); ln.maj = u2f(x[n++]); ln.dim = (int32_t)x[n++];
+  ln.Tn = u2f(x[n++]); ln.T1 = u2f(x[n++]); ln.pw = x[n++]; ln.s_t0 = u2f(x[n++]); ln.s_t1 = u2f(x[n++]);
+  ln.s_dmaj = u2f(x[n++]);
+  lc.x0 = (int32_t)x[n++]; lc.y0 = (int32_t)x[n++]; lc.pix = (int32_t)x[n++]; lc.depth = x[n++];
+  for (int i = 0; i < 3; ++i) { lc.L[i] = u2f(x[n++]); lc.ro[i] = u2f(x[n++]); lc.rd[i] = u2f(x[n++]); }
+  lc.dens_cell.i = (int32_t)x[n++]; lc.dens_cell.j = (int32_t)x[n++]; lc.dens_cell.k = (int32_t)x[n++];
+  lc.dens_cell.code = (int32_t)x[n++]; lc.Tr = u2f(x[n++]); lc.y_draw = u2f(x[n++]); lc.item_lo = x[n++];
+  lc.item_hi = x[n++];
+  if (HasTemp) {
+    ln.temp_cell.i = (int32_t)x[n++]; ln.temp_cell.j = (int32_t)x[n++]; ln.temp_cell.k = (int32_t)x[n++];
+  }
+  if (HasTemp) ln.temp_cell.code = (int32_t)x[n];
+}
+// Dynamic LDS of the compacting kernel: [kXWords / 4][kBlockThreads] uint4 (57 344 B).
+constexpr size_t kXchgBytes = (size_t)kXWords * kBlockThreads * sizeof(uint32_t);
+
+template <bool HasTemp, bool Runs>
+__device__ __forceinline__ void compact_loop(ScenePtr sp, Lane& ln, LaneCold& lc, KernelEnvT<true>& env) {
+  extern __shared__ uint4 g_xchg[];
+  __shared__ int32_t cnt[8];  // per wavefront: walking paths, other live paths
+  const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const uint64_t below = l ? (~0ULL >> (64 - l)) : 0ULL;
+  const uint32_t every = env.compact_every;
+  for (;;) {
+    for (uint32_t it = 0; it < every; ++it) {
+      if (__builtin_amdgcn_ballot_w64(ln.state != ST_DONE) == 0) break;  // (wave-uniform)
+      if (ln.state != ST_DONE) lane_iteration<HasTemp, false, Runs>(sp, ln, env);
+    }
+    const bool walking = ln.state == ST_SAMPLE && ln.sm != SM_EVAL, live = ln.state != ST_DONE;
+    const uint64_t mw = __builtin_amdgcn_ballot_w64(walking), mo = __builtin_amdgcn_ballot_w64(live && !walking);
+    if (l == 0) {
+      cnt[w] = __popcll(mw);
+      cnt[4 + w] = __popcll(mo);
+    }
+    __syncthreads();
+    int32_t nw = 0, no = 0, pw = 0, po = 0, pd = 0, wave_w = 0, wave_l = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < 4; ++v) {
+      const int32_t a = cnt[v], b = cnt[4 + v];
+      nw += a;
+      no += b;
+      wave_w += a > 0;
+      wave_l += a + b > 0;
+      if (v < w) {
+        pw += a;
+        po += b;
+        pd += 64 - a - b;
+      }
+    }
+    if (nw + no == 0) break;  // the block's paths are all done (uniform)
+    // exchange only when packing leaves fewer wavefronts with walkers, or with live paths (uniform)
+    if ((nw + 63) / 64 < wave_w || (nw + no + 63) / 64 < wave_l) {
+      const int32_t dest = walking ? pw + __popcll(mw & below)
+                                   : live ? nw + po + __popcll(mo & below) : nw + no + pd + __popcll(~(mw | mo) & below);
+      uint32_t x[kXWords];
+      xchg_pack<HasTemp>(ln, lc, x);
+#pragma unroll
+      for (int q = 0; q < kXWords / 4; ++q)
+        g_xchg[q * kBlockThreads + dest] = make_uint4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < kXWords / 4; ++q) {
+        const uint4 v = g_xchg[q * kBlockThreads + threadIdx.x];
+        x[4 * q] = v.x;
+        x[4 * q + 1] = v.y;
+        x[4 * q + 2] = v.z;
+        x[4 * q + 3] = v.w;
+      }
+      xchg_unpack<HasTemp>(ln, lc, x);
+      env.tally(CNT_EXCHANGED, 1);
+    }
+    __syncthreads();  // cnt and g_xchg are rewritten at the next meeting
+  }
+}
+
 // counters[] order = vpt_counters field order
-template <bool HasTemp, bool Debug, bool Runs, bool Lat = false>
-__global__ __launch_bounds__(kBlockThreads, Lat ? VPT_WAVES_LAT : (Debug ? VPT_WAVES_SLOW : (HasTemp ? VPT_WAVES_TEMP : VPT_WAVES_FAST))) void vpt_integrate_kernel(const DevScene* scene, KernelEnvT<Lat> env,
+template <bool HasTemp, bool Debug, bool Runs, bool Lat = false, bool Compact = false>
+__global__ __launch_bounds__(kBlockThreads, Compact ? 2 : (Lat ? VPT_WAVES_LAT : (Debug ? VPT_WAVES_SLOW : (HasTemp ? VPT_WAVES_TEMP : VPT_WAVES_FAST)))) void vpt_integrate_kernel(const DevScene* scene, KernelEnvT<Lat> env,
                                                                        unsigned long long* counters) {
   __shared__ unsigned long long wg_counters[kCounterCount];
   if (threadIdx.x < kCounterCount) wg_counters[threadIdx.x] = 0;
@@ -348,6 +473,10 @@ __global__ __launch_bounds__(kBlockThreads, Lat ? VPT_WAVES_LAT : (Debug ? VPT_W
   if constexpr (Lat) env.reg_cold = &lc_reg;
   cold_init(env.cold());
   const ScenePtr sp = (ScenePtr)scene;
+  if constexpr (Compact) {
+    static_assert(Lat && !Debug, "compaction runs in the latency kernel only");
+    compact_loop<HasTemp, Runs>(sp, ln, lc_reg, env);
+  } else
   while (ln.state != ST_DONE) {
     lane_iteration<HasTemp, Debug, Runs>(sp, ln, env);
     // Feed mode: a wavefront whose every live lane waits for the host to publish its item sleeps between
@@ -607,6 +736,8 @@ struct vpt_gpu_ctx {
   int lat_mode = -1;              // latency kernel: -1 auto (launches of <= lat_per_cu blocks per CU), 0 off, 1 on
   int lat_ungated = 0;             // its partly filled launches read the latency gates (1) or the context's (0)
   int lat_per_cu = 1;              // resident blocks per CU of the latency kernel
+  int compact_every = 0;           // live-path compaction on partly filled latency launches: meeting period (0 off)
+  int compact_per_cu = 0;          // resident blocks per CU of the compacting kernel (its LDS exchange)
 };
 
 namespace {
@@ -832,6 +963,10 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   const bool use_lat = !dbg && !feed && ctx->lat_mode != 0 &&
                        (ctx->lat_mode == 1 || (!ctx->grid_user && (latency || blocks <= lat_blocks)));
   if (use_lat) blocks = (uint32_t)std::min<uint64_t>(latency ? lat_blocks : blocks, lat_blocks);
+  // Live-path compaction (vpt_gpu_set_compaction): partly filled launches of the latency kernel whose grid fits
+  // the compacting kernel's occupancy (its LDS exchange: 2 blocks per CU; C2 runs 2).
+  const bool compact = use_lat && !latency && ctx->compact_every > 0 &&
+                       (uint64_t)blocks <= cus * (uint64_t)std::max(0, ctx->compact_per_cu);
   const uint64_t T = ctx->scene.T;
   if (!feed && ctx->order_mode != VPT_ORDER_JID && jid_begin % T == 0 && jid_count % T == 0 && jid_count < (1ULL << 32)) {
     // whole waves: take the jobs in cost order (same jobs, same samples)
@@ -860,6 +995,7 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.feed_error = feed ? feed->error : nullptr;
   env.feed_started = feed ? feed->started : nullptr;
   env.tile_done = feed ? feed->tile_done : nullptr;
+  env.compact_every = 0;
   env.event_count = ctx->job_counter + 2 * slot + 1;
   env.event_cap = event_cap;
   if (slot_out) *slot_out = slot;
@@ -868,10 +1004,18 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
     vpt::KernelEnvT<true> envl;
     static_assert(sizeof envl == sizeof env, "one layout for both kernel environments");
     std::memcpy(&envl, &env, sizeof env);
-    auto kernel = temp ? vpt::vpt_integrate_kernel<true, false, false, true>
-                       : ctx->use_runs ? vpt::vpt_integrate_kernel<false, false, true, true>
-                                       : vpt::vpt_integrate_kernel<false, false, false, true>;
-    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, scene, envl, ctx->counters);
+    envl.compact_every = (uint32_t)std::max(1, ctx->compact_every);
+    if (compact) {
+      auto kernel = temp ? vpt::vpt_integrate_kernel<true, false, false, true, true>
+                         : ctx->use_runs ? vpt::vpt_integrate_kernel<false, false, true, true, true>
+                                         : vpt::vpt_integrate_kernel<false, false, false, true, true>;
+      hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), vpt::kXchgBytes, s, scene, envl, ctx->counters);
+    } else {
+      auto kernel = temp ? vpt::vpt_integrate_kernel<true, false, false, true>
+                         : ctx->use_runs ? vpt::vpt_integrate_kernel<false, false, true, true>
+                                         : vpt::vpt_integrate_kernel<false, false, false, true>;
+      hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, scene, envl, ctx->counters);
+    }
   } else {
     auto kernel = temp ? (dbg ? vpt::vpt_integrate_kernel<true, true, false> : vpt::vpt_integrate_kernel<true, false, false>)
                        : ctx->use_runs
@@ -984,6 +1128,13 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
                                                 : vpt::vpt_integrate_kernel<false, false, false, true>),
       vpt::kBlockThreads, 0));
   ctx->lat_per_cu = std::max(1, std::min(lat_per_cu, per_cu));
+  int compact_per_cu = 0;
+  VPT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &compact_per_cu, temperature ? vpt::vpt_integrate_kernel<true, false, false, true, true>
+                                   : (ctx->use_runs ? vpt::vpt_integrate_kernel<false, false, true, true, true>
+                                                    : vpt::vpt_integrate_kernel<false, false, false, true, true>),
+      vpt::kBlockThreads, vpt::kXchgBytes));
+  ctx->compact_per_cu = compact_per_cu;
   ctx->cus = cus > 0 ? cus : 1;
   // Scheduling defaults from tools/tune.py sweeps on MI355X (C3, 256 spp): rare states run for >= 6
   // waiting lanes, density evaluations (with the deferred exact draw) for >= 36, everything runs when
@@ -1755,6 +1906,12 @@ int vpt_gpu_launch_info(const vpt_gpu_ctx* ctx, int* grid_blocks, int* block_thr
   if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
   if (grid_blocks) *grid_blocks = ctx->grid_blocks;
   if (block_threads) *block_threads = vpt::kBlockThreads;
+  return VPT_OK;
+}
+
+int vpt_gpu_set_compaction(vpt_gpu_ctx* ctx, int every) {
+  if (!ctx || every < 0) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_compaction: bad argument");
+  ctx->compact_every = every;  // read by the next render's host code only: no wait
   return VPT_OK;
 }
 

@@ -470,7 +470,7 @@ enum : int32_t { PT_FETCH = 0, PT_PIXEL, PT_RAY, PT_WALK, PT_EVAL, PT_NEE, PT_FI
 // the debug kernel (per-sample records) counts all of them for parity checks.
 enum : int32_t {
   CNT_SAMPLES = 0, CNT_DDA_STEPS, CNT_SEGMENTS, CNT_DRAWS, CNT_STENCILS, CNT_DENSITY_EVALS, CNT_TEMP_STENCILS,
-  CNT_SCATTERS, CNT_SHADOW_RAYS, CNT_RNG_DRAWS, CNT_COUNT
+  CNT_SCATTERS, CNT_SHADOW_RAYS, CNT_RNG_DRAWS, CNT_EXCHANGED, CNT_COUNT
 };
 
 // The lane's cold state: touched only by the per-pixel, per-bounce and film blocks, never by the

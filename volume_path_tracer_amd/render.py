@@ -198,6 +198,11 @@ class Integrator:
         launches on it use the latency gates / the context's (-1 keeps; default 0).  Samples never depend on it."""
         capi.check(capi.lib().vpt_gpu_set_latency_kernel(self.h, int(mode), int(ungated)), "vpt_gpu_set_latency_kernel")
 
+    def set_compaction(self, every: int) -> None:
+        """Live-path compaction on partly filled latency launches every `every` outer iterations (0: off);
+        see include/vpt_gpu.h vpt_gpu_set_compaction.  Samples never depend on it."""
+        capi.check(capi.lib().vpt_gpu_set_compaction(self.h, int(every)), "vpt_gpu_set_compaction")
+
     def latency_kernel_info(self) -> dict:
         m, b = C.c_int(), C.c_int()
         capi.check(capi.lib().vpt_gpu_latency_kernel_info(self.h, C.byref(m), C.byref(b)), "vpt_gpu_latency_kernel_info")
