@@ -135,7 +135,8 @@ def dropin_frames(wl, frames: int = 3, timeout_s: int = 300):
     TileProvider and one worker thread calling vpt_gpu::drain (include/vpt_run.hpp: one staged feed, the
     pusher and film threads, the 0.2-s progressive film) -- through tests/native/run_gpu_harness, on this
     config's frame: `frames` frames on one context (setup -- grid upload, tile costs, the feed's memory --
-    outside the timed drains, as the harness and run_checked do it).  Then the provider alone (mode=tokens: one
+    outside the timed drains, as the harness and run_checked do it) after one untimed frame (the GPU clocks up
+    out of idle over the first frames: r05f, C4 206 / 188 / 170 / 124 ms).  Then the provider alone (mode=tokens: one
     thread taking every token of the frame), the drop-in's host-side floor.  A child process, started before
     this process touches the GPU.  None for configs the harness does not run (C2's constant cube, C5)."""
     import subprocess
@@ -148,8 +149,8 @@ def dropin_frames(wl, frames: int = 3, timeout_s: int = 300):
     base = [str(HARNESS), f"config={scene}", f"w={W}", f"h={H}", f"waves={spp}", f"grid_n={wl.grid_n}", "threads=1",
             "batch=4096", f"temperature={1 if wl.temperature else 0}"]
     with tempfile.TemporaryDirectory() as tmp:
-        r = subprocess.run(base + [f"out={tmp}/film.f32", f"frames={frames}"], capture_output=True, text=True,
-                           timeout=timeout_s)
+        r = subprocess.run(base + [f"out={tmp}/film.f32", f"frames={frames}", "warmup=1"], capture_output=True,
+                           text=True, timeout=timeout_s)
         if r.returncode != 0:
             log(f"bench: drop-in harness failed ({r.returncode}): {r.stderr[-500:]}")
             return {"error": r.returncode}
@@ -160,7 +161,8 @@ def dropin_frames(wl, frames: int = 3, timeout_s: int = 300):
     med = sorted(ms)[len(ms) // 2]
     rec = {"path": "vpt_gpu::drain (include/vpt_run.hpp) behind the restated TileProvider, main.cpp:46-87 headless "
                    "(tests/native/run_gpu_harness), 1 worker thread, 0.2-s progressive film",
-           "workload": f"{wl.name}: {W}x{H}, {spp} spp", "frames": len(ms), "ms_frames": ms, "ms_per_frame": med,
+           "workload": f"{wl.name}: {W}x{H}, {spp} spp", "frames": len(ms), "warmup_frames": 1, "ms_frames": ms,
+           "ms_per_frame": med,
            "value": round(W * H * spp / (med / 1e3) / 1e6, 3), "unit": "Msamples/s", "film_counts_exact": counts_ok}
     for line in t.stdout.splitlines():
         if "tokens_ms" in line:  # "tokens_ms 125.5, 8294400 tokens, 66.1 M tokens/s, 1 threads"
@@ -416,6 +418,9 @@ def main():
                     help="the latency kernel (cold lane state in VGPRs): auto = latency-bound launches (C1, latency "
                          "gates) and partly filled ones (C2, small shares; the context's gates); off never; on / gated "
                          "force it with the latency / the context's gates on partly filled launches (A/B runs)")
+    ap.add_argument("--compaction", type=int, default=None,
+                    help="live-path compaction period on partly filled latency launches (A/B runs; default: the "
+                         "library's, off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the reference-API (drop-in) frame timing")
     ap.add_argument("--dropin-frames", type=int, default=3)
@@ -437,7 +442,11 @@ def main():
     import torch.distributed as dist
 
     dropin = None
-    if world == 1 and not args.no_dropin and args.rng_mode == "reference" and args.spp is None and args.grid_n is None:
+    # (not under rocprofv3: its preloaded library has initialised the GPU in this process, which then must not
+    # start another program)
+    profiled = any(k.startswith("ROCPROF") for k in os.environ)
+    if (world == 1 and not args.no_dropin and not profiled and args.rng_mode == "reference" and args.spp is None
+            and args.grid_n is None):
         # the drop-in runs in a child process, before this one touches the GPU
         from volume_path_tracer_amd.scenes import workload as _workload
 
@@ -466,6 +475,8 @@ def main():
         mode, ungated = {"auto": (-1, -1), "off": (0, -1), "on": (1, 1), "gated": (1, 0)}[args.latency_kernel]
         it.set_latency_kernel(mode, ungated)
         lat_info = it.latency_kernel_info()
+    if args.compaction is not None:
+        it.set_compaction(args.compaction)
     log(f"[rank {rank}] grids ready in {time.time() - t0:.1f}s: {dens.leaf_count} leaves, "
         f"launch {it.launch_info()}, latency kernel {lat_info}")
 
@@ -527,7 +538,8 @@ def main():
                        "width": wl.cfg.width, "height": wl.cfg.height, "spp": spp,
                        "jobs_per_step_per_gpu": jobs_rank, "volume": f"synthetic {wl.grid_n}^3 kind {wl.density_kind}",
                        "parallelism": f"wave-sharded x{world} ({args.mode}), RCCL film all-reduce" if world > 1 else "1 GPU",
-                       "rng_mode": args.rng_mode, "latency_kernel": args.latency_kernel},
+                       "rng_mode": args.rng_mode, "latency_kernel": args.latency_kernel,
+                       **({"compaction": args.compaction} if args.compaction is not None else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_source": traffic_source,

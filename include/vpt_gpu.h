@@ -426,7 +426,7 @@ int vpt_gpu_set_latency_kernel(vpt_gpu_ctx* ctx, int mode, int ungated);
 /* Live-path compaction (north_star's "ballot/prefix-sum to compact live rays") on the latency kernel's partly
  * filled launches (e.g. C2): every `every` outer iterations a block's four wavefronts meet and, when packing
  * helps, move their paths through LDS so that walking paths fill the first wavefronts (a kernel variant with a
- * 56 KiB LDS exchange: <= 2 blocks per CU; launches with more blocks per CU do not use it).  0 (default): off.
+ * 60 KiB LDS exchange: <= 2 blocks per CU; launches with more blocks per CU do not use it).  0 (default): off.
  * Samples never depend on it (counters: `exchanged`).  Takes effect at the next launch. */
 int vpt_gpu_set_compaction(vpt_gpu_ctx* ctx, int every);
 /* The mode and the latency kernel's resident blocks per CU. */

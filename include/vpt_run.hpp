@@ -66,6 +66,9 @@ struct DrainOptions {
   // When the provider runs dry the held jobs are pushed costliest tile first (vpt_gpu_tile_costs), so the launch
   // ends on cheap jobs -- the one-launch frame's cost tail (VPT_ORDER_COST_TAIL), over the jobs still held.
   bool cost_tail = true;
+  // Before that, every push of held jobs (kChunk = 16 384 at a time, half a C3 wave) goes costliest tile first
+  // -- the one-launch frame's wave-major cost order (VPT_ORDER_COST_WAVE_MAJOR), chunk by chunk.
+  bool cost_chunks = true;
 };
 
 // Takes up to max_jobs tokens; on_token(token&) sees each before it is released.  Returns the count.
@@ -127,7 +130,8 @@ class FeedPipeline {
     lanes_ = lanes;
     hold_max_ = opt.hold_jobs ? opt.hold_jobs : 2 * lanes;
     backlog_ = opt.backlog_jobs ? opt.backlog_jobs : lanes;
-    if (opt.cost_tail) {  // cost classes per tile, before the feed holds the device (the cost pass syncs)
+    cost_chunks_ = opt.cost_chunks;
+    if (opt.cost_tail || opt.cost_chunks) {  // cost classes per tile, before the feed holds the device (the cost pass syncs)
       uint64_t T = 0, total = 0;
       if (int rc = vpt_gpu_job_space(ctx_, &T, &total)) return rc;
       std::vector<uint32_t> rank(T);
@@ -135,6 +139,7 @@ class FeedPipeline {
       cls_.assign(T, 0);
       for (uint64_t i = 0; i < T; ++i) cls_[rank[i]] = (uint8_t)((i * kClasses) / T);  // 0: costliest
     }
+    cost_tail_ = opt.cost_tail;
     // the ring holds the backlog plus the lanes' reservations; the feed's own stream
     if (int rc = vpt_gpu_feed_open_staged(ctx_, nullptr, nullptr, backlog_ + lanes, &feed_)) return rc;
     pusher_ = std::thread([this] { pusher_main(); });
@@ -196,6 +201,17 @@ class FeedPipeline {
     taker_cv_.notify_all();
   }
   int push(const uint64_t* ids, uint64_t n) { return n ? vpt_gpu_feed_push(feed_, ids, n) : VPT_OK; }
+  // ids[0..n) costliest tile class first (a counting sort; the order taken within a class: consecutive items
+  // are different tiles of one wave), into sorted_.
+  const uint64_t* by_cost(const uint64_t* ids, uint64_t n) {
+    const uint64_t T = cls_.size();
+    uint64_t start[kClasses + 1] = {};
+    for (uint64_t i = 0; i < n; ++i) ++start[cls_[ids[i] % T] + 1];
+    for (int c = 0; c < kClasses; ++c) start[c + 1] += start[c];
+    sorted_.resize(n);
+    for (uint64_t i = 0; i < n; ++i) sorted_[start[cls_[ids[i] % T]]++] = ids[i];
+    return sorted_.data();
+  }
   // Pushes held jobs, oldest first, while the feed's backlog is below its mark -- and, until the launch has
   // started (it starts once a lane's worth of jobs is pushed, vpt_gpu_feed_push), below the lanes.
   int top_up(std::vector<uint64_t>& hold, size_t& head) {
@@ -204,7 +220,8 @@ class FeedPipeline {
     const uint64_t mark = pushed_ < lanes_ ? std::max(backlog_, lanes_) : backlog_;
     while (head < hold.size() && b < mark) {
       const uint64_t n = std::min<uint64_t>(kChunk, hold.size() - head);
-      if (int rc = push(hold.data() + head, n)) return rc;
+      const uint64_t* ids = hold.data() + head;
+      if (int rc = push(cost_chunks_ && !cls_.empty() ? by_cost(ids, n) : ids, n)) return rc;
       head += n;
       b += n;
       pushed_ += n;
@@ -251,14 +268,9 @@ class FeedPipeline {
     // items are different tiles of one wave), then the end of the feed.
     std::vector<uint64_t> rest(hold.begin() + (ptrdiff_t)head, hold.end());
     detail::drain_trace("final_hold", (double)rest.size(), (double)pushed_);
-    if (!cls_.empty() && !rest.empty()) {
-      const uint64_t T = cls_.size();
-      uint64_t start[kClasses + 1] = {};
-      for (uint64_t j : rest) ++start[cls_[j % T] + 1];
-      for (int c = 0; c < kClasses; ++c) start[c + 1] += start[c];
-      std::vector<uint64_t> sorted(rest.size());
-      for (uint64_t j : rest) sorted[start[cls_[j % T]]++] = j;
-      rest.swap(sorted);
+    if (cost_tail_ && !cls_.empty() && !rest.empty()) {
+      by_cost(rest.data(), rest.size());
+      rest.swap(sorted_);
     }
     for (size_t i = 0; i < rest.size(); i += kChunk)
       if (int rc = push(rest.data() + i, std::min<uint64_t>(kChunk, rest.size() - i))) return fail(rc);
@@ -298,6 +310,8 @@ class FeedPipeline {
   uint64_t pushed_ = 0;  // (the pusher's)
   vpt_gpu_feed* feed_ = nullptr;
   std::vector<uint8_t> cls_;  // per tile: cost class (0 = costliest)
+  bool cost_tail_ = true, cost_chunks_ = true;
+  std::vector<uint64_t> sorted_;  // (the pusher's)
   std::thread pusher_, film_;
   std::mutex mu_;  // queue_, queued_, held_, no_more_, err_
   std::condition_variable taker_cv_;

@@ -185,7 +185,7 @@ int vpt_gpu_feed_collect(vpt_gpu_feed* f, float* host) {
 int main(int argc, char** argv) {
   std::map<std::string, long long> a{{"drivers", 1}, {"helpers", 0}, {"w", 72}, {"h", 40}, {"waves", 5},
                                      {"batch", 7}, {"flush_ms", 0}, {"hold", 0}, {"backlog", 0}, {"stop_after", 0},
-                                     {"cost_tail", 1}};
+                                     {"cost_tail", 1}, {"cost_chunks", 1}};
   for (int i = 1; i < argc; ++i) {
     const char* eq = std::strchr(argv[i], '=');
     if (eq) a[std::string(argv[i], eq - argv[i])] = std::atoll(eq + 1);
@@ -215,6 +215,7 @@ int main(int argc, char** argv) {
   opt.hold_jobs = (uint64_t)a["hold"];
   opt.backlog_jobs = (uint64_t)a["backlog"];
   opt.cost_tail = a["cost_tail"] != 0;
+  opt.cost_chunks = a["cost_chunks"] != 0;
   {
     std::lock_guard<std::mutex> l(vpt_gpu::detail::Helpers::get().mu);
     vpt_gpu::detail::Helpers::get().drivers += drivers;  // (run() counts them when they claim a device)

@@ -5,7 +5,7 @@
 //
 //   run_gpu_harness config=<scene.json> out=<film.f32> [mode=drain|run w= h= waves= threads= batch=
 //                   grid_n= dist= temperature=0|1 stop_after=<jobs> nvdb=<file.nvdb> gridbuf=<file>
-//                   tempbuf=<file> hold= backlog= flush_ms= cost_tail= helpers= grid_blocks= sample_ms= frames=]
+//                   tempbuf=<file> hold= backlog= flush_ms= cost_tail= cost_chunks= helpers= grid_blocks= sample_ms= frames= warmup=]
 //
 // mode=drain (default): each thread owns a context made with vpt_gpu_create and calls
 //   vpt_gpu::drain(ctx, tp, film, batch).  The volume is nvdb= (vpt_grid_read_nvdb: "density", and
@@ -205,6 +205,7 @@ int main(int argc, char** argv) {
     opt.hold_jobs = (uint64_t)num("hold", (long long)opt.hold_jobs);
     opt.backlog_jobs = (uint64_t)num("backlog", (long long)opt.backlog_jobs);
     opt.cost_tail = num("cost_tail", opt.cost_tail ? 1 : 0) != 0;
+    opt.cost_chunks = num("cost_chunks", opt.cost_chunks ? 1 : 0) != 0;
     opt.flush_seconds = (double)num("flush_ms", (long long)(opt.flush_seconds * 1000)) / 1000.0;
     if (num("grid_blocks", 0) > 0)
       for (auto* c : ctx)
@@ -212,8 +213,10 @@ int main(int argc, char** argv) {
     for (auto* c : ctx)  // setup outside the timed render, as run_checked does it: the tile-cost pass, the feed's memory
       if (vpt_gpu_tile_costs(c, nullptr, nullptr) || vpt_gpu_feed_prepare(c, 0, 1) || vpt_gpu_sync(c)) return fail("warm-up");
     // frames=N: N - 1 more frames first, each with a fresh provider and film (main.cpp renders one frame per
-    // process: these time the same drain again, on the contexts already built), one render_ms line each
-    for (long long fr = 1; fr < num("frames", 1); ++fr) {
+    // process: these time the same drain again, on the contexts already built), one render_ms line each;
+    // warmup=M: M more such frames before them, untimed (a GPU coming out of idle clocks up over the first ones)
+    const long long warm = num("warmup", 0);
+    for (long long fr = 1 - warm; fr < num("frames", 1); ++fr) {
       vpt_headless::TileProvider tp2(cfg.output_size[0], cfg.output_size[1], cfg.num_waves, cfg.tile_size[0], cfg.tile_size[1]);
       vpt_headless::Image<float, 4> film2(cfg.output_size[0], cfg.output_size[1]);
       float* fh2 = reinterpret_cast<float*>(film2.data().data());
@@ -223,7 +226,7 @@ int main(int argc, char** argv) {
       for (auto& t : pool) t.join();
       for (int i = 0; i < threads; ++i)
         if (rc[i]) return fail("vpt_gpu::drain");
-      std::printf("run_gpu_harness: render_ms %.1f\n",
+      std::printf("run_gpu_harness: %s %.1f\n", fr < 1 ? "warmup_ms" : "render_ms",
                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count());
     }
     {

@@ -19,7 +19,7 @@ CASES = [
     "drivers=3 helpers=2 flush_ms=1 batch=1",
     "drivers=1 helpers=4 stop_after=50 batch=2",
     "drivers=2 helpers=7 batch=1 w=200 h=120 waves=4",
-    "drivers=1 helpers=0 hold=100 cost_tail=0 batch=7",
+    "drivers=1 helpers=0 hold=100 cost_tail=0 cost_chunks=0 batch=7",
     "drivers=1 helpers=0 hold=5 backlog=3 batch=7 flush_ms=1",
     "drivers=2 helpers=3 hold=37 backlog=11 batch=5 stop_after=90 flush_ms=1",
 ]

@@ -16,7 +16,7 @@ for r in $(seq 1 $ROUNDS); do
     L=$BASE; [ $v = variant ] && L=$VAR
     for c in ${CFGS//,/ }; do
       f=$O/b_${v}_${c}_$r
-      VPT_LIB=$L timeout -k 10 200 python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > $f.json 2> $f.err || exit 1
+      VPT_LIB=$L timeout -k 10 200 python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-dropin > $f.json 2> $f.err || exit 1
       python -c "import json; d=json.loads(open('$f.json').read().strip().splitlines()[-1]); print('$v $c $r', d['ms_per_step'], d['value'])"
     done
   done

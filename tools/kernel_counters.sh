@@ -11,7 +11,7 @@ i=0
 while IFS= read -r P; do
   [ -z "$P" ] && continue
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $O/pass_$i -o run -- python3 bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline "$@" > $O/pass_$i.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $O/pass_$i -o run -- python3 bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline --no-dropin "$@" > $O/pass_$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc: $P"; if [ $rc -ne 0 ]; then tail -3 $O/pass_$i.log; exit $rc; fi
 done <<'PASSES'
 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU

@@ -6,7 +6,7 @@ set -u
 O=${1:-gpurun_out/lat_ab}; mkdir -p $O
 one() {  # tag, args...
   local tag=$1; shift
-  timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > $O/$tag.json 2> $O/$tag.err || { echo "$tag failed"; tail -3 $O/$tag.err; exit 1; }
+  timeout -k 10 300 python bench.py --no-cpu-baseline --no-dropin "$@" > $O/$tag.json 2> $O/$tag.err || { echo "$tag failed"; tail -3 $O/$tag.err; exit 1; }
   python3 -c "import json,sys; j=json.loads(open('$O/$tag.json').read().strip().splitlines()[-1]); print('$tag', j['config']['latency_kernel'], j['ms_per_step'], j['value'])"
 }
 for r in 1 2; do

@@ -11,7 +11,7 @@ step() { local name=$1 to=$2; shift 2; echo "== $name"; timeout -k 10 "$to" "$@"
 i=0
 while IFS= read -r P; do
   i=$((i+1))
-  step pmc_$i 300 rocprofv3 --pmc $P --output-format csv -d $O/pmc_$i -o run -- python3 bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline
+  step pmc_$i 300 rocprofv3 --pmc $P --output-format csv -d $O/pmc_$i -o run -- python3 bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline --no-dropin
 done <<'PASSES'
 TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum
 TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum
@@ -21,5 +21,5 @@ TCC_HIT_sum TCC_MISS_sum
 PASSES
 python3 tools/pmc_traffic.py ${TAG}_${CFG} $CFG $(python3 -c "from volume_path_tracer_amd.scenes import workload; print(workload('$CFG').spp)") $O/pmc_* || exit 1
 cp profiles/${TAG}_${CFG}_pmc.json $O/
-step rocprof 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --config $CFG --no-cpu-baseline
+step rocprof 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --config $CFG --no-cpu-baseline --no-dropin
 if [ "$CFG" = "c3" ]; then step bench 900 python3 bench.py; tail -1 $O/bench.log | cut -c1-400; fi

@@ -9,7 +9,7 @@ for L in ${LIBS}; do
   i=0
   for P in "$P1" "$P2"; do
     i=$((i+1))
-    VPT_LIB=$PWD/volume_path_tracer_amd/lib/$L.so timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $O/$L/p$i -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/$L.p$i.log 2>&1
+    VPT_LIB=$PWD/volume_path_tracer_amd/lib/$L.so timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $O/$L/p$i -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-dropin > $O/$L.p$i.log 2>&1
     rc=$?; echo "$L pass $i rc=$rc"; if [ $rc -ne 0 ]; then tail -3 $O/$L.p$i.log; exit $rc; fi
   done
 done

@@ -11,6 +11,6 @@ i=0
 while IFS= read -r P; do
   [ -z "$P" ] && continue
   i=$((i+1)); N=p$i
-  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $O/pmc_$N -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline "$@" > $O/pmc_$N.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $O/pmc_$N -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-dropin "$@" > $O/pmc_$N.log 2>&1
   rc=$?; echo "pass $i ($P) rc=$rc"; if [ $rc -ne 0 ]; then tail -3 $O/pmc_$N.log; exit $rc; fi
 done <<< "$PASSES"

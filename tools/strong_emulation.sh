@@ -7,6 +7,6 @@ set -u
 O=gpurun_out/${1:-strong}; mkdir -p $O; export TMPDIR=/tmp
 for spec in "c3 256" "c3 128" "c3 64" "c3 32" "c5 1024" "c5 256" "c5 128"; do
   set -- $spec
-  timeout -k 10 300 python3 bench.py --config $1 --spp $2 --steps 3 --warmup 1 --no-cpu-baseline > $O/strong_$1_$2.json 2> $O/strong_$1_$2.err
+  timeout -k 10 300 python3 bench.py --config $1 --spp $2 --steps 3 --warmup 1 --no-cpu-baseline --no-dropin > $O/strong_$1_$2.json 2> $O/strong_$1_$2.err
   rc=$?; echo "$1 spp $2 rc=$rc $(grep -o '"ms_per_step": [0-9.]*' $O/strong_$1_$2.json)"; if [ $rc -ne 0 ]; then tail -3 $O/strong_$1_$2.err; exit $rc; fi
 done

@@ -328,13 +328,13 @@ using KernelEnv = KernelEnvT<false>;
 // evaluation) and 12.5 finished paths (r05f census, profiles/r05f_c2_census.txt).  Every `compact_every` outer
 // iterations the block's four wavefronts meet (two barriers), count their walking / other live paths with
 // ballots, and -- when packing would leave fewer wavefronts holding walkers, or live paths -- move every path
-// (its hot Lane registers and its cold state, which this kernel keeps in VGPRs: kXWords words) through LDS so
+// (its hot Lane registers and its cold state, which this kernel keeps in VGPRs: 54 words, 58 with a temperature grid) through LDS so
 // that walkers fill the block's first wavefronts, the other live paths the next, finished ones the last.  A
 // wavefront without a live path skips its iterations until the next meeting; the block ends when none is left.
 // A path's operations and draws never depend on the thread that runs it (its RNG state and every value it reads
 // travel with it; the gates only choose when a block runs), so samples are bit-identical; only the order of the
 // film's fp32 atomics changes.  The HDDA step counter stays with the thread (it is summed per launch).
-constexpr int kXWords = 56;  // 53 state words, padded to uint4
+constexpr int kXWords = 60;  // 54 state words (58 with a temperature grid), padded to uint4
 __device__ __forceinline__ uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
 __device__ __forceinline__ float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 template <bool HasTemp>
@@ -357,9 +357,10 @@ __device__ __forceinline__ void xchg_pack(const Lane& ln, const LaneCold& lc, ui
   if (HasTemp) {
     x[n++] = (uint32_t)ln.temp_cell.i; x[n++] = (uint32_t)ln.temp_cell.j; x[n++] = (uint32_t)ln.temp_cell.k;
   }
-  x[n++] = HasTemp ? (uint32_t)ln.temp_cell.code : 0u;
+  if (HasTemp) x[n++] = (uint32_t)ln.temp_cell.code;
   while (n < kXWords) x[n++] = 0;
 }
+static_assert(54 + 4 <= kXWords, "the exchange holds every state word");
 template <bool HasTemp>
 __device__ __forceinline__ void xchg_unpack(Lane& ln, LaneCold& lc, const uint32_t x[kXWords]) {
   int n = 0;
@@ -383,7 +384,7 @@ __device__ __forceinline__ void xchg_unpack(Lane& ln, LaneCold& lc, const uint32
   }
   if (HasTemp) ln.temp_cell.code = (int32_t)x[n];
 }
-// Dynamic LDS of the compacting kernel: [kXWords / 4][kBlockThreads] uint4 (57 344 B).
+// Dynamic LDS of the compacting kernel: [kXWords / 4][kBlockThreads] uint4 (61 440 B).
 constexpr size_t kXchgBytes = (size_t)kXWords * kBlockThreads * sizeof(uint32_t);
 
 template <bool HasTemp, bool Runs>
