@@ -286,9 +286,16 @@ class FeedPipeline {
         std::this_thread::sleep_for(std::chrono::milliseconds(1));
         continue;
       }
-      next += std::chrono::duration_cast<std::chrono::steady_clock::duration>(std::chrono::duration<double>(flush_));
-      std::lock_guard<std::mutex> lock(film_mutex());
-      if (int rc = vpt_gpu_feed_snapshot(feed_, film_host_)) return fail(rc);
+      const auto period = std::chrono::duration_cast<std::chrono::steady_clock::duration>(std::chrono::duration<double>(flush_));
+      next += period;
+      {
+        std::lock_guard<std::mutex> lock(film_mutex());
+        if (int rc = vpt_gpu_feed_snapshot(feed_, film_host_)) return fail(rc);
+      }
+      // a snapshot that overran its period skips the missed ones: back-to-back snapshots would hold the film
+      // lock (and the feed's) nearly all the time
+      const auto now = std::chrono::steady_clock::now();
+      if (next <= now) next = now + period;
     }
   }
   void stop_threads() {

@@ -63,6 +63,11 @@ out = {"block_first_fetch_ms_pct": {p: float(np.percentile(first, p) / 1e5) for 
        "first_below_95pct_lanes_ms": first_idle, "lane_busy_fraction": busy, "drain_ms": span / 1e5 - first_idle,
        "job_ms_mean": float(dur.mean() / 1e5), "job_ms_p99": float(np.percentile(dur, 99) / 1e5),
        "job_ms_max": float(dur.max() / 1e5),
+       # the launch's lower bounds: the longest single job (one lane traces it serially) and the work spread
+       # evenly over every lane; span / max(both) is how far the drain is from ideal
+       "work_over_lanes_ms": float(dur.sum() / lanes / 1e5),
+       "ideal_span_ms": float(max(dur.max(), dur.sum() / lanes) / 1e5),
+       "span_over_ideal": float(span / max(dur.max(), dur.sum() / lanes)),
        "last_2000_jobs_start_ms_min": float(t0[last].min() / 1e5), "last_2000_jobs_dur_ms_max": float(dur[last].max() / 1e5),
        "rank_corr_measured_vs_estimated_cost": float(rc),
        "running_jobs_at_ms": {f"{x:.0f}": float(run[int(x * 2)]) for x in np.linspace(0, span / 1e5 - 0.5, 41)}}
