@@ -1,6 +1,6 @@
 #!/bin/bash
 # The drop-in's drain (include/vpt_run.hpp: one staged feed, pusher and film threads) on the full C3 frame
-# (1920x1080, 256 waves, 512^3 stand-in) and the C4 frame, one host thread, across the run-ahead bounds (hold /
+# (1920x1080, 256 waves, 512^3 stand-in), the C4 frame and the C5 frame (3840x2160, 1 024 waves), one host thread, across the run-ahead bounds (hold /
 # backlog), the cost tail and the film period; each line: the knobs and render_ms (bench.py's C3 frame is the
 # one-launch reference), one warm-up frame and 3 timed frames per setting.  Then the provider alone (mode=tokens:
 # the host-side floor) and a run sampling what main.cpp's window would show every 50 ms.
@@ -28,6 +28,9 @@ run c3_default2 wdas_cloud "$@"
 run c4_default fire "$@"
 run c4_nofilm fire flush_ms=100000 "$@"
 run c4_default2 fire "$@"
+# C5 (3840x2160, 1 024 waves): the 133-MB film's snapshots every 0.2 s (bench.py's C5 one-launch: ~5.2 s)
+run c5_default wdas_cloud w=3840 h=2160 waves=1024 warmup=0 frames=2 "$@"
+run c5_nofilm wdas_cloud w=3840 h=2160 waves=1024 warmup=0 frames=2 flush_ms=100000 "$@"
 for th in 1 2; do
   timeout -k 10 60 $H config=volume_path_tracer_amd/scenes/wdas_cloud.json out=$O/x w=1920 h=1080 waves=256 mode=tokens \
     threads=$th > $O/tokens_$th.log 2>&1 && echo "provider alone: $(grep tokens_ms $O/tokens_$th.log)"

@@ -9,6 +9,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c3")
 ap.add_argument("--spp", type=int, default=None)
 ap.add_argument("--out", default="gpurun_out/joblog")
+ap.add_argument("--alone", type=int, default=0,
+                help="then render the N longest jobs again one at a time (one lane on the device), on the "
+                     "throughput and the latency kernel: their duration without the full launch's contention")
 a = ap.parse_args()
 import torch
 from volume_path_tracer_amd.render import Integrator
@@ -71,6 +74,27 @@ out = {"block_first_fetch_ms_pct": {p: float(np.percentile(first, p) / 1e5) for 
        "last_2000_jobs_start_ms_min": float(t0[last].min() / 1e5), "last_2000_jobs_dur_ms_max": float(dur[last].max() / 1e5),
        "rank_corr_measured_vs_estimated_cost": float(rc),
        "running_jobs_at_ms": {f"{x:.0f}": float(run[int(x * 2)]) for x in np.linspace(0, span / 1e5 - 0.5, 41)}}
+if a.alone:
+    # the longest jobs alone: a launch of one job (its lane has a SIMD to itself); each twice, the second kept
+    one = torch.zeros(4, dtype=torch.float32, device="cuda")
+    def alone_ms(jid):
+        for _ in range(2):
+            one.zero_()
+            capi.check(capi.lib().vpt_gpu_render_jobs_records(it.h, int(jid), 1, C.c_void_p(it.film.data_ptr()),
+                                                              C.c_void_p(one.data_ptr()), C.c_void_p(None)), "render")
+            torch.cuda.synchronize()
+        r = one.view(torch.int32).cpu().numpy().view(np.uint32).astype(np.int64)
+        assert r[0] == tile[jid], ("the one-job launch rendered another tile", int(r[0]), int(tile[jid]))
+        return float((r[2] - r[1]) / 1e5)
+    top = np.argsort(dur)[::-1][:a.alone]
+    rows = []
+    for lat in (0, 1):
+        it.set_latency_kernel(lat, 0)
+        rows.append([alone_ms(j) for j in top])
+    it.set_latency_kernel(-1, 0)
+    out["longest_jobs"] = [{"jid": int(j), "tile": int(tile[j]), "in_launch_ms": float(dur[j] / 1e5),
+                            "start_ms": float(t0[j] / 1e5), "alone_ms": rows[0][i], "alone_latency_kernel_ms": rows[1][i]}
+                           for i, j in enumerate(top)]
 Path(a.out).mkdir(parents=True, exist_ok=True)
 np.save(Path(a.out) / f"tile_cost_{a.config}.npy", cost.astype(np.float32))
 Path(a.out, f"summary_{a.config}.json").write_text(json.dumps(out, indent=1))
