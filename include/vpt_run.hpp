@@ -236,6 +236,7 @@ class FeedPipeline {
     return VPT_OK;
   }
   void pusher_main() {
+    (void)vpt_gpu_bind_thread_near(ctx_, nullptr);  // the ring is in the GPU's node's memory
     std::vector<uint64_t> hold;  // taken, not pushed: hold[head..] in the order taken
     size_t head = 0;
     JobRuns batch;
@@ -280,6 +281,7 @@ class FeedPipeline {
     held_ = 0;
   }
   void film_main() {
+    (void)vpt_gpu_bind_thread_near(ctx_, nullptr);  // the pinned film copies are there too
     auto next = std::chrono::steady_clock::now() + std::chrono::duration<double>(flush_);
     while (!film_stop_.load()) {
       if (std::chrono::steady_clock::now() < next) {  // (slices of 1 ms: stop_threads() ends the wait)

@@ -100,6 +100,10 @@ int vpt_gpu_tile_costs(vpt_gpu_ctx*, float*, uint32_t* rank) {  // the last tile
   return VPT_OK;
 }
 int vpt_gpu_feed_prepare(vpt_gpu_ctx*, uint64_t, int) { return VPT_OK; }
+int vpt_gpu_bind_thread_near(vpt_gpu_ctx*, int* node) {
+  if (node) *node = -1;
+  return VPT_OK;
+}
 int vpt_gpu_feed_open(vpt_gpu_ctx* c, float* film, void* stream, uint64_t, vpt_gpu_feed** out) {
   if (!stream) return VPT_E_INVALID;
   *out = new vpt_gpu_feed();

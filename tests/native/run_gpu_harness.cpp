@@ -4,7 +4,7 @@
 // with the oracle.
 //
 //   run_gpu_harness config=<scene.json> out=<film.f32> [mode=drain|run w= h= waves= threads= batch=
-//                   grid_n= dist= temperature=0|1 stop_after=<jobs> nvdb=<file.nvdb> gridbuf=<file>
+//                   grid_n= dist= temperature=0|1 stop_after=<jobs> nvdb=<file.nvdb> gridbuf=<file> taker_node=<n>
 //                   tempbuf=<file> hold= backlog= flush_ms= cost_tail= cost_chunks= helpers= grid_blocks= sample_ms= frames= warmup=]
 //
 // mode=drain (default): each thread owns a context made with vpt_gpu_create and calls
@@ -37,6 +37,9 @@
 #include <thread>
 #include <vector>
 
+#include <pthread.h>
+#include <sched.h>
+
 #include "reference_types_headless.hpp"
 #include "tile_provider_headless.hpp"
 #include "vpt_run.hpp"
@@ -66,9 +69,30 @@ std::vector<char> slurp(const std::string& path) {
 
 vpt_headless::Vector3f v3(const float* f) { return vpt_headless::Vector3f{{f[0], f[1], f[2]}}; }
 
+// taker_node=N: the driving threads (the takers) run on NUMA node N's CPUs (/sys cpulist); -1: wherever
+void pin_to_node(long long node) {
+  if (node < 0) return;
+  std::ifstream in("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
+  std::string list;
+  if (!std::getline(in, list)) return;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  for (size_t pos = 0; pos < list.size();) {
+    size_t end = list.find(',', pos);
+    if (end == std::string::npos) end = list.size();
+    const std::string r = list.substr(pos, end - pos);
+    const size_t dash = r.find('-');
+    const int a = std::atoi(r.c_str()), b = dash == std::string::npos ? a : std::atoi(r.c_str() + dash + 1);
+    for (int c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET(c, &set);
+    pos = end + 1;
+  }
+  (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
+  std::setvbuf(stdout, nullptr, _IOLBF, 0);  // (lines survive a run killed at its time limit)
   std::map<std::string, std::string> a;
   for (int i = 1; i < argc; ++i) {
     const char* eq = std::strchr(argv[i], '=');
@@ -222,7 +246,11 @@ int main(int argc, char** argv) {
       float* fh2 = reinterpret_cast<float*>(film2.data().data());
       const auto r0 = std::chrono::steady_clock::now();
       std::vector<std::thread> pool;
-      for (int i = 0; i < threads; ++i) pool.emplace_back([&, i] { rc[i] = vpt_gpu::drain(ctx[i], tp2, fh2, batch, opt); });
+      for (int i = 0; i < threads; ++i)
+        pool.emplace_back([&, i] {
+          pin_to_node(num("taker_node", -1));
+          rc[i] = vpt_gpu::drain(ctx[i], tp2, fh2, batch, opt);
+        });
       for (auto& t : pool) t.join();
       for (int i = 0; i < threads; ++i)
         if (rc[i]) return fail("vpt_gpu::drain");
@@ -236,7 +264,10 @@ int main(int argc, char** argv) {
       // helpers=N: N more threads take tokens for the drivers (vpt_gpu::help, as run()'s non-driving threads do)
       const int helpers = (int)num("helpers", 0);
       for (int i = 0; i < threads; ++i)
-        pool.emplace_back([&, i] { rc[i] = vpt_gpu::drain(ctx[i], sp, fh, batch, opt, nullptr, helpers > 0); });
+        pool.emplace_back([&, i] {
+          pin_to_node(num("taker_node", -1));
+          rc[i] = vpt_gpu::drain(ctx[i], sp, fh, batch, opt, nullptr, helpers > 0);
+        });
       std::vector<int> hrc(helpers, 0);
       {
         // the drivers register their pipelines as they start; helpers wait for one (Helpers::drivers counts

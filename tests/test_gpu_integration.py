@@ -441,3 +441,41 @@ def test_staged_feed_snapshots_add_up_to_the_film():
     np.testing.assert_allclose(host[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
     # the collect left the feed's film zero
     assert not it.film.any().item()
+
+
+@pytest.mark.gpu
+def test_bind_thread_near_binds_to_the_gpus_node():
+    """vpt_gpu_bind_thread_near: a thread -- here one whose own CPU set was narrowed to a single CPU, as a
+    thread inherits its creator's -- ends up on the CPUs of the device's NUMA node that the process may use
+    (the node from sysfs, the process's set), or is left as it was when the node is unknown."""
+    import ctypes as C
+    import os
+    import threading
+
+    from volume_path_tracer_amd import capi
+    from volume_path_tracer_amd.render import Integrator
+
+    wl = workload("c3", width=32, height=32, spp=1, grid_n=64)
+    it = Integrator(wl.cfg, SynthGrid(1, 64).grid(), None, device=0)
+    proc = os.sched_getaffinity(0)
+    out = {}
+
+    def body():
+        os.sched_setaffinity(0, {min(proc)})
+        node = C.c_int(-2)
+        out["rc"] = capi.lib().vpt_gpu_bind_thread_near(it.h, C.byref(node))
+        out["node"], out["cpus"] = node.value, os.sched_getaffinity(0)
+
+    t = threading.Thread(target=body)
+    t.start()
+    t.join()
+    assert out["rc"] == 0
+    if out["node"] < 0:
+        assert out["cpus"] == {min(proc)}
+        return
+    text = Path(f"/sys/devices/system/node/node{out['node']}/cpulist").read_text().strip()
+    node_cpus = set()
+    for part in text.split(","):
+        a, _, b = part.partition("-")
+        node_cpus.update(range(int(a), int(b or a) + 1))
+    assert out["cpus"] == node_cpus & proc, (out["node"], sorted(out["cpus"])[:8])

@@ -262,6 +262,8 @@ def lib() -> C.CDLL:
     if hasattr(L, "vpt_gpu_set_compaction"):
         L.vpt_gpu_set_compaction.argtypes = [vp, C.c_int]
         L.vpt_gpu_latency_kernel_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    if hasattr(L, "vpt_gpu_bind_thread_near"):
+        L.vpt_gpu_bind_thread_near.argtypes = [vp, C.POINTER(C.c_int)]
     if hasattr(L, "vpt_gpu_stream_create"):
         L.vpt_gpu_stream_create.argtypes = [vp, C.POINTER(vp)]
         L.vpt_gpu_stream_destroy.argtypes = [vp, vp]

@@ -6,12 +6,16 @@
 // fetches into one atomic), so lanes are refilled until the job range is drained and every wave
 // reaches ST_DONE.  Film accumulation uses no-return fp32 atomics into the [H][W][4] XYZW film.
 #include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <sched.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <functional>
 #include <memory>
 #include <atomic>
@@ -1325,6 +1329,43 @@ int vpt_gpu_stream_create(vpt_gpu_ctx* ctx, void** hip_stream) {
   return VPT_OK;
 }
 
+int vpt_gpu_bind_thread_near(vpt_gpu_ctx* ctx, int* node_out) {
+  if (node_out) *node_out = -1;
+  if (!ctx) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_bind_thread_near: null context");
+  char bus[64] = {};
+  if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, ctx->device) != hipSuccess) return VPT_OK;
+  for (char* c = bus; *c; ++c) *c = (char)std::tolower((unsigned char)*c);
+  int node = -1;
+  {
+    std::ifstream in(std::string("/sys/bus/pci/devices/") + bus + "/numa_node");
+    if (!(in >> node) || node < 0) return VPT_OK;
+  }
+  std::ifstream in("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
+  std::string list;
+  if (!std::getline(in, list)) return VPT_OK;
+  // Allowed: the process's CPUs (its main thread's set: taskset / numactl restrict it), not this thread's own --
+  // a thread inherits its creator's set, and a caller bound to the far node would otherwise pin its helpers
+  // there too (r05n: a taker on node 1 made the pusher it started run there).
+  cpu_set_t cur, near;
+  CPU_ZERO(&near);
+  if (sched_getaffinity(getpid(), sizeof cur, &cur) != 0) return VPT_OK;
+  // "0-63,128-191"
+  for (size_t pos = 0; pos < list.size();) {
+    size_t end = list.find(',', pos);
+    if (end == std::string::npos) end = list.size();
+    const std::string r = list.substr(pos, end - pos);
+    const size_t dash = r.find('-');
+    const int a = std::atoi(r.c_str()), b = dash == std::string::npos ? a : std::atoi(r.c_str() + dash + 1);
+    for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
+      if (c >= 0 && CPU_ISSET(c, &cur)) CPU_SET(c, &near);
+    pos = end + 1;
+  }
+  if (CPU_COUNT(&near) == 0) return VPT_OK;
+  if (pthread_setaffinity_np(pthread_self(), sizeof near, &near) != 0) return VPT_OK;
+  if (node_out) *node_out = node;
+  return VPT_OK;
+}
+
 int vpt_gpu_stream_destroy(vpt_gpu_ctx* ctx, void* hip_stream) {
   if (!ctx || !hip_stream) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_stream_destroy: null argument");
   int rc = ctx_device(ctx);
@@ -1548,6 +1589,9 @@ int feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t w
   // launched at once, its idle wavefronts would poll the host link for work (r04).
   f->launched = false;
   f->launch_at = (uint64_t)ctx->grid_blocks * vpt::kBlockThreads;
+  // (A/B knob, r05: VPT_FEED_LAUNCH_DIV=d launches at 1/d of the lanes -- earlier, with idle lanes polling)
+  static const long launch_div = std::getenv("VPT_FEED_LAUNCH_DIV") ? std::atol(std::getenv("VPT_FEED_LAUNCH_DIV")) : 1;
+  if (launch_div > 1) f->launch_at = std::max<uint64_t>(1, f->launch_at / (uint64_t)launch_div);
   feed_trace(f.get(), stage ? "open_stg" : "open", (double)cap, (double)(uintptr_t)hip_stream);
   *out = f.release();
   return VPT_OK;
