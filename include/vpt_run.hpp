@@ -69,6 +69,9 @@ struct DrainOptions {
   // Before that, every push of held jobs (kChunk = 16 384 at a time, half a C3 wave) goes costliest tile first
   // -- the one-launch frame's wave-major cost order (VPT_ORDER_COST_WAVE_MAJOR), chunk by chunk.
   bool cost_chunks = true;
+  // Frames the provider hands out in fewer than direct_below jobs render as jid-range launches instead of a feed
+  // (detail::render_runs); 0 = auto: the launch's lanes (a feed would launch only at its close).  1: always a feed.
+  uint64_t direct_below = 0;
 };
 
 // Takes up to max_jobs tokens; on_token(token&) sees each before it is released.  Returns the count.
@@ -376,9 +379,49 @@ struct Helpers {
 //     under a mutex shared by all callers; the final film is the launch's.
 // `first`: job runs already taken by the caller (queued first).  `share`: other threads of run() may queue
 // into this pipeline while it drains (detail::Helpers); drain returns once they have detached.
+namespace detail {
+inline void append_runs(JobRuns& to, const JobRuns& from) {
+  for (const auto& r : from)
+    if (!to.empty() && to.back().first + to.back().second == r.first)
+      to.back().second += r.second;
+    else
+      to.push_back(r);
+}
+// A frame the provider hands out in fewer jobs than the launch has lanes: a feed's launch would start only at its
+// close anyway (it waits for a lane's worth), on the throughput kernel.  Rendered instead as jid-range launches,
+// which render() sizes as latency-bound or partly filled ones (C1: 4 096 jobs, 49-70 ms through a feed vs the
+// 20.8-ms one-launch frame), then added into the caller's film.
+inline int render_runs(vpt_gpu_ctx* ctx, const JobRuns& runs, float* film_host) {
+  for (const auto& r : runs)
+    if (int rc = vpt_gpu_render_jobs(ctx, r.first, r.second, nullptr, nullptr)) return rc;
+  if (int rc = vpt_gpu_sync(ctx)) return rc;
+  std::lock_guard<std::mutex> lock(film_mutex());
+  return vpt_gpu_film_flush_to_host(ctx, nullptr, film_host);
+}
+}  // namespace detail
+
 template <class Provider>
 int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs, const DrainOptions& opt = {},
           const JobRuns* first = nullptr, bool share = false) {
+  JobRuns head;  // the first lane's worth of jobs, taken before the pipeline starts
+  if (!share) {  // (a shared pipeline takes helpers' jobs: it always runs)
+    int blocks = 0, threads = 0;
+    if (int rc = vpt_gpu_launch_info(ctx, &blocks, &threads)) return rc;
+    const uint64_t direct = opt.direct_below ? opt.direct_below : (uint64_t)blocks * (uint64_t)threads;
+    uint64_t have = 0;
+    if (first) {
+      head = *first;
+      for (const auto& r : head) have += r.second;
+    }
+    JobRuns runs;
+    while (have < direct) {
+      const uint64_t n = take_jobs(tp, std::min<uint64_t>(std::max<uint64_t>(1, batch_jobs), direct - have), runs, [](auto&) {});
+      if (n == 0) return detail::render_runs(ctx, head, film_host);  // the provider is dry: a small frame
+      detail::append_runs(head, runs);
+      have += n;
+    }
+    first = &head;
+  }
   FeedPipeline pipe(ctx);
   int rc = pipe.start(film_host, opt);
   if (rc == VPT_OK && first) rc = pipe.add(*first);

@@ -27,6 +27,7 @@ int64_t g_w = 0, g_h = 0, g_tw = 8, g_th = 8, g_ntx = 0;
 std::mutex g_mu;
 std::vector<uint32_t> g_rendered;  // per jid: times pushed into an open feed
 std::atomic<int> g_open_feeds{0}, g_max_open{0};
+std::atomic<uint64_t> g_direct_jobs{0};  // jobs rendered by jid-range launches (small frames), not feeds
 std::mutex g_dev_mu;            // the "device": feeds in open order
 std::vector<struct vpt_gpu_feed*> g_dev_feeds;
 }  // namespace
@@ -100,6 +101,31 @@ int vpt_gpu_tile_costs(vpt_gpu_ctx*, float*, uint32_t* rank) {  // the last tile
   return VPT_OK;
 }
 int vpt_gpu_feed_prepare(vpt_gpu_ctx*, uint64_t, int) { return VPT_OK; }
+int vpt_gpu_render_jobs(vpt_gpu_ctx* c, uint64_t begin, uint64_t count, float* film, void*) {  // a small frame's launch
+  if (film) return VPT_E_INVALID;
+  const int64_t T = g_ntx * ((g_h + g_th - 1) / g_th);
+  for (uint64_t jid = begin; jid < begin + count; ++jid) {
+    {
+      std::lock_guard<std::mutex> l(g_mu);
+      if (jid >= g_rendered.size()) return VPT_E_INVALID;
+      ++g_rendered[jid];
+    }
+    const int64_t tile = (int64_t)(jid % (uint64_t)T), x0 = (tile % g_ntx) * g_tw, y0 = (tile / g_ntx) * g_th;
+    for (int64_t y = y0; y < std::min(g_h, y0 + g_th); ++y)
+      for (int64_t x = x0; x < std::min(g_w, x0 + g_tw); ++x) c->own[(y * g_w + x) * 4 + 3] += 1.0f;
+  }
+  g_direct_jobs += count;
+  return VPT_OK;
+}
+int vpt_gpu_sync(vpt_gpu_ctx*) { return VPT_OK; }
+int vpt_gpu_film_flush_to_host(vpt_gpu_ctx* c, float* film, float* host) {
+  if (film) return VPT_E_INVALID;
+  for (size_t i = 0; i < c->own.size(); ++i) {
+    host[i] += c->own[i];
+    c->own[i] = 0.0f;
+  }
+  return VPT_OK;
+}
 int vpt_gpu_bind_thread_near(vpt_gpu_ctx*, int* node) {
   if (node) *node = -1;
   return VPT_OK;
@@ -227,7 +253,7 @@ int main(int argc, char** argv) {
   std::vector<int> rc(drivers + helpers, 0);
   std::vector<std::thread> pool;
   for (int i = 0; i < drivers; ++i)
-    pool.emplace_back([&, i] { rc[i] = vpt_gpu::drain(&ctx[i], sp, film.data(), (uint64_t)a["batch"], opt, nullptr, true); });
+    pool.emplace_back([&, i] { rc[i] = vpt_gpu::drain(&ctx[i], sp, film.data(), (uint64_t)a["batch"], opt, nullptr, helpers > 0); });
   for (int i = 0; i < helpers; ++i) pool.emplace_back([&, i] { rc[drivers + i] = vpt_gpu::help(sp, (uint64_t)a["batch"]); });
   for (int i = 0; i < drivers; ++i) pool[i].join();
   {
@@ -253,7 +279,8 @@ int main(int argc, char** argv) {
       std::printf("dropin_mock: pixel %zu counts %g samples, want %llu\n", p / 4, film[p], (unsigned long long)waves);
       return 1;
     }
-  std::printf("dropin_mock: ok %llu waves, %llu jobs, max %d feeds open\n", (unsigned long long)waves,
-              (unsigned long long)ran, g_max_open.load());
+  std::printf("dropin_mock: ok %llu waves, %llu jobs, max %d feeds open, %llu jobs in direct launches\n",
+              (unsigned long long)waves, (unsigned long long)ran, g_max_open.load(),
+              (unsigned long long)g_direct_jobs.load());
   return 0;
 }

@@ -230,6 +230,7 @@ int main(int argc, char** argv) {
     opt.backlog_jobs = (uint64_t)num("backlog", (long long)opt.backlog_jobs);
     opt.cost_tail = num("cost_tail", opt.cost_tail ? 1 : 0) != 0;
     opt.cost_chunks = num("cost_chunks", opt.cost_chunks ? 1 : 0) != 0;
+    opt.direct_below = (uint64_t)num("direct_below", (long long)opt.direct_below);
     opt.flush_seconds = (double)num("flush_ms", (long long)(opt.flush_seconds * 1000)) / 1000.0;
     if (num("grid_blocks", 0) > 0)
       for (auto* c : ctx)

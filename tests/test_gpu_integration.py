@@ -53,12 +53,14 @@ def test_harness_binary_built():
 
 @pytest.mark.gpu
 @pytest.mark.spawns
+@pytest.mark.parametrize("direct_below", [0, 1])
 @pytest.mark.parametrize("threads,batch", [(2, 37), (2, 1000), (4, 7)])
-def test_run_gpu_threads_share_one_tile_provider(tmp_path, threads, batch):
+def test_run_gpu_threads_share_one_tile_provider(tmp_path, threads, batch, direct_below):
     """Batches smaller and larger than a wave (T = 45 tiles), several threads racing on one provider:
-    the batches cross wave boundaries and interleave, which deadlocked the round-1 sketch."""
+    the batches cross wave boundaries and interleave, which deadlocked the round-1 sketch.  direct_below 0:
+    the frame is small (225 jobs), so drain renders it as jid-range launches; 1: through a feed."""
     w, h, waves = 72, 40, 5
-    film, log = _harness(tmp_path, "wdas_cloud.json", w, h, waves, threads, batch)
+    film, log = _harness(tmp_path, "wdas_cloud.json", w, h, waves, threads, batch, direct_below=direct_below)
     np.testing.assert_array_equal(film[..., 3], waves)
     ref = _oracle_film("c3", w, h, waves)
     np.testing.assert_allclose(film[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
@@ -79,11 +81,12 @@ def test_drain_with_helper_threads(tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.spawns
-def test_run_gpu_fire_scene_batches_over_two_waves(tmp_path):
-    """Temperature grid (fire.json) and batches of two waves."""
+@pytest.mark.parametrize("direct_below", [0, 1])
+def test_run_gpu_fire_scene_batches_over_two_waves(tmp_path, direct_below):
+    """Temperature grid (fire.json) and batches of two waves (jid-range launches / a feed)."""
     w, h, waves = 48, 32, 4
     T = (w // 8) * (h // 8)
-    film, _ = _harness(tmp_path, "fire.json", w, h, waves, 3, 2 * T, temperature=1)
+    film, _ = _harness(tmp_path, "fire.json", w, h, waves, 3, 2 * T, temperature=1, direct_below=direct_below)
     np.testing.assert_array_equal(film[..., 3], waves)
     ref = _oracle_film("c4", w, h, waves)
     np.testing.assert_allclose(film[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
@@ -91,12 +94,13 @@ def test_run_gpu_fire_scene_batches_over_two_waves(tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.spawns
-def test_run_gpu_stop_at_next_wave(tmp_path):
+@pytest.mark.parametrize("direct_below", [0, 1])
+def test_run_gpu_stop_at_next_wave(tmp_path, direct_below):
     """stop_at_next_wave() during wave 2 (tile_provider.cpp:107-110): wave 2 completes, wave 3 never
     starts, so every pixel holds exactly 2 samples and the film is the oracle's 2-wave film."""
     w, h, waves = 64, 40, 6
     T = (w // 8) * (h // 8)
-    film, log = _harness(tmp_path, "wdas_cloud.json", w, h, waves, 2, 11, stop_after=T + 5)
+    film, log = _harness(tmp_path, "wdas_cloud.json", w, h, waves, 2, 11, stop_after=T + 5, direct_below=direct_below)
     np.testing.assert_array_equal(film[..., 3], 2)
     ref = _oracle_film("c3", w, h, 2)
     np.testing.assert_allclose(film[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
