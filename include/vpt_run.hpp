@@ -242,6 +242,7 @@ class FeedPipeline {
     (void)vpt_gpu_bind_thread_near(ctx_, nullptr);  // the ring is in the GPU's node's memory
     std::vector<uint64_t> hold;  // taken, not pushed: hold[head..] in the order taken
     size_t head = 0;
+    auto last_push = std::chrono::steady_clock::now();
     JobRuns batch;
     for (;;) {
       bool last;
@@ -261,7 +262,14 @@ class FeedPipeline {
       batch.clear();
       if (last) break;
       const size_t before = hold.size() - head;
+      const uint64_t pushed_before = pushed_;
       if (int rc = top_up(hold, head)) return fail(rc);
+      if (pushed_ != pushed_before) {
+        last_push = std::chrono::steady_clock::now();
+      } else if (std::chrono::steady_clock::now() - last_push > std::chrono::seconds(1)) {
+        detail::drain_trace("nopush", (double)(hold.size() - head), (double)pushed_);  // (diagnostics)
+        last_push = std::chrono::steady_clock::now();
+      }
       if (hold.size() - head != before) {
         std::lock_guard<std::mutex> l(mu_);
         held_ = hold.size() - head;

@@ -79,6 +79,14 @@ constexpr uint32_t kFeedDeadline = 3000000000u;
 // Every kStartedHint-th reserved item is reported to the host (the feed's backlog, vpt_gpu_feed_backlog):
 // one posted write per 1 024 jobs.
 constexpr uint64_t kStartedHint = 1024;
+// The hints go to kHintSlots words, item k's to slot (k / kStartedHint) % kHintSlots, and the host takes their
+// maximum.  One shared word is not enough: the lanes' posted writes land in any order, so after a burst of
+// reservations (a launch's first lane's worth reserves within microseconds) the word could keep an early
+// hint for good, and a host that saw the backlog as full would never push again -- r05q: the launch's
+// 393 216 items all reserved, the word left at 220 160, the pusher waiting for a backlog of 173 056 to drain
+// while every lane waited for it.  Writes to one slot are kHintSlots x kStartedHint items apart.
+constexpr uint64_t kHintSlots = 16;
+constexpr uint64_t kFeedHeaderWords = 8 + kHintSlots;  // word, error, padding, the hint slots; then the ring
 // LDS copies of the small lookup tables the evaluation reads per lane (logf's 16 x 2 doubles; the
 // temperature kernel's 501 x 3 blackbody table): LDS reads instead of vector-memory loads, which
 // would count in vmcnt with the walk's loads.
@@ -113,7 +121,7 @@ struct KernelEnvT {
   uint64_t* feed_ring;
   uint64_t feed_mask;                // ring slots - 1 (a power of two)
   unsigned* feed_error;
-  uint64_t* feed_started;            // a lane that reserves item k, k % kStartedHint == 0, stores k here
+  uint64_t* feed_started;            // [kHintSlots]: a lane that reserves item k, k % kStartedHint == 0, stores k
   uint32_t* tile_done;               // a staged feed: jobs completed per tile (device memory), else nullptr
   uint32_t compact_every;            // the compacting latency kernel: outer iterations between two meetings
 
@@ -262,7 +270,8 @@ struct KernelEnvT {
       }
       const uint64_t k = atomicAdd(job_counter, 1ULL);
       // the host's backlog estimate (vpt_gpu_feed_backlog): a posted write every kStartedHint items
-      if ((k & (kStartedHint - 1)) == 0) __hip_atomic_store(feed_started, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if ((k & (kStartedHint - 1)) == 0)
+        __hip_atomic_store(feed_started + (k / kStartedHint) % kHintSlots, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       lc.item_lo = (uint32_t)k;
       lc.item_hi = (uint32_t)(k >> 32);
       if (lc.pix != kFeedWait) lc.x0 = (int32_t)now;  // wait start
@@ -1430,10 +1439,11 @@ struct vpt_gpu_feed {
   vpt_gpu_ctx* ctx = nullptr;
   hipStream_t stream = nullptr;
   float* film = nullptr;
-  uint64_t* block = nullptr;  // hipHostMalloc'd: [8] word, error word, started hint, padding; [cap] ring; uint32 counts[T]
+  uint64_t* block = nullptr;  // hipHostMalloc'd: [8] word, error word, padding; [kHintSlots] started hints; [cap] ring;
+                              // uint32 counts[T]
   uint64_t* word = nullptr;
   uint32_t* error = nullptr;    // block[1]: a lane that gave up waiting stores 1 here
-  uint64_t* started = nullptr;  // block[2]: the last reported reserved item (kStartedHint)
+  uint64_t* started = nullptr;  // block[8..8 + kHintSlots): reported reserved items (kStartedHint)
   uint64_t* ring = nullptr;
   uint32_t* counts = nullptr;
   bool stage = false;
@@ -1451,6 +1461,8 @@ struct vpt_gpu_feed {
   uint64_t cap = 0;
   uint64_t published = 0;
   uint64_t started_seen = 0;
+  std::chrono::steady_clock::time_point started_moved{};  // when started_seen last moved (vpt_gpu_feed_backlog)
+  std::chrono::steady_clock::time_point stale_traced{};
   hipEvent_t closed_ev = nullptr;
   bool closed = false;
   bool launched = false;     // the launch starts once launch_at items are published, or at close
@@ -1461,6 +1473,7 @@ struct vpt_gpu_feed {
 
 namespace {
 constexpr double kFeedHostWaitS = 120.0;  // a push waiting this long for a ring slot gives up
+constexpr auto kHintStale = std::chrono::milliseconds(2);  // vpt_gpu_feed_backlog: hints this old are suspect
 constexpr size_t kZeroBytes = 4u << 20;   // the context's pinned zeros (staged feeds' clears)
 
 // VPT_FEED_TRACE=1: one stderr line per feed event (open / launch / close / a push's wait for a ring slot /
@@ -1524,12 +1537,12 @@ int feed_get(vpt_gpu_ctx* ctx, uint64_t cap, bool stage, std::unique_ptr<vpt_gpu
   f->ctx = ctx;
   f->cap = cap;
   const uint64_t T = ctx->scene.T;
-  const size_t bytes = (8 + cap) * sizeof(uint64_t) + T * sizeof(uint32_t);
+  const size_t bytes = (vpt::kFeedHeaderWords + cap) * sizeof(uint64_t) + T * sizeof(uint32_t);
   VPT_HIP(hipHostMalloc((void**)&f->block, bytes, hipHostMallocCoherent | hipHostMallocMapped));
   f->word = f->block;
   f->error = reinterpret_cast<uint32_t*>(f->block + 1);
-  f->started = f->block + 2;
-  f->ring = f->block + 8;  // its own cache lines, away from the words the waiting wavefronts poll
+  f->started = f->block + 8;  // the hints: their own lines, away from the word the waiting wavefronts poll
+  f->ring = f->block + vpt::kFeedHeaderWords;
   f->counts = reinterpret_cast<uint32_t*>(f->ring + cap);
   VPT_HIP(hipEventCreateWithFlags(&f->closed_ev, hipEventDisableTiming));
   if (stage) {
@@ -1572,6 +1585,7 @@ int feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t w
   f->film = film_device ? film_device : ctx->film;
   f->published = 0;
   f->started_seen = 0;
+  f->started_moved = {};
   f->closed = false;
   f->counted = false;
   if (!f->ring_clean)
@@ -1579,11 +1593,12 @@ int feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t w
   f->ring_clean = false;
   std::memset(f->counts, 0, ctx->scene.T * sizeof(uint32_t));
   __atomic_store_n(f->error, 0u, __ATOMIC_RELAXED);
-  __atomic_store_n(f->started, 0ULL, __ATOMIC_RELAXED);
+  for (uint64_t i = 0; i < vpt::kHintSlots; ++i) __atomic_store_n(f->started + i, 0ULL, __ATOMIC_RELAXED);
   __atomic_store_n(f->word, 0ULL, __ATOMIC_RELEASE);
   uint64_t* word_dev = nullptr;
   VPT_HIP(hipHostGetDevicePointer((void**)&word_dev, f->word, 0));
-  f->fl = vpt::FeedLaunch{word_dev, word_dev + 8, cap - 1, reinterpret_cast<unsigned*>(word_dev + 1), word_dev + 2,
+  f->fl = vpt::FeedLaunch{word_dev, word_dev + vpt::kFeedHeaderWords, cap - 1, reinterpret_cast<unsigned*>(word_dev + 1),
+                          word_dev + 8,
                           stage ? f->done_dev : nullptr};
   // The launch is deferred until the ring holds as many items as it has lanes (or the feed is closed):
   // launched at once, its idle wavefronts would poll the host link for work (r04).
@@ -1780,9 +1795,29 @@ int vpt_gpu_feed_push(vpt_gpu_feed* f, const uint64_t* jids, uint64_t n) {
 int vpt_gpu_feed_backlog(vpt_gpu_feed* f, uint64_t* backlog) {
   if (!f || !backlog) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_backlog: null argument");
   // the newest reported reservation (the lanes' posted writes may land out of order: keep the largest)
-  const uint64_t s = __atomic_load_n(f->started, __ATOMIC_RELAXED);
-  if (s > f->started_seen) f->started_seen = s;
+  uint64_t s = 0;  // the largest reported reservation (each slot only grows between two of its writes)
+  for (uint64_t i = 0; i < vpt::kHintSlots; ++i) s = std::max(s, __atomic_load_n(f->started + i, __ATOMIC_RELAXED));
+  const auto now = std::chrono::steady_clock::now();
+  if (s > f->started_seen || f->started_moved == std::chrono::steady_clock::time_point{}) {
+    f->started_seen = std::max(s, f->started_seen);
+    f->started_moved = f->stale_traced = now;
+  }
   *backlog = f->published > f->started_seen ? f->published - f->started_seen : 0;
+  // The hints are an estimate, and one too low reads as a full backlog: a pusher that waited for it to drain
+  // while the lanes waited for items would never push again.  Hints arrive every kStartedHint reservations --
+  // at the GPU's job rate, every few tens of microseconds while lanes take items -- so a launched feed whose
+  // hints have not moved for kHintStale with items outstanding reports an empty backlog: the caller pushes (at
+  // worst more run-ahead than it asked for; the ring's capacity still bounds it).
+  if (f->launched && *backlog > 0 && now - f->started_moved > kHintStale) {
+    *backlog = 0;
+    if (now - f->stale_traced > std::chrono::seconds(1)) {
+      f->stale_traced = now;
+      const hipError_t q = hipStreamQuery(f->stream);
+      feed_trace(f, "stale", (double)f->published, (double)f->started_seen);
+      feed_trace(f, "state", (double)__atomic_load_n(f->error, __ATOMIC_RELAXED),
+                 q == hipSuccess ? 1.0 : (q == hipErrorNotReady ? 0.0 : -(double)q));
+    }
+  }
   return VPT_OK;
 }
 
