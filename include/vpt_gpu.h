@@ -376,10 +376,10 @@ int vpt_gpu_feed_close(vpt_gpu_feed* feed);
 int vpt_gpu_feed_query(vpt_gpu_feed* feed, int* done, uint64_t* pushed);
 int vpt_gpu_feed_destroy(vpt_gpu_feed* feed);
 /* Jobs pushed and not yet taken by a lane -- an estimate: the lanes report every 1 024th job they take into
- * 16 words of the pinned block (their posted writes land in any order; the largest counts), before the launch
- * every pushed job counts.  An estimate too high could leave a caller waiting for a backlog the lanes are not
- * draining, so once the reports have not moved for 2 ms with jobs outstanding it reads 0 (push more).  Cheap:
- * a read of two cache lines. */
+ * 4 words of the pinned block (their posted writes land in any order; the largest counts); before the launch
+ * every pushed job counts.  It can read high, never for long while the lanes wait: a wavefront that finds
+ * every published job taken stores the job count it saw, and a count >= the published one reads as 0.
+ * Cheap: a read of one cache line. */
 int vpt_gpu_feed_backlog(vpt_gpu_feed* feed, uint64_t* backlog);
 /* A staged feed renders into film_device (NULL = the context's own film), which must be zero, on hip_stream
  * (NULL = a stream of the feed's own), and counts the jobs it completes per tile; its film reaches the host through the copy engines, which run beside a launch

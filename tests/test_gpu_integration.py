@@ -246,6 +246,20 @@ def test_progressive_film_rises_during_the_drain(tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.spawns
+def test_drain_with_a_small_backlog_never_stalls(tmp_path):
+    """Full C4 frames with the pusher's backlog at a quarter of the lanes (98 304): the launch's first lane's
+    worth of reservations lands its backlog hints in any order, and before r05 the one hint word could keep an
+    early value for good -- a backlog that read full while every lane waited, one run in ~5 hanging (r05q).
+    Now 6 frames in a row complete and count every sample."""
+    w, h, waves = 1920, 1080, 256
+    film, log = _harness(tmp_path, "fire.json", w, h, waves, 1, 4096, grid_n=512, temperature=1, backlog=98304,
+                         frames=6)
+    assert log.count("render_ms") == 6, log[-2000:]
+    assert (film[..., 3] == waves).all()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["full_grid", "small_grid", "staged_small_grid"])
 def test_feed_renders_pushed_jobs_in_any_order(mode):
     """vpt_gpu_feed_*: job ids pushed out of order and with gaps render the oracle's samples; the close (or,

@@ -84,9 +84,10 @@ constexpr uint64_t kStartedHint = 1024;
 // reservations (a launch's first lane's worth reserves within microseconds) the word could keep an early
 // hint for good, and a host that saw the backlog as full would never push again -- r05q: the launch's
 // 393 216 items all reserved, the word left at 220 160, the pusher waiting for a backlog of 173 056 to drain
-// while every lane waited for it.  Writes to one slot are kHintSlots x kStartedHint items apart.
-constexpr uint64_t kHintSlots = 16;
-constexpr uint64_t kFeedHeaderWords = 8 + kHintSlots;  // word, error, padding, the hint slots; then the ring
+// while every lane waited for it.  Writes to one slot are kHintSlots x kStartedHint items apart.  (16 slots past the word's line measured slower: r05t.)
+constexpr uint64_t kHintSlots = 4;
+constexpr uint64_t kFeedHeaderWords = 8;  // word, error, waiting, padding, the hint slots [4, 8); then the ring
+static_assert(4 + kHintSlots <= kFeedHeaderWords, "the hints fit the header");
 // LDS copies of the small lookup tables the evaluation reads per lane (logf's 16 x 2 doubles; the
 // temperature kernel's 501 x 3 blackbody table): LDS reads instead of vector-memory loads, which
 // would count in vmcnt with the walk's loads.
@@ -122,6 +123,8 @@ struct KernelEnvT {
   uint64_t feed_mask;                // ring slots - 1 (a power of two)
   unsigned* feed_error;
   uint64_t* feed_started;            // [kHintSlots]: a lane that reserves item k, k % kStartedHint == 0, stores k
+  uint64_t* feed_waiting;            // a wavefront whose lanes find every published item taken stores the count
+  uint32_t feed_hint_mask;           // hint slots - 1
   uint32_t* tile_done;               // a staged feed: jobs completed per tile (device memory), else nullptr
   uint32_t compact_every;            // the compacting latency kernel: outer iterations between two meetings
 
@@ -257,11 +260,18 @@ struct KernelEnvT {
     const uint64_t w = __hip_atomic_load(feed_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint64_t published = w & ~kFeedClosed;
     if (lc.pix != kFeedPending) {
-      if (__hip_atomic_load(job_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= published) {
+      const uint64_t c = __hip_atomic_load(job_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (c >= published) {
         if (w & kFeedClosed) return 0;
         if (lc.pix != kFeedWait) {
           lc.pix = kFeedWait;
           lc.x0 = (int32_t)now;  // wait start
+          // The lanes have taken every item published: say so (one lane per wavefront, as it starts waiting).
+          // The host's backlog estimate comes from hints that may land out of order; a count >= its published
+          // count here means the lanes wait for it, whatever the hints say (vpt_gpu_feed_backlog).
+          const uint64_t m = __builtin_amdgcn_ballot_w64(true);
+          if (feed_waiting && __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == (uint32_t)__builtin_ctzll(m))
+            __hip_atomic_store(feed_waiting, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         } else if (now - (uint32_t)lc.x0 > kFeedDeadline) {
           __hip_atomic_store(feed_error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // (host memory: a store)
           return 0;
@@ -271,7 +281,7 @@ struct KernelEnvT {
       const uint64_t k = atomicAdd(job_counter, 1ULL);
       // the host's backlog estimate (vpt_gpu_feed_backlog): a posted write every kStartedHint items
       if ((k & (kStartedHint - 1)) == 0)
-        __hip_atomic_store(feed_started + (k / kStartedHint) % kHintSlots, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(feed_started + ((k / kStartedHint) & feed_hint_mask), k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       lc.item_lo = (uint32_t)k;
       lc.item_hi = (uint32_t)(k >> 32);
       if (lc.pix != kFeedWait) lc.x0 = (int32_t)now;  // wait start
@@ -691,6 +701,7 @@ struct FeedLaunch {
   uint64_t mask;
   unsigned* error;
   uint64_t* started;
+  uint64_t* waiting;
   uint32_t* tile_done;  // nullptr unless a staged feed
 };
 }  // namespace vpt
@@ -1008,6 +1019,13 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.feed_mask = feed ? feed->mask : 0;
   env.feed_error = feed ? feed->error : nullptr;
   env.feed_started = feed ? feed->started : nullptr;
+  env.feed_waiting = feed ? feed->waiting : nullptr;
+  {  // (A/B knobs, r05: VPT_FEED_WAITING=0 drops the waiting word, VPT_HINT_SLOTS=1 uses one hint word)
+    static const bool no_wait = std::getenv("VPT_FEED_WAITING") && std::atoi(std::getenv("VPT_FEED_WAITING")) == 0;
+    static const bool one_slot = std::getenv("VPT_HINT_SLOTS") && std::atoi(std::getenv("VPT_HINT_SLOTS")) == 1;
+    if (no_wait) env.feed_waiting = nullptr;
+    env.feed_hint_mask = one_slot ? 0u : (uint32_t)(vpt::kHintSlots - 1);
+  }
   env.tile_done = feed ? feed->tile_done : nullptr;
   env.compact_every = 0;
   env.event_count = ctx->job_counter + 2 * slot + 1;
@@ -1439,11 +1457,12 @@ struct vpt_gpu_feed {
   vpt_gpu_ctx* ctx = nullptr;
   hipStream_t stream = nullptr;
   float* film = nullptr;
-  uint64_t* block = nullptr;  // hipHostMalloc'd: [8] word, error word, padding; [kHintSlots] started hints; [cap] ring;
-                              // uint32 counts[T]
+  uint64_t* block = nullptr;  // hipHostMalloc'd: [8] word, error word, waiting word, padding, [4..8) the started
+                              // hints; [cap] ring; uint32 counts[T]
   uint64_t* word = nullptr;
   uint32_t* error = nullptr;    // block[1]: a lane that gave up waiting stores 1 here
-  uint64_t* started = nullptr;  // block[8..8 + kHintSlots): reported reserved items (kStartedHint)
+  uint64_t* started = nullptr;  // block[4..4 + kHintSlots): reported reserved items (kStartedHint)
+  uint64_t* waiting = nullptr;  // block[2]: the job count a wavefront saw when it ran out of published items
   uint64_t* ring = nullptr;
   uint32_t* counts = nullptr;
   bool stage = false;
@@ -1473,7 +1492,6 @@ struct vpt_gpu_feed {
 
 namespace {
 constexpr double kFeedHostWaitS = 120.0;  // a push waiting this long for a ring slot gives up
-constexpr auto kHintStale = std::chrono::milliseconds(2);  // vpt_gpu_feed_backlog: hints this old are suspect
 constexpr size_t kZeroBytes = 4u << 20;   // the context's pinned zeros (staged feeds' clears)
 
 // VPT_FEED_TRACE=1: one stderr line per feed event (open / launch / close / a push's wait for a ring slot /
@@ -1541,7 +1559,8 @@ int feed_get(vpt_gpu_ctx* ctx, uint64_t cap, bool stage, std::unique_ptr<vpt_gpu
   VPT_HIP(hipHostMalloc((void**)&f->block, bytes, hipHostMallocCoherent | hipHostMallocMapped));
   f->word = f->block;
   f->error = reinterpret_cast<uint32_t*>(f->block + 1);
-  f->started = f->block + 8;  // the hints: their own lines, away from the word the waiting wavefronts poll
+  f->started = f->block + 4;
+  f->waiting = f->block + 2;
   f->ring = f->block + vpt::kFeedHeaderWords;
   f->counts = reinterpret_cast<uint32_t*>(f->ring + cap);
   VPT_HIP(hipEventCreateWithFlags(&f->closed_ev, hipEventDisableTiming));
@@ -1594,11 +1613,12 @@ int feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t w
   std::memset(f->counts, 0, ctx->scene.T * sizeof(uint32_t));
   __atomic_store_n(f->error, 0u, __ATOMIC_RELAXED);
   for (uint64_t i = 0; i < vpt::kHintSlots; ++i) __atomic_store_n(f->started + i, 0ULL, __ATOMIC_RELAXED);
+  __atomic_store_n(f->waiting, 0ULL, __ATOMIC_RELAXED);
   __atomic_store_n(f->word, 0ULL, __ATOMIC_RELEASE);
   uint64_t* word_dev = nullptr;
   VPT_HIP(hipHostGetDevicePointer((void**)&word_dev, f->word, 0));
   f->fl = vpt::FeedLaunch{word_dev, word_dev + vpt::kFeedHeaderWords, cap - 1, reinterpret_cast<unsigned*>(word_dev + 1),
-                          word_dev + 8,
+                          word_dev + 4, word_dev + 2,
                           stage ? f->done_dev : nullptr};
   // The launch is deferred until the ring holds as many items as it has lanes (or the feed is closed):
   // launched at once, its idle wavefronts would poll the host link for work (r04).
@@ -1803,20 +1823,20 @@ int vpt_gpu_feed_backlog(vpt_gpu_feed* f, uint64_t* backlog) {
     f->started_moved = f->stale_traced = now;
   }
   *backlog = f->published > f->started_seen ? f->published - f->started_seen : 0;
-  // The hints are an estimate, and one too low reads as a full backlog: a pusher that waited for it to drain
-  // while the lanes waited for items would never push again.  Hints arrive every kStartedHint reservations --
-  // at the GPU's job rate, every few tens of microseconds while lanes take items -- so a launched feed whose
-  // hints have not moved for kHintStale with items outstanding reports an empty backlog: the caller pushes (at
-  // worst more run-ahead than it asked for; the ring's capacity still bounds it).
-  if (f->launched && *backlog > 0 && now - f->started_moved > kHintStale) {
-    *backlog = 0;
-    if (now - f->stale_traced > std::chrono::seconds(1)) {
-      f->stale_traced = now;
-      const hipError_t q = hipStreamQuery(f->stream);
-      feed_trace(f, "stale", (double)f->published, (double)f->started_seen);
-      feed_trace(f, "state", (double)__atomic_load_n(f->error, __ATOMIC_RELAXED),
-                 q == hipSuccess ? 1.0 : (q == hipErrorNotReady ? 0.0 : -(double)q));
-    }
+  // The hints may land out of order, so the estimate can read high after a burst of reservations (a launch's
+  // first lane's worth reserves within microseconds) -- and with no reservation after it to correct it, a
+  // pusher waiting for that backlog to drain would wait for ever while the lanes wait for it (r05q).  A
+  // wavefront that runs out of published items stores the job count it saw: one >= the published count means
+  // the lanes are waiting now.
+  const uint64_t waiting = __atomic_load_n(f->waiting, __ATOMIC_RELAXED);
+  if (f->launched && waiting >= f->published) *backlog = 0;
+  if (f->launched && *backlog > 0 && now - f->started_moved > std::chrono::seconds(1) &&
+      now - f->stale_traced > std::chrono::seconds(1)) {  // (diagnostics) nothing reserved for a second
+    f->stale_traced = now;
+    const hipError_t q = hipStreamQuery(f->stream);
+    feed_trace(f, "noreserve", (double)f->published, (double)f->started_seen);
+    feed_trace(f, "state", (double)__atomic_load_n(f->error, __ATOMIC_RELAXED),
+               q == hipSuccess ? 1.0 : (q == hipErrorNotReady ? 0.0 : -(double)q));
   }
   return VPT_OK;
 }
