@@ -46,13 +46,16 @@
 
 namespace {
 
-// A provider that forwards to the restated TileProvider and, once, stops at the next wave.
+// A provider that forwards to the restated TileProvider and, once, stops at the next wave.  It counts the
+// tokens only when something reads the count (stop_after, sample_ms): a counter's atomic add per token would
+// time this frame ~20 ms slower than the frames=/warmup= frames, which take the provider as it is (C4, r05).
 struct StoppingProvider {
   vpt_headless::TileProvider& tp;
   uint64_t stop_after;
+  bool count;
   std::atomic<uint64_t> handed{0};
   vpt_headless::TileProvider::token next() {
-    if (handed.fetch_add(1) + 1 == stop_after) tp.stop_at_next_wave();
+    if (count && handed.fetch_add(1) + 1 == stop_after) tp.stop_at_next_wave();
     return tp.next();
   }
 };
@@ -127,7 +130,7 @@ int main(int argc, char** argv) {
   // main.cpp:46-55: provider and film; then num_workers threads (main.cpp:62-68)
   vpt_headless::TileProvider tp(cfg.output_size[0], cfg.output_size[1], cfg.num_waves, cfg.tile_size[0],
                                 cfg.tile_size[1]);
-  StoppingProvider sp{tp, (uint64_t)num("stop_after", 0)};
+  StoppingProvider sp{tp, (uint64_t)num("stop_after", 0), num("stop_after", 0) > 0 || num("sample_ms", 0) > 0};
   vpt_headless::Image<float, 4> film(cfg.output_size[0], cfg.output_size[1]);
   std::vector<int> rc(threads, 0);
 
@@ -308,6 +311,7 @@ int main(int argc, char** argv) {
   if (!f || std::fwrite(film.px.data(), sizeof(float), n, f) != n) return fail("write film");
   std::fclose(f);
   std::printf("run_gpu_harness: %s, %d threads, %u waves started, %llu jobs handed out\n", mode.c_str(), threads,
-              tp.max_wave_started(), (unsigned long long)sp.handed.load());
+              tp.max_wave_started(),
+              (unsigned long long)(sp.count ? sp.handed.load() : (uint64_t)tp.num_tiles() * tp.max_wave_started()));
   return 0;
 }
