@@ -224,7 +224,10 @@ class FeedPipeline {
     while (head < hold.size() && b < mark) {
       const uint64_t n = std::min<uint64_t>(kChunk, hold.size() - head);
       const uint64_t* ids = hold.data() + head;
-      if (int rc = push(cost_chunks_ && !cls_.empty() ? by_cost(ids, n) : ids, n)) return rc;
+      // (the launch's first lane's worth goes unsorted: every lane takes one of those jobs at once, so their order
+      // changes nothing, and sorting them would delay the launch -- ~3 ms of C3's 458 752)
+      const bool sort = cost_chunks_ && !cls_.empty() && pushed_ >= lanes_;
+      if (int rc = push(sort ? by_cost(ids, n) : ids, n)) return rc;
       head += n;
       b += n;
       pushed_ += n;
