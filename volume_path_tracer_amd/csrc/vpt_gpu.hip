@@ -1020,12 +1020,7 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.feed_error = feed ? feed->error : nullptr;
   env.feed_started = feed ? feed->started : nullptr;
   env.feed_waiting = feed ? feed->waiting : nullptr;
-  {  // (A/B knobs, r05: VPT_FEED_WAITING=0 drops the waiting word, VPT_HINT_SLOTS=1 uses one hint word)
-    static const bool no_wait = std::getenv("VPT_FEED_WAITING") && std::atoi(std::getenv("VPT_FEED_WAITING")) == 0;
-    static const bool one_slot = std::getenv("VPT_HINT_SLOTS") && std::atoi(std::getenv("VPT_HINT_SLOTS")) == 1;
-    if (no_wait) env.feed_waiting = nullptr;
-    env.feed_hint_mask = one_slot ? 0u : (uint32_t)(vpt::kHintSlots - 1);
-  }
+  env.feed_hint_mask = (uint32_t)(vpt::kHintSlots - 1);
   env.tile_done = feed ? feed->tile_done : nullptr;
   env.compact_every = 0;
   env.event_count = ctx->job_counter + 2 * slot + 1;
@@ -1624,9 +1619,8 @@ int feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t w
   // launched at once, its idle wavefronts would poll the host link for work (r04).
   f->launched = false;
   f->launch_at = (uint64_t)ctx->grid_blocks * vpt::kBlockThreads;
-  // (A/B knob, r05: VPT_FEED_LAUNCH_DIV=d launches at 1/d of the lanes -- earlier, with idle lanes polling)
-  static const long launch_div = std::getenv("VPT_FEED_LAUNCH_DIV") ? std::atol(std::getenv("VPT_FEED_LAUNCH_DIV")) : 1;
-  if (launch_div > 1) f->launch_at = std::max<uint64_t>(1, f->launch_at / (uint64_t)launch_div);
+  // (Launching at a quarter or a sixteenth of the lanes saved nothing and stalled: lanes racing past the
+  // published count hold items their waves serve late, and the wrapping ring waits for them; r05k.)
   feed_trace(f.get(), stage ? "open_stg" : "open", (double)cap, (double)(uintptr_t)hip_stream);
   *out = f.release();
   return VPT_OK;
