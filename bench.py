@@ -138,17 +138,25 @@ def dropin_frames(wl, frames: int = 3, timeout_s: int = 300):
     outside the timed drains, as the harness and run_checked do it) after one untimed frame.  The median of the
     frames is the record's ms_per_frame.  Then the provider alone (mode=tokens: one
     thread taking every token of the frame), the drop-in's host-side floor.  A child process, started before
-    this process touches the GPU.  None for configs the harness does not run (C2's constant cube, C5)."""
+    this process touches the GPU.  None for C5 (one GPU's frame of BASELINE's 8-GPU configuration)."""
     import subprocess
     import tempfile
 
-    if wl.density_kind != 1 or wl.name not in ("c1", "c3", "c4") or not HARNESS.exists():
+    if wl.name not in ("c1", "c2", "c3", "c4") or not HARNESS.exists():
         return None
     scene = ROOT / "volume_path_tracer_amd" / "scenes" / ("fire.json" if wl.temperature else "wdas_cloud.json")
     W, H, spp = wl.cfg.width, wl.cfg.height, wl.spp
-    base = [str(HARNESS), f"config={scene}", f"w={W}", f"h={H}", f"waves={spp}", f"grid_n={wl.grid_n}", "threads=1",
-            "batch=4096", f"temperature={1 if wl.temperature else 0}"]
     with tempfile.TemporaryDirectory() as tmp:
+        if wl.name == "c2":  # the constant cube: wdas_cloud.json with C2's medium (scenes.workload), camera at 300
+            doc = json.loads(scene.read_text())
+            v = wl.cfg.volume_parameters
+            vp = doc["volume_parameters"]
+            vp.update(sigma_s=v.sigma_s, sigma_a=v.sigma_a, henyey_greenstein_g=v.henyey_greenstein_g, le_scale=v.le_scale)
+            scene = Path(tmp) / "c2.json"
+            scene.write_text(json.dumps(doc))
+        base = [str(HARNESS), f"config={scene}", f"w={W}", f"h={H}", f"waves={spp}", f"grid_n={wl.grid_n}",
+                f"kind={wl.density_kind}", f"dist={-wl.cfg.camera_parameters.position[2]:g}", "threads=1", "batch=4096",
+                f"temperature={1 if wl.temperature else 0}"]
         try:
             r = subprocess.run(base + [f"out={tmp}/film.f32", f"frames={frames}", "warmup=1"], capture_output=True,
                                text=True, timeout=timeout_s)

@@ -4,7 +4,7 @@
 // with the oracle.
 //
 //   run_gpu_harness config=<scene.json> out=<film.f32> [mode=drain|run w= h= waves= threads= batch=
-//                   grid_n= dist= temperature=0|1 stop_after=<jobs> nvdb=<file.nvdb> gridbuf=<file> taker_node=<n>
+//                   grid_n= kind= dist= temperature=0|1 stop_after=<jobs> nvdb=<file.nvdb> gridbuf=<file> taker_node=<n>
 //                   tempbuf=<file> hold= backlog= flush_ms= cost_tail= cost_chunks= helpers= grid_blocks= sample_ms= frames= warmup=]
 //
 // mode=drain (default): each thread owns a context made with vpt_gpu_create and calls
@@ -219,7 +219,7 @@ int main(int argc, char** argv) {
       if (vpt_grid_read_nvdb(a["nvdb"].c_str(), "density", &dens) || !dens) return fail("vpt_grid_read_nvdb density");
       if (vpt_grid_read_nvdb(a["nvdb"].c_str(), "temperature", &temp)) return fail("vpt_grid_read_nvdb temperature");
     } else {
-      dens = vpt_synth_grid(1, grid_n);
+      dens = vpt_synth_grid((int)num("kind", 1), grid_n);  // kind 0: C2's constant cube
       temp = num("temperature", 0) ? vpt_synth_grid(2, grid_n) : nullptr;
       if (!dens || (num("temperature", 0) && !temp)) return fail("vpt_synth_grid");
     }
