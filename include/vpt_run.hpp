@@ -390,6 +390,9 @@ struct Helpers {
 //     under a mutex shared by all callers; the final film is the launch's.
 // `first`: job runs already taken by the caller (queued first).  `share`: other threads of run() may queue
 // into this pipeline while it drains (detail::Helpers); drain returns once they have detached.
+// drain(): tokens taken before a provider with progress() is asked how large its frame is.
+constexpr uint64_t kDirectProbe = 65536;
+
 namespace detail {
 inline void append_runs(JobRuns& to, const JobRuns& from) {
   for (const auto& r : from)
@@ -414,7 +417,7 @@ inline int render_runs(vpt_gpu_ctx* ctx, const JobRuns& runs, float* film_host) 
 template <class Provider>
 int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs, const DrainOptions& opt = {},
           const JobRuns* first = nullptr, bool share = false) {
-  JobRuns head;  // the first lane's worth of jobs, taken before the pipeline starts
+  JobRuns head;  // the jobs taken before the pipeline starts
   if (!share) {  // (a shared pipeline takes helpers' jobs: it always runs)
     int blocks = 0, threads = 0;
     if (int rc = vpt_gpu_launch_info(ctx, &blocks, &threads)) return rc;
@@ -424,12 +427,23 @@ int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs,
       head = *first;
       for (const auto& r : head) have += r.second;
     }
+    // A provider with the reference's progress() (percent of its jobs handed out, tile_provider.hpp:72-74)
+    // tells a large frame after a few batches: the pipeline then starts at once, its pusher filling the ring
+    // while the rest of the launch's first lane's worth is taken.  (Starting the launch itself earlier than a
+    // lane's worth was measured 5-15x slower: tools/experiments/r05_wave_cas_early_launch.patch.)
+    const uint64_t probe = std::min<uint64_t>(direct, kDirectProbe);
     JobRuns runs;
     while (have < direct) {
       const uint64_t n = take_jobs(tp, std::min<uint64_t>(std::max<uint64_t>(1, batch_jobs), direct - have), runs, [](auto&) {});
       if (n == 0) return detail::render_runs(ctx, head, film_host);  // the provider is dry: a small frame
       detail::append_runs(head, runs);
       have += n;
+      if constexpr (requires { tp.progress(); }) {
+        if (have >= probe && have < direct) {
+          const uint64_t pct = (uint64_t)tp.progress();  // floor: the frame has >= have * 100 / (pct + 1) jobs
+          if (pct == 0 || have * 100 / (pct + 1) >= direct) break;
+        }
+      }
     }
     first = &head;
   }

@@ -58,6 +58,7 @@ struct StoppingProvider {
     if (count && handed.fetch_add(1) + 1 == stop_after) tp.stop_at_next_wave();
     return tp.next();
   }
+  unsigned progress() const { return tp.progress(); }
 };
 
 int fail(const char* what) {
