@@ -274,6 +274,21 @@ def pipe_roofline(config: str, samples_per_s_per_cu: float, stencil_entries_per_
             "pipe_pool_mib": round(pool_mib, 1), "pipe_sources": [cnt_src, ceil_src, pool_src]}
 
 
+def mix_roofline(config: str, spp: int, avg_launch_s: float, frame_samples: float, samples_per_launch: float) -> dict:
+    """The launch's memory work alone, measured: the newest committed profiles/*_<config>_mix_ceiling.json
+    (tools/ubench/gather mix: the config's per-sample request mix -- walk-class 4-B gathers from an L2-resident
+    table, 32-B pool gathers, both dependent chains -- chased at the kernel's occupancy with half the lanes
+    active, no arithmetic) gives the frame's memory-only time; mix_frac = that time / this launch's time, scaled
+    to this launch's samples.  Unlike pipe_frac (two classes priced apart and added) one chase prices the mix
+    jointly (r05: C3 0.51, C4 0.28 -- the kernels are not at their memory ceiling)."""
+    mj, src = newest_profile("*_mix_ceiling.json", lambda j: j.get("config") == config and j.get("spp") == spp)
+    if not mj or not frame_samples:
+        return {"mix_frac": None}
+    mix_ms = mj["frame_ms"] * samples_per_launch / frame_samples
+    return {"mix_frac": round(mix_ms / (avg_launch_s * 1e3), 4), "mix_ms_per_launch": round(mix_ms, 2),
+            "mix_source": src}
+
+
 def init_rank(args, env=None):
     """(rank, world, device, scalar device) of this process.  One process per GPU: device LOCAL_RANK
     (device 0 for --one-device, the one-GPU multi-process tests).  For world > 1 the process group is
@@ -532,6 +547,8 @@ def main():
         pool_mib = (dens.leaf_count + (temp.leaf_count if temp is not None else 0)) * POOL_BYTES_PER_LEAF / 2**20
         req.update(pipe_roofline(args.config, samples_rank / args.steps / launches_per_step / avg_launch_s / cus,
                                  (counters["stencils"] + counters["temp_stencils"]) / samples_rank, pool_mib))
+        req.update(mix_roofline(args.config, spp, avg_launch_s, wl.cfg.width * wl.cfg.height * spp,
+                                samples_rank / (args.steps * launches_per_step)))
         out = {
             "metric": baseline_metric(),
             "value": round(value, 3),

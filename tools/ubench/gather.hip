@@ -4,7 +4,7 @@
 // so a wavefront keeps Chains divergent loads in flight; occupancy is set with dynamic LDS.  Reports
 // loads/s per CU for table sizes from L2-resident (1.2 MiB, the C3 walk table) to HBM-resident, and
 // the memory-level parallelism (chains x waves/SIMD) the request rate saturates at.
-//   hipcc -O3 --offload-arch=gfx950 -o gather gather.hip && ./gather [calib | width | pool MiB...]
+//   hipcc -O3 --offload-arch=gfx950 -o gather gather.hip && ./gather [calib | width | pool MiB... | mix ...]
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -132,6 +132,48 @@ void width_rows(size_t bytes, int cus, uint32_t* out, size_t lds_total) {
   CHECK(hipFree(t));
 }
 
+// The C3 kernel's request mix in one chase (the `mix` mode, r05 -- a joint check of the two-class pipe model
+// bench.py reports as pipe_frac): every lane runs one chain of divergent 4-B gathers through an L2-resident
+// table (the walk words and cell entries: 81.6 per sample on C3) and, every `Period`-th step, one step of a
+// second chain of 32-B gathers through a pool-sized table (the stencil pieces: 11.9 per sample), both
+// dependent chains as in the kernel (a lane has at most one walk word and one stencil in flight); `active`
+// lanes of each wavefront (the kernel's walk runs at ~32 of 64).
+template <int Period>
+__global__ __launch_bounds__(256) void chase_mix(const uint32_t* __restrict__ walk, uint32_t nw,
+                                                 const uint32_t* __restrict__ pool, uint32_t np, int iters,
+                                                 uint32_t* out, int active) {
+  extern __shared__ uint32_t occupancy_lds[];
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if ((int)(threadIdx.x & 63) >= active) return;
+  uint32_t w = (g * 2654435761u) % nw, p = (g * 40503u + 17u) % np;
+  for (int i = 0; i < iters; ++i) {
+    w = walk[w];
+    if (i % Period == 0) p = Entry<8>::next(pool, p);
+  }
+  if ((w ^ p) == 0xFFFFFFFFu) out[0] = w + occupancy_lds[0];
+}
+
+template <int Period>
+double run_mix(const uint32_t* walk, uint32_t nw, const uint32_t* pool, uint32_t np, int waves, int cus,
+               uint32_t* out, size_t lds_total, int active) {
+  const int blocks = cus * waves;
+  const size_t lds = lds_total / waves - 1024;
+  const int iters = 4096;
+  CHECK(hipFuncSetAttribute((const void*)chase_mix<Period>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  hipLaunchKernelGGL(chase_mix<Period>, dim3(blocks), dim3(256), lds, 0, walk, nw, pool, np, iters, out, active);
+  CHECK(hipEventRecord(e0));
+  hipLaunchKernelGGL(chase_mix<Period>, dim3(blocks), dim3(256), lds, 0, walk, nw, pool, np, iters, out, active);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  CHECK(hipGetLastError());
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  return (double)blocks * 4 * active * iters / (ms * 1e-3);  // lane walk steps per second (whole device)
+}
+
 template <int Chains>
 double run(const uint32_t* t, uint32_t n, int waves, int cus, uint32_t* out, size_t lds_total, int active = 64) {
   const int blocks = cus * waves;  // 256 threads = 4 waves per block, one per SIMD
@@ -173,6 +215,38 @@ int main(int argc, char** argv) {
   if (argc > 2 && std::string(argv[1]) == "pool") {  // 32-B entries (a stencil's piece) from tables of the given MiB
     std::printf("%5s %5s %10s %6s %6s %10s\n", "", "bytes", "table_MiB", "chains", "waves", "Gentry/s/CU");
     for (int a = 2; a < argc; ++a) width_rows<8>((size_t)(std::atof(argv[a]) * 1048576.0) & ~size_t(31), cus, out, lds_total);
+    return 0;
+  }
+  if (argc > 1 && std::string(argv[1]) == "mix") {  // mix [pool MiB] [walk KiB] [steps per sample] [samples] [period 4|7]
+    const double pool_mib = argc > 2 ? std::atof(argv[2]) : 797.0, walk_kib = argc > 3 ? std::atof(argv[3]) : 1200.0;
+    const double steps_per_sample = argc > 4 ? std::atof(argv[4]) : 81.6, samples = argc > 5 ? std::atof(argv[5]) : 530841600.0;
+    const int period = argc > 6 ? std::atoi(argv[6]) : 7;
+    auto table = [](size_t n, size_t stride) {
+      std::vector<uint32_t> h(n * stride, 0u);
+      uint64_t s = 88172645463325252ull;
+      for (size_t i = 0; i < n; ++i) {
+        s ^= s << 13;
+        s ^= s >> 7;
+        s ^= s << 17;
+        h[i * stride] = (uint32_t)(s % n);
+      }
+      uint32_t* d;
+      CHECK(hipMalloc(&d, h.size() * 4));
+      CHECK(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+      return d;
+    };
+    const uint32_t nw = (uint32_t)(walk_kib * 1024 / 4), np = (uint32_t)(pool_mib * 1048576.0 / 32);
+    uint32_t* walk = table(nw, 1);
+    uint32_t* pool = table(np, 8);
+    std::printf("mix: %d CUs, walk table %.0f KiB, pool %.0f MiB, a 32-B step every %d walk steps; a sample = %.1f walk "
+                "steps, frame = %.0f samples\n", cus, walk_kib, pool_mib, period, steps_per_sample, samples);
+    std::printf("%6s %6s %14s %14s\n", "waves", "active", "Gsteps/s", "frame_ms");
+    for (int waves : {7, 5})
+      for (int act : {64, 32}) {
+        const double r = period == 4 ? run_mix<4>(walk, nw, pool, np, waves, cus, out, lds_total, act)
+                                     : run_mix<7>(walk, nw, pool, np, waves, cus, out, lds_total, act);
+        std::printf("%6d %6d %14.3f %14.1f\n", waves, act, r * 1e-9, samples * steps_per_sample / r * 1e3);
+      }
     return 0;
   }
   const size_t sizes[] = {307200, 1u << 22, 1u << 26};  // 1.2 MiB (L2), 16 MiB (MALL), 256 MiB (HBM)
