@@ -282,8 +282,8 @@ def mix_roofline(config: str, spp: int, avg_launch_s: float, frame_samples: floa
     to this launch's samples.  Unlike pipe_frac (two classes priced apart and added) one chase prices the mix
     jointly (r05: C3 0.51, C4 0.28 -- the kernels are not at their memory ceiling)."""
     mj, src = newest_profile("*_mix_ceiling.json", lambda j: j.get("config") == config and j.get("spp") == spp)
-    if not mj or not frame_samples:
-        return {"mix_frac": None}
+    if not mj or not frame_samples:  # (measured for the full launches, C3 / C4; C1 / C2 are latency-bound)
+        return {}
     mix_ms = mj["frame_ms"] * samples_per_launch / frame_samples
     return {"mix_frac": round(mix_ms / (avg_launch_s * 1e3), 4), "mix_ms_per_launch": round(mix_ms, 2),
             "mix_source": src}
