@@ -108,8 +108,9 @@ def cpu_baseline(wl, dens, temp, budget_s: float = 15.0, runs: int = 3):
     _, ms1, _ = O.render_pool(cfg, od, ot, 1, threads)  # calibration: wave 1
     k = int(max(1, min(wl.spp, budget_s / runs / max(ms1 / 1e3, 1e-3))))
     rates, secs = [], []
+    film = None
     for _ in range(runs):
-        _, ms, _ = O.render_pool(cfg, od, ot, k, threads)
+        film, ms, _ = O.render_pool(cfg, od, ot, k, threads)
         rates.append(k * per_wave / (ms / 1e3) / 1e6)
         secs.append(ms / 1e3)
     rates.sort()
@@ -124,7 +125,33 @@ def cpu_baseline(wl, dens, temp, budget_s: float = 15.0, runs: int = 3):
             # not measured: the per-thread rate times every hardware thread of the node (the job is granted
             # `cores` of them), an upper bound that ignores SMT and memory contention
             "node_extrapolated": {"threads": node, "value": round(med / threads * node, 3), "unit": "Msamples/s",
-                                  "kind": "linear extrapolation of per_thread, not a measurement"}}
+                                  "kind": "linear extrapolation of per_thread, not a measurement"}}, film, k
+
+
+def film_parity(wl, dens, temp, ref_film, waves: int, device: int) -> dict:
+    """north_star's parity criterion on the bench's own frame: the production kernel renders the waves the CPU
+    baseline just rendered with the oracle's worker pool (waves 1..k, the same jobs and PCG streams), and the
+    per-pixel radiance (film XYZ / sample count) is compared -- RMSE over every pixel and channel against the
+    stated bound of 1e-4, the largest difference, and the sample counts (which must be equal).  Only the fp32
+    order of the film's atomic adds differs from the oracle's per-pixel wave order."""
+    import numpy as np
+    import torch
+
+    from volume_path_tracer_amd.render import Integrator
+
+    it = Integrator(wl.cfg, dens, temp, device=device)
+    it.render_waves(1, waves)
+    torch.cuda.synchronize()
+    gpu = it.film_host()
+    del it
+    counts_equal = bool(np.array_equal(gpu[..., 3], ref_film[..., 3]))
+    n = np.maximum(ref_film[..., 3:4].astype(np.float64), 1.0)
+    lg, lr = gpu[..., :3].astype(np.float64) / n, ref_film[..., :3].astype(np.float64) / n
+    rmse = float(np.sqrt(np.mean((lg - lr) ** 2)))
+    return {"waves": waves, "pixels": int(lg.shape[0] * lg.shape[1]), "counts_equal": counts_equal,
+            "rmse_per_pixel": rmse, "max_abs_diff": float(np.abs(lg - lr).max()),
+            "mean_radiance": float(np.abs(lr).mean()), "bound": 1e-4, "ok": counts_equal and rmse < 1e-4,
+            "vs": "oracle worker pool (tests/oracle_lib.py render_pool), same waves and seeds"}
 
 
 HARNESS = ROOT / "tests" / "native" / "build" / "run_gpu_harness"
@@ -589,8 +616,9 @@ def main():
                 dropin["vs_one_launch"] = round(out["ms_per_step"] / dropin["ms_per_frame"], 4)
             out["dropin"] = dropin
         if world == 1 and not args.no_cpu_baseline:
-            cb = cpu_baseline(wl, dens, temp, args.cpu_budget)
+            cb, ref_film, k = cpu_baseline(wl, dens, temp, args.cpu_budget)
             out["cpu_baseline"] = cb
+            out["parity"] = film_parity(wl, dens, temp, ref_film, k, dev.index)
             out["speedup_vs_cpu_baseline"] = round(value / cb["value"], 1) if cb["value"] else None
             ne = cb["node_extrapolated"]["value"]
             out["speedup_vs_cpu_node_extrapolated"] = round(value / ne, 1) if ne else None
