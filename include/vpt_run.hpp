@@ -114,7 +114,7 @@ inline std::mutex& film_mutex() {  // the host film is shared by every caller
 // launch drain between batches), a pusher thread that feeds it from the jobs the takers queue, and a film
 // thread that adds the launch's progress into the caller's film every flush_seconds.  The takers (the driving
 // thread and help() threads) only take tokens and queue their job ids: the provider's next() is the drop-in's
-// host-side bound (C4: ~40 M tokens/s on one thread vs ~84 M jobs/s the GPU renders), so nothing else runs on
+// host-side bound (C4: 66 M tokens/s on one thread of the GPU box vs ~83 M jobs/s the GPU renders), so nothing else runs on
 // that thread.
 class FeedPipeline {
  public:
@@ -349,9 +349,9 @@ class FeedPipeline {
 namespace detail {
 // Threads on one provider: each GPU is driven by the one thread that claimed it; other threads may take
 // tokens too and queue their job ids into a driving thread's pipeline (help()).  run() does not use it: with
-// the restated TileProvider, contended next() calls are slower than one thread's (r05: 1 thread 36 M tokens/s,
-// 2 threads 23 M/s, 4 threads 20 M/s on an 8-core Xeon: the provider's one job counter); a provider whose
-// next() scales across threads could.
+// the restated TileProvider, contended next() calls are slower than one thread's (r05: 1 thread 64-67 M tokens/s,
+// 2 threads 3.8-5.3 M/s on the GPU box's EPYC; 42 / 29 / 28 M/s for 1 / 2 / 4 threads on an 8-core Xeon: the
+// provider's one job counter); a provider whose next() scales across threads could.
 struct Helpers {
   std::mutex mu;
   std::condition_variable cv;
