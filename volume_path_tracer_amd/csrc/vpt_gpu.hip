@@ -230,6 +230,11 @@ struct KernelEnvT {
   // one lane with a few jobs in a row wins: C1 frames on the full grid (r02g,
   // profiles/r02g_c1_lanes_sweep.txt), 1 / 2 / 3 lanes: 8 spp (x = 1.1) 23.3 / 29.3 / - ms, 16 spp
   // (x = 2.3) 31.7 / 32.5 / 35.6, 32 spp (x = 4.6) 51.9 / 43.1 / 42.1 (5 lanes: 41.5).
+  // Feed mode: this lane holds a reserved item it has not read (it pins a ring slot until it does), so its
+  // wavefront's fetch block runs now rather than when enough lanes wait (see fetch_feed).
+  __device__ __forceinline__ bool fetch_urgent() {
+    return !RegCold && feed_word && cold().pix == kFeedPending;
+  }
   __device__ __forceinline__ int fetch_job(uint64_t& j, int32_t wave_lanes) {
     if (!RegCold && feed_word) return fetch_feed(j);  // (feeds run the throughput kernels only)
     if (wave_lanes == 0) {
@@ -1619,6 +1624,8 @@ int feed_open(vpt_gpu_ctx* ctx, float* film_device, void* hip_stream, uint64_t w
   // launched at once, its idle wavefronts would poll the host link for work (r04).
   f->launched = false;
   f->launch_at = (uint64_t)ctx->grid_blocks * vpt::kBlockThreads;
+  // (With the urgent-fetch gate, launching at 1/4 or 1/16 of the lanes no longer stalls, but gains nothing
+  // measurable either: C3 368.6-372.7 vs 368.4-376.2 ms, C4 116-137 vs 117-134; r05u2.)
   // (Launching at a quarter or a sixteenth of the lanes saved nothing and stalled: lanes racing past the
   // published count hold items their waves serve late, and the wrapping ring waits for them; r05k.)
   feed_trace(f.get(), stage ? "open_stg" : "open", (double)cap, (double)(uintptr_t)hip_stream);

@@ -1190,7 +1190,10 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
     const DevScene S = *opaque(sp);
     const DevGrid& G = S.density;
     (void)G;
-    if (go(ST_FETCH)) {
+    // (a feed lane holding an unread item runs the block at once: its ring slot is pinned until it reads it)
+    const int32_t n_fetch = env.count(ln.state == ST_FETCH);
+    if (n_fetch > 0 && (starving || n_fetch >= gate_min || env.count(ln.state == ST_FETCH && env.fetch_urgent()) > 0) &&
+        ln.state == ST_FETCH) {
       env.prof(PB_FETCH);
       uint64_t j;
       // 1: job j (an item index, or a job id in the feed mode); 0: no more work; < 0 (feed mode): the lane
