@@ -1,0 +1,9 @@
+#!/bin/bash
+# r05final2: the final GPU check of the round: the whole GPU suite, smoke, bench.py C3 (dropin, CPU baseline) and C4 / C2 / C1.
+# bench.py C3 (its dropin record, CPU baseline) and C4 / C2 / C1 lines.
+set -u
+STEPS="pytest smoke bench" bash tools/gpu_check.sh r05final2 || exit 1
+for c in c4 c2 c1; do
+  timeout -k 10 600 python bench.py --config $c --no-cpu-baseline > gpurun_out/r05final2/bench_$c.log 2>&1 || { tail -5 gpurun_out/r05final2/bench_$c.log; exit 1; }
+  tail -1 gpurun_out/r05final2/bench_$c.log | cut -c1-300
+done
