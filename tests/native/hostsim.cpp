@@ -42,7 +42,7 @@ struct HostEnv {
   void prof_add(int32_t, int32_t) {}
   void tick(int32_t) {}
   void event(vpt::Lane&, uint32_t, const float*, const float*, float) {}
-  bool fetch_urgent() const { return false; }  // (no feeds on the host)
+  bool fetch_urgent(bool) const { return false; }  // (no feeds on the host)
   bool fetch_job(uint64_t& j, int32_t /*wave_lanes: the GPU's job spreading*/) {
     if (next >= jid_count) return false;
     j = next++;

@@ -95,8 +95,11 @@ __shared__ double g_logf_tab[16][2];
 constexpr int kBbFloats = kBbLdsRows * 3;
 
 
-template <bool RegCold>
+// RegCold: the latency kernel's environment (the lane's cold state in VGPRs).  Feed: a feed launch's (job ids from
+// the host's ring, fetch_feed); other launches compile the feed protocol out.
+template <bool RegCold, bool Feed = false>
 struct KernelEnvT {
+  static_assert(!(RegCold && Feed), "feeds run the throughput kernels only");
   uint64_t jid_begin;
   uint64_t jid_count;
   unsigned long long* job_counter;
@@ -230,13 +233,16 @@ struct KernelEnvT {
   // one lane with a few jobs in a row wins: C1 frames on the full grid (r02g,
   // profiles/r02g_c1_lanes_sweep.txt), 1 / 2 / 3 lanes: 8 spp (x = 1.1) 23.3 / 29.3 / - ms, 16 spp
   // (x = 2.3) 31.7 / 32.5 / 35.6, 32 spp (x = 4.6) 51.9 / 43.1 / 42.1 (5 lanes: 41.5).
-  // Feed mode: this lane holds a reserved item it has not read (it pins a ring slot until it does), so its
-  // wavefront's fetch block runs now rather than when enough lanes wait (see fetch_feed).
-  __device__ __forceinline__ bool fetch_urgent() {
-    return !RegCold && feed_word && cold().pix == kFeedPending;
+  // Feed mode: a fetching lane of this wavefront holds a reserved item it has not read (it pins a ring slot
+  // until it does), so the fetch block runs now rather than when enough lanes wait (see fetch_feed).
+  __device__ __forceinline__ bool fetch_urgent(bool fetching) {
+    if constexpr (Feed)
+      return count(fetching && cold().pix == kFeedPending) > 0;
+    else
+      return false;
   }
   __device__ __forceinline__ int fetch_job(uint64_t& j, int32_t wave_lanes) {
-    if (!RegCold && feed_word) return fetch_feed(j);  // (feeds run the throughput kernels only)
+    if constexpr (Feed) return fetch_feed(j);
     if (wave_lanes == 0) {
       const float x = (float)jid_count * __builtin_amdgcn_rcpf((float)(gridDim.x * (kBlockThreads / 64)));
       wave_lanes = x < 3.0f ? 1 : 1 + (int32_t)x;
@@ -321,7 +327,7 @@ struct KernelEnvT {
   // A job's last pixel is done: a staged feed counts it for its tile (the film's sample counts are the host's
   // per-tile job counts, vpt_gpu_feed_snapshot / _collect).  Once per job (64 samples); a uniform branch.
   __device__ __forceinline__ void job_end(const DevScene& S, const LaneCold& lc) {
-    if (!RegCold && tile_done)
+    if (Feed && tile_done)
       atomicAdd(tile_done + (uint32_t)(lc.y0 / S.th) * S.ntx + (uint32_t)(lc.x0 / S.tw), 1u);
   }
   __device__ __forceinline__ void film_add(const DevScene& S, const Lane& ln, int32_t px, int32_t py, int32_t rw) {
@@ -475,8 +481,8 @@ __device__ __forceinline__ void compact_loop(ScenePtr sp, Lane& ln, LaneCold& lc
 }
 
 // counters[] order = vpt_counters field order
-template <bool HasTemp, bool Debug, bool Runs, bool Lat = false, bool Compact = false>
-__global__ __launch_bounds__(kBlockThreads, Compact ? 2 : (Lat ? VPT_WAVES_LAT : (Debug ? VPT_WAVES_SLOW : (HasTemp ? VPT_WAVES_TEMP : VPT_WAVES_FAST)))) void vpt_integrate_kernel(const DevScene* scene, KernelEnvT<Lat> env,
+template <bool HasTemp, bool Debug, bool Runs, bool Lat = false, bool Compact = false, bool Feed = false>
+__global__ __launch_bounds__(kBlockThreads, Compact ? 2 : (Lat ? VPT_WAVES_LAT : (Debug ? VPT_WAVES_SLOW : (HasTemp ? VPT_WAVES_TEMP : VPT_WAVES_FAST)))) void vpt_integrate_kernel(const DevScene* scene, KernelEnvT<Lat, Feed> env,
                                                                        unsigned long long* counters) {
   __shared__ unsigned long long wg_counters[kCounterCount];
   if (threadIdx.x < kCounterCount) wg_counters[threadIdx.x] = 0;
@@ -510,7 +516,7 @@ __global__ __launch_bounds__(kBlockThreads, Compact ? 2 : (Lat ? VPT_WAVES_LAT :
     lane_iteration<HasTemp, Debug, Runs>(sp, ln, env);
     // Feed mode: a wavefront whose every live lane waits for the host to publish its item sleeps between
     // polls (~27 us), so idle wavefronts do not flood the host link with reads.
-    if (!Debug && !Lat && env.feed_word &&
+    if (Feed &&
         __builtin_amdgcn_ballot_w64(ln.state == ST_FETCH && (env.cold().pix == kFeedPending ||
                                                               env.cold().pix == kFeedWait)) ==
             __builtin_amdgcn_read_exec())
@@ -1048,6 +1054,14 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
                                          : vpt::vpt_integrate_kernel<false, false, false, true>;
       hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, scene, envl, ctx->counters);
     }
+  } else if (feed) {  // (never a debug launch: no records or events)
+    vpt::KernelEnvT<false, true> envf;
+    static_assert(sizeof envf == sizeof env, "one layout for every kernel environment");
+    std::memcpy(&envf, &env, sizeof env);
+    auto kernel = temp ? vpt::vpt_integrate_kernel<true, false, false, false, false, true>
+                       : ctx->use_runs ? vpt::vpt_integrate_kernel<false, false, true, false, false, true>
+                                       : vpt::vpt_integrate_kernel<false, false, false, false, false, true>;
+    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, scene, envf, ctx->counters);
   } else {
     auto kernel = temp ? (dbg ? vpt::vpt_integrate_kernel<true, true, false> : vpt::vpt_integrate_kernel<true, false, false>)
                        : ctx->use_runs

@@ -1192,7 +1192,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
     (void)G;
     // (a feed lane holding an unread item runs the block at once: its ring slot is pinned until it reads it)
     const int32_t n_fetch = env.count(ln.state == ST_FETCH);
-    if (n_fetch > 0 && (starving || n_fetch >= gate_min || env.count(ln.state == ST_FETCH && env.fetch_urgent()) > 0) &&
+    if (n_fetch > 0 && (starving || n_fetch >= gate_min || env.fetch_urgent(ln.state == ST_FETCH)) &&
         ln.state == ST_FETCH) {
       env.prof(PB_FETCH);
       uint64_t j;
