@@ -33,6 +33,7 @@ struct HostEnv {
   const uint32_t* perm = nullptr;   // explicit job order (vpt_gpu_set_job_permutation)
   uint32_t order_tail_k0 = 0;
   uint32_t order_tail_n = 0;
+  const HostEnv* args() const { return this; }  // (the kernel reads its launch arguments through args())
   int32_t count(bool pred) { return pred ? 1 : 0; }  // one lane
   vpt::LaneCold cold_{};
   vpt::LaneCold& cold() { return cold_; }

@@ -95,11 +95,8 @@ __shared__ double g_logf_tab[16][2];
 constexpr int kBbFloats = kBbLdsRows * 3;
 
 
-// RegCold: the latency kernel's environment (the lane's cold state in VGPRs).  Feed: a feed launch's (job ids from
-// the host's ring, fetch_feed); other launches compile the feed protocol out.
-template <bool RegCold, bool Feed = false>
-struct KernelEnvT {
-  static_assert(!(RegCold && Feed), "feeds run the throughput kernels only");
+// A launch's arguments (the host fills them; the integrator kernel's first argument).
+struct KernelArgs {
   uint64_t jid_begin;
   uint64_t jid_count;
   unsigned long long* job_counter;
@@ -108,8 +105,6 @@ struct KernelEnvT {
   int32_t tile_area;
   uint32_t pixel_chunk;  // throughput mode: pixels per work item (a power of two dividing tile_area; else 1)
   unsigned long long* prof_buf;  // [PB_COUNT][2] wave executions, active lanes; then [PT_COUNT] cycles
-  unsigned long long* lds_prof;  // this workgroup's section cycles (LDS, VPT_PROFILE builds)
-  unsigned long long* lds_counters;  // this workgroup's event counters (LDS)
   const uint32_t* order;             // job order: tile ranks (nullptr = jid order), see ordered_job
   const uint32_t* perm;              // explicit job order (item k -> job perm[k]), overrides order
   uint32_t order_tail_k0;
@@ -130,20 +125,43 @@ struct KernelEnvT {
   uint32_t feed_hint_mask;           // hint slots - 1
   uint32_t* tile_done;               // a staged feed: jobs completed per tile (device memory), else nullptr
   uint32_t compact_every;            // the compacting latency kernel: outer iterations between two meetings
+};
+typedef const __attribute__((address_space(4))) KernelArgs* ArgsPtr;
+// This workgroup's event counters and (VPT_PROFILE builds) section cycles; the temperature kernel's LDS copy of
+// S.bb's first kBbLdsRows rows.
+__shared__ unsigned long long g_wg_counters[kCounterCount];
+#if defined(VPT_PROFILE) || defined(VPT_PROFILE_TIME)
+__shared__ unsigned long long g_wg_prof[PT_COUNT + kBlockThreads / 64];
+#endif
+__shared__ float g_bb_lds[kBbFloats];
+
+// The kernel's view of its launch.  RegCold: the latency kernel's (the lane's cold state in VGPRs).  Feed: a feed
+// launch's (job ids from the host's ring, fetch_feed); other launches compile the feed protocol out.  The
+// arguments are read where they are used, through an opaque pointer to the kernel's argument segment (scalar
+// loads, as the scene's constants are, see ScenePtr): loads the optimiser cannot hoist, so no argument stays live
+// in SGPRs across the state-machine loop (they spilled to VGPR lanes: v_readlane / v_writelane in every block).
+template <bool RegCold, bool Feed = false>
+struct KernelEnvT {
+  static_assert(!(RegCold && Feed), "feeds run the throughput kernels only");
+  __device__ __forceinline__ ArgsPtr args() const {
+    ArgsPtr p = (ArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();  // (KernelArgs is the first argument: offset 0)
+    asm volatile("" : "+s"(p));
+    return p;
+  }
 
   // Adds w for every active lane with w != 0 (w uniform per call site) to a workgroup counter.
   __device__ __forceinline__ void tally(int32_t k, int32_t w) {
     const unsigned long long m = __builtin_amdgcn_ballot_w64(w != 0);
     if (m && __lane_id() == (uint32_t)__builtin_ctzll(m))
-      atomicAdd(lds_counters + k, (unsigned long long)(__popcll(m) * (uint64_t)(w ? w : 1)));
+      atomicAdd(g_wg_counters + k, (unsigned long long)(__popcll(m) * (uint64_t)(w ? w : 1)));
   }
 
   __device__ __forceinline__ void prof(int32_t id) {
 #ifdef VPT_PROFILE
     const unsigned long long m = __ballot(1);
     if ((__lane_id() == (uint32_t)__builtin_ctzll(m))) {
-      atomicAdd(prof_buf + 2 * id, 1ULL);
-      atomicAdd(prof_buf + 2 * id + 1, (unsigned long long)__popcll(m));
+      atomicAdd(args()->prof_buf + 2 * id, 1ULL);
+      atomicAdd(args()->prof_buf + 2 * id + 1, (unsigned long long)__popcll(m));
     }
 #else
     (void)id;
@@ -154,8 +172,8 @@ struct KernelEnvT {
 #ifdef VPT_PROFILE
     const unsigned long long m = __ballot(1);
     if ((__lane_id() == (uint32_t)__builtin_ctzll(m))) {
-      atomicAdd(prof_buf + 2 * id, 1ULL);
-      atomicAdd(prof_buf + 2 * id + 1, (unsigned long long)n);
+      atomicAdd(args()->prof_buf + 2 * id, 1ULL);
+      atomicAdd(args()->prof_buf + 2 * id + 1, (unsigned long long)n);
     }
 #else
     (void)id;
@@ -169,8 +187,8 @@ struct KernelEnvT {
     const unsigned long long t = clock64();
     const unsigned long long m = __ballot(1);
     if (__lane_id() == (uint32_t)__builtin_ctzll(m)) {
-      unsigned long long* last = lds_prof + PT_COUNT + threadIdx.x / 64;
-      atomicAdd(lds_prof + id, t - *last);
+      unsigned long long* last = g_wg_prof + PT_COUNT + threadIdx.x / 64;
+      atomicAdd(g_wg_prof + id, t - *last);
       *last = t;
     }
 #else
@@ -179,12 +197,13 @@ struct KernelEnvT {
   }
   // One Logger line (src/worker.cpp:16-48); a = xyz, b = xyz or (b == nullptr) x in v[3].
   __device__ __forceinline__ void event(Lane& ln, uint32_t type, const float* a, const float* b, float x) {
+    vpt_event* const events = args()->events;
     if (!events) return;
-    const unsigned long long slot = atomicAdd(event_count, 1ULL);
+    const unsigned long long slot = atomicAdd(args()->event_count, 1ULL);
     const uint32_t seq = ln.n_events++;
-    if (slot >= event_cap) return;
+    if (slot >= args()->event_cap) return;
     vpt_event* e = events + slot;
-    e->jid = jid_begin + ln.jid_local;
+    e->jid = args()->jid_begin + ln.jid_local;
     e->pixel = (uint32_t)((cold().pix & kPixelMask) - 1);
     e->seq = seq;
     e->type = type;
@@ -203,20 +222,19 @@ struct KernelEnvT {
     else
       return g_lane_cold[threadIdx.x];
   }
-  const float* bb_lds;  // the temperature kernel's LDS copy of S.bb's first kBbLdsRows rows
   __device__ __forceinline__ const double (*logf_table() const)[2] { return g_logf_tab; }
   // blackbody_radiation_xyz from the LDS rows when the grid's temperatures stay in them (a uniform
   // branch, so each path keeps its own address space: ds_read or global loads, no flat pointer)
   __device__ __forceinline__ void blackbody(const DevScene& S, float t, float& X, float& Y, float& Z) const {
     if (S.bb_lds_ok)
-      blackbody_xyz(S, bb_lds, t, X, Y, Z);
+      blackbody_xyz(S, g_bb_lds, t, X, Y, Z);
     else
       blackbody_xyz(S, S.bb, t, X, Y, Z);
   }
 #ifdef VPT_JOB_LOG
   // diagnostic build: per job (tile, fetch time, end time, hardware id) into the records buffer
   __device__ __forceinline__ void job_done(uint32_t job, uint32_t tile, uint32_t t0) {
-    uint32_t* e = reinterpret_cast<uint32_t*>(records) + 4 * (uint64_t)job;
+    uint32_t* e = reinterpret_cast<uint32_t*>(args()->records) + 4 * (uint64_t)job;
     e[0] = tile;
     e[1] = t0;
     e[2] = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -244,12 +262,12 @@ struct KernelEnvT {
   __device__ __forceinline__ int fetch_job(uint64_t& j, int32_t wave_lanes) {
     if constexpr (Feed) return fetch_feed(j);
     if (wave_lanes == 0) {
-      const float x = (float)jid_count * __builtin_amdgcn_rcpf((float)(gridDim.x * (kBlockThreads / 64)));
+      const float x = (float)args()->jid_count * __builtin_amdgcn_rcpf((float)(gridDim.x * (kBlockThreads / 64)));
       wave_lanes = x < 3.0f ? 1 : 1 + (int32_t)x;
     }
     if ((int32_t)__lane_id() >= wave_lanes) return false;
-    unsigned long long v = atomicAdd(job_counter, 1ULL);
-    if (v >= jid_count) return 0;
+    unsigned long long v = atomicAdd(args()->job_counter, 1ULL);
+    if (v >= args()->jid_count) return 0;
     j = v;
     return 1;
   }
@@ -265,6 +283,10 @@ struct KernelEnvT {
   // host memory are vector-memory atomics of system scope.
   __device__ int fetch_feed(uint64_t& j) {
     LaneCold& lc = cold();
+    const ArgsPtr A = args();
+    unsigned long long* const job_counter = A->job_counter;
+    const uint64_t* const feed_word = A->feed_word;
+    unsigned* const feed_error = A->feed_error;
     const uint32_t now = (uint32_t)__builtin_amdgcn_s_memrealtime();  // 100 MHz
     // System-scope loads of host memory go to the host every time.  The host writes a slot before the word
     // that publishes it (release); the slot is read after an acquire fence that follows the word's load.
@@ -281,8 +303,8 @@ struct KernelEnvT {
           // The host's backlog estimate comes from hints that may land out of order; a count >= its published
           // count here means the lanes wait for it, whatever the hints say (vpt_gpu_feed_backlog).
           const uint64_t m = __builtin_amdgcn_ballot_w64(true);
-          if (feed_waiting && __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == (uint32_t)__builtin_ctzll(m))
-            __hip_atomic_store(feed_waiting, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if (A->feed_waiting && __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == (uint32_t)__builtin_ctzll(m))
+            __hip_atomic_store(A->feed_waiting, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         } else if (now - (uint32_t)lc.x0 > kFeedDeadline) {
           __hip_atomic_store(feed_error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // (host memory: a store)
           return 0;
@@ -292,7 +314,7 @@ struct KernelEnvT {
       const uint64_t k = atomicAdd(job_counter, 1ULL);
       // the host's backlog estimate (vpt_gpu_feed_backlog): a posted write every kStartedHint items
       if ((k & (kStartedHint - 1)) == 0)
-        __hip_atomic_store(feed_started + ((k / kStartedHint) & feed_hint_mask), k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(A->feed_started + ((k / kStartedHint) & A->feed_hint_mask), k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       lc.item_lo = (uint32_t)k;
       lc.item_hi = (uint32_t)(k >> 32);
       if (lc.pix != kFeedWait) lc.x0 = (int32_t)now;  // wait start
@@ -300,7 +322,7 @@ struct KernelEnvT {
     }
     const uint64_t k = ((uint64_t)lc.item_hi << 32) | lc.item_lo;
     if (k < published) {
-      uint64_t* slot = feed_ring + (k & feed_mask);
+      uint64_t* slot = A->feed_ring + (k & A->feed_mask);
       // Acquire after the word's load: the slot's load cannot be satisfied before it (ADVICE / VERDICT r04).
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       j = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -327,11 +349,12 @@ struct KernelEnvT {
   // A job's last pixel is done: a staged feed counts it for its tile (the film's sample counts are the host's
   // per-tile job counts, vpt_gpu_feed_snapshot / _collect).  Once per job (64 samples); a uniform branch.
   __device__ __forceinline__ void job_end(const DevScene& S, const LaneCold& lc) {
+ uint32_t* const tile_done = Feed ? args()->tile_done : nullptr;
     if (Feed && tile_done)
       atomicAdd(tile_done + (uint32_t)(lc.y0 / S.th) * S.ntx + (uint32_t)(lc.x0 / S.tw), 1u);
   }
   __device__ __forceinline__ void film_add(const DevScene& S, const Lane& ln, int32_t px, int32_t py, int32_t rw) {
-    float* f = film + ((int64_t)py * S.W + px) * 4;
+    float* f = args()->film + ((int64_t)py * S.W + px) * 4;
     const float r = S.imaging_ratio;
     const LaneCold& lc = cold();
     // The sample-count channel (w += 1 per sample) is added per launch by vpt_count_kernel: each fp32
@@ -342,17 +365,16 @@ struct KernelEnvT {
 #ifdef VPT_JOB_LOG
     if (false) {
 #else
-    if (records) {
+    if (float* const records = args()->records) {
 #endif
       const int32_t xl = px - lc.x0, yl = py - lc.y0;
-      float* rec = records + (ln.jid_local * (uint64_t)tile_area + (uint64_t)(yl * rw + xl)) * 3;
+      float* rec = args()->records + (ln.jid_local * (uint64_t)args()->tile_area + (uint64_t)(yl * rw + xl)) * 3;
       rec[0] = lc.L[0];
       rec[1] = lc.L[1];
       rec[2] = lc.L[2];
     }
   }
 };
-using KernelEnv = KernelEnvT<false>;
 
 
 // ---- live-path compaction (north_star: "wavefront ballot/prefix-sum to compact live rays") ----
@@ -427,7 +449,7 @@ __device__ __forceinline__ void compact_loop(ScenePtr sp, Lane& ln, LaneCold& lc
   __shared__ int32_t cnt[8];  // per wavefront: walking paths, other live paths
   const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const uint64_t below = l ? (~0ULL >> (64 - l)) : 0ULL;
-  const uint32_t every = env.compact_every;
+  const uint32_t every = env.args()->compact_every;
   for (;;) {
     for (uint32_t it = 0; it < every; ++it) {
       if (__builtin_amdgcn_ballot_w64(ln.state != ST_DONE) == 0) break;  // (wave-uniform)
@@ -482,26 +504,23 @@ __device__ __forceinline__ void compact_loop(ScenePtr sp, Lane& ln, LaneCold& lc
 
 // counters[] order = vpt_counters field order
 template <bool HasTemp, bool Debug, bool Runs, bool Lat = false, bool Compact = false, bool Feed = false>
-__global__ __launch_bounds__(kBlockThreads, Compact ? 2 : (Lat ? VPT_WAVES_LAT : (Debug ? VPT_WAVES_SLOW : (HasTemp ? VPT_WAVES_TEMP : VPT_WAVES_FAST)))) void vpt_integrate_kernel(const DevScene* scene, KernelEnvT<Lat, Feed> env,
+__global__ __launch_bounds__(kBlockThreads, Compact ? 2 : (Lat ? VPT_WAVES_LAT : (Debug ? VPT_WAVES_SLOW : (HasTemp ? VPT_WAVES_TEMP : VPT_WAVES_FAST)))) void vpt_integrate_kernel(KernelArgs args, const DevScene* scene,
                                                                        unsigned long long* counters) {
-  __shared__ unsigned long long wg_counters[kCounterCount];
-  if (threadIdx.x < kCounterCount) wg_counters[threadIdx.x] = 0;
+  (void)args;  // read through KernelEnvT::args()
+  if (threadIdx.x < kCounterCount) g_wg_counters[threadIdx.x] = 0;
   if (threadIdx.x < 32) g_logf_tab[threadIdx.x >> 1][threadIdx.x & 1] = math::kLogfTab[threadIdx.x >> 1][threadIdx.x & 1];
-  __shared__ float bb_lds[HasTemp ? kBbFloats : 1];
   if (HasTemp) {
     const float* bb = scene->bb;
-    for (int i = threadIdx.x; i < kBbFloats; i += kBlockThreads) bb_lds[i] = bb[i];
+    for (int i = threadIdx.x; i < kBbFloats; i += kBlockThreads) g_bb_lds[i] = bb[i];
   }
-  env.bb_lds = bb_lds;
   __syncthreads();
-  env.lds_counters = wg_counters;
 #if defined(VPT_PROFILE) || defined(VPT_PROFILE_TIME)
-  __shared__ unsigned long long wg_prof[PT_COUNT + kBlockThreads / 64];
-  if (threadIdx.x < PT_COUNT) wg_prof[threadIdx.x] = 0;
+  if (threadIdx.x < PT_COUNT) g_wg_prof[threadIdx.x] = 0;
   __syncthreads();
-  if (threadIdx.x % 64 == 0) wg_prof[PT_COUNT + threadIdx.x / 64] = clock64();
-  env.lds_prof = wg_prof;
+  if (threadIdx.x % 64 == 0) g_wg_prof[PT_COUNT + threadIdx.x / 64] = clock64();
 #endif
+  KernelEnvT<Lat, Feed> env;
+  env.reg_cold = nullptr;
   Lane ln;
   lane_init(ln);
   LaneCold lc_reg;
@@ -522,12 +541,12 @@ __global__ __launch_bounds__(kBlockThreads, Compact ? 2 : (Lat ? VPT_WAVES_LAT :
             __builtin_amdgcn_read_exec())
       for (int i = 0; i < 8; ++i) __builtin_amdgcn_s_sleep(127);
   }
-  atomicAdd(wg_counters + CNT_DDA_STEPS, (unsigned long long)ln.n_dda);
+  atomicAdd(g_wg_counters + CNT_DDA_STEPS, (unsigned long long)ln.n_dda);
   __syncthreads();
-  if (threadIdx.x < kCounterCount && wg_counters[threadIdx.x])
-    atomicAdd(counters + threadIdx.x, wg_counters[threadIdx.x]);
+  if (threadIdx.x < kCounterCount && g_wg_counters[threadIdx.x])
+    atomicAdd(counters + threadIdx.x, g_wg_counters[threadIdx.x]);
 #if defined(VPT_PROFILE) || defined(VPT_PROFILE_TIME)
-  if (threadIdx.x < PT_COUNT) atomicAdd(env.prof_buf + 2 * PB_COUNT + threadIdx.x, wg_prof[threadIdx.x]);
+  if (threadIdx.x < PT_COUNT) atomicAdd(env.args()->prof_buf + 2 * PB_COUNT + threadIdx.x, g_wg_prof[threadIdx.x]);
 #endif
 }
 
@@ -925,8 +944,7 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   const uint64_t total = ctx->scene.T * (uint64_t)ctx->cfg.num_waves;
   (void)total;  // jids beyond num_waves are valid jobs too (TileProvider only stops at requested_waves)
   hipStream_t s = (hipStream_t)stream_ptr;  // NULL = the null stream (HIP convention)
-  vpt::KernelEnv env;
-  env.reg_cold = nullptr;  // the latency kernel points it at its own local
+  vpt::KernelArgs env{};
   env.jid_begin = jid_begin;
   env.jid_count = jid_count;
   env.pixel_chunk = 1;
@@ -1039,35 +1057,29 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   if (slot_out) *slot_out = slot;
   const vpt::DevScene* scene = latency || (use_lat && ctx->lat_ungated) ? ctx->scene_lat_dev : ctx->scene_dev;
   if (use_lat) {
-    vpt::KernelEnvT<true> envl;
-    static_assert(sizeof envl == sizeof env, "one layout for both kernel environments");
-    std::memcpy(&envl, &env, sizeof env);
-    envl.compact_every = (uint32_t)std::max(1, ctx->compact_every);
+    env.compact_every = (uint32_t)std::max(1, ctx->compact_every);
     if (compact) {
       auto kernel = temp ? vpt::vpt_integrate_kernel<true, false, false, true, true>
                          : ctx->use_runs ? vpt::vpt_integrate_kernel<false, false, true, true, true>
                                          : vpt::vpt_integrate_kernel<false, false, false, true, true>;
-      hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), vpt::kXchgBytes, s, scene, envl, ctx->counters);
+      hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), vpt::kXchgBytes, s, env, scene, ctx->counters);
     } else {
       auto kernel = temp ? vpt::vpt_integrate_kernel<true, false, false, true>
                          : ctx->use_runs ? vpt::vpt_integrate_kernel<false, false, true, true>
                                          : vpt::vpt_integrate_kernel<false, false, false, true>;
-      hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, scene, envl, ctx->counters);
+      hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, env, scene, ctx->counters);
     }
   } else if (feed) {  // (never a debug launch: no records or events)
-    vpt::KernelEnvT<false, true> envf;
-    static_assert(sizeof envf == sizeof env, "one layout for every kernel environment");
-    std::memcpy(&envf, &env, sizeof env);
     auto kernel = temp ? vpt::vpt_integrate_kernel<true, false, false, false, false, true>
                        : ctx->use_runs ? vpt::vpt_integrate_kernel<false, false, true, false, false, true>
                                        : vpt::vpt_integrate_kernel<false, false, false, false, false, true>;
-    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, scene, envf, ctx->counters);
+    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, env, scene, ctx->counters);
   } else {
     auto kernel = temp ? (dbg ? vpt::vpt_integrate_kernel<true, true, false> : vpt::vpt_integrate_kernel<true, false, false>)
                        : ctx->use_runs
                            ? (dbg ? vpt::vpt_integrate_kernel<false, true, true> : vpt::vpt_integrate_kernel<false, false, true>)
                            : (dbg ? vpt::vpt_integrate_kernel<false, true, false> : vpt::vpt_integrate_kernel<false, false, false>);
-    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, scene, env, ctx->counters);
+    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(vpt::kBlockThreads), 0, s, env, scene, ctx->counters);
   }
   VPT_HIP(hipGetLastError());
   const uint64_t npix = (uint64_t)ctx->scene.W * (uint64_t)ctx->scene.H;

@@ -1205,14 +1205,14 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       }
       uint32_t p = 0;
       if (S.pixel_mode) {  // throughput mode: item = job * tile_area + pixel, taken pixel_chunk at a time
-        j *= env.pixel_chunk;
+        j *= env.args()->pixel_chunk;
         p = (uint32_t)(j % S.tile_area);
         j /= S.tile_area;
       }
-      if (env.perm)
-        j = env.perm[j];
-      else if (env.order)
-        j = ordered_job((uint32_t)j, (uint32_t)S.T, env.order, env.order_tail_k0, env.order_tail_n);
+      if (const uint32_t* const perm = env.args()->perm)
+        j = perm[j];
+      else if (const uint32_t* const order = env.args()->order)
+        j = ordered_job((uint32_t)j, (uint32_t)S.T, order, env.args()->order_tail_k0, env.args()->order_tail_n);
       if (Debug) {
         ln.jid_local = j;
         ln.n_events = 0;
@@ -1221,7 +1221,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       lc.job = (uint32_t)j;
       lc.t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-      uint64_t jid = env.jid_begin + j;
+      uint64_t jid = env.args()->jid_begin + j;
       if (S.pixel_mode) {  // each pixel's stream is seeded when the pixel starts (ST_PIXEL)
         const uint64_t base = jid * S.tile_area;
         lc.item_lo = (uint32_t)base;
@@ -1256,7 +1256,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       int32_t q = lc.pix & kPixelMask;
       // Throughput mode: the lane's chunk of pixel_chunk pixels (a power of two dividing the tile area; chunk
       // starts are multiples of it) ends at the next multiple once a pixel of it has been taken.
-      const int32_t K = (int32_t)env.pixel_chunk;
+      const int32_t K = (int32_t)env.args()->pixel_chunk;
       const int32_t end = one ? (((lc.pix & kPixelTaken) && (q & (K - 1)) == 0) ? 0 : min((q & ~(K - 1)) + K, rw * rh))
                               : rw * rh;
       while (true) {
