@@ -315,6 +315,22 @@ struct DevScene {
   float y_integral;
 };
 
+// The scene as the kernel reads it: a pointer into the constant address space (scalar loads).
+// opaque() hides the pointer's value from the optimiser, so loads through it are not hoisted out
+// of the state-machine loop (they would pin ~100 SGPRs for the whole kernel and spill to VGPR
+// lanes); each block re-reads the few constants it uses with s_load instead.
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(4))) DevScene* ScenePtr;
+#else
+typedef const DevScene* ScenePtr;
+#endif
+__host__ __device__ __forceinline__ ScenePtr opaque(ScenePtr p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+s"(p));
+#endif
+  return p;
+}
+
 // ------------------------------------------------------------------------------------------------
 // RNG: hash(seed, jid) + pcg32_fast + uniform<float> (hash.hpp:20-67, random.hpp:86-115)
 // ------------------------------------------------------------------------------------------------
@@ -902,10 +918,13 @@ __host__ __device__ inline void scene_finalize(DevScene& S) {
 // A primary ray's real-or-null collision (worker.cpp:148-188) at the index point pi with density
 // dens: emission (HasTemp), then sample_discrete({Null, Absorption, Scatter}, u) with
 // p_a = sigma_a*dens/sigma_maj, p_s = sigma_s*dens/sigma_maj.  u < 0: draw the event's uniform here
-// (after the emission, as the reference); else u is that draw, taken by the caller.
+// (after the emission, as the reference); else u is that draw, taken by the caller.  The emission re-reads the
+// scene through sp at its own point: the temperature grid's fields and the blackbody constants, loaded from the
+// evaluation's copy S, were scheduled at the evaluation's start and held across the density lookup -- ~17 SGPRs
+// spilled to VGPR lanes and read back (a v_writelane / v_readlane pair each) on every evaluation.
 // (r04's temperature-corner prefetch, measured 2.5 % slower on C4: tools/experiments/r04_temp_prefetch.patch.)
 template <bool HasTemp, bool Debug, class Env>
-__host__ __device__ __forceinline__ void primary_event(const DevScene& S, const DevGrid& G, Lane& ln, LaneCold& lc, Env& env,
+__host__ __device__ __forceinline__ void primary_event(ScenePtr sp, const DevScene& S, const DevGrid& G, Lane& ln, LaneCold& lc, Env& env,
                                                        float pi_x, float pi_y, float pi_z, float dens, float p_a,
                                                        float p_s, float u) {
   env.prof(PB_EVENT);
@@ -914,17 +933,18 @@ __host__ __device__ __forceinline__ void primary_event(const DevScene& S, const 
   if (Debug) env.event(ln, VPT_EV_SAMPLED_POINT, cp, nullptr, dens);
   const float p_n = fmaxf(1.0f - p_a - p_s, 0.0f);
   if (HasTemp) {
+    const DevScene St = *opaque(sp);
     float tx, ty, tz, tadim, X, Y, Z;
-    map_inv(S.temperature, cp[0], cp[1], cp[2], tx, ty, tz);
+    map_inv(St.temperature, cp[0], cp[1], cp[2], tx, ty, tz);
 #ifdef VPT_EXP_TEMP_NOCACHE
     StencilCell tc{kNoCell, 0, 0, -1};
-    env.tally(CNT_TEMP_STENCILS, trilinear(S.temperature, tc, tx, ty, tz, tadim) ? 1 : 0);
+    env.tally(CNT_TEMP_STENCILS, trilinear(St.temperature, tc, tx, ty, tz, tadim) ? 1 : 0);
 #else
-    env.tally(CNT_TEMP_STENCILS, trilinear(S.temperature, ln.temp_cell, tx, ty, tz, tadim) ? 1 : 0);
+    env.tally(CNT_TEMP_STENCILS, trilinear(St.temperature, ln.temp_cell, tx, ty, tz, tadim) ? 1 : 0);
 #endif
-    float tK = tadim * S.temp_scale + S.temp_offset;
-    env.blackbody(S, tK, X, Y, Z);
-    float sc = p_a * S.le_scale;
+    float tK = tadim * St.temp_scale + St.temp_offset;
+    env.blackbody(St, tK, X, Y, Z);
+    float sc = p_a * St.le_scale;
     lc.L[0] = lc.L[0] + sc * X;
     lc.L[1] = lc.L[1] + sc * Y;
     lc.L[2] = lc.L[2] + sc * Z;
@@ -974,7 +994,7 @@ __host__ __device__ __forceinline__ void primary_event(const DevScene& S, const 
 // A tentative collision at s_t0 (SM_EVAL): density, then the primary path's event
 // (worker.cpp:145-188) or the shadow ray's ratio-tracking update (worker.cpp:66-85).
 template <bool HasTemp, bool Debug, class Env>
-__host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const DevGrid& G, Lane& ln, Env& env) {
+__host__ __device__ __forceinline__ void eval_collision(ScenePtr sp, const DevScene& S, const DevGrid& G, Lane& ln, Env& env) {
   LaneCold& lc = env.cold();
   const float sigma_maj = ln.s_dmaj * S.sigma_t;
   {
@@ -1014,7 +1034,7 @@ __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const
         if (Debug) env.tally(CNT_RNG_DRAWS, 1);
       }
       if (!sh) {
-        primary_event<HasTemp, Debug>(S, G, ln, lc, env, pi_x, pi_y, pi_z, dens, q1, (S.sigma_s * dens) / sigma_maj, u);
+        primary_event<HasTemp, Debug>(sp, S, G, ln, lc, env, pi_x, pi_y, pi_z, dens, q1, (S.sigma_s * dens) / sigma_maj, u);
       } else {
         env.prof(PB_SHADOW_HIT);
         float T = tr;  // Russian roulette, q = 0.75
@@ -1030,7 +1050,7 @@ __host__ __device__ __forceinline__ void eval_collision(const DevScene& S, const
       // worker.cpp:148-188
       const float p_a = (S.sigma_a * dens) / sigma_maj;
       const float p_s = (S.sigma_s * dens) / sigma_maj;
-      primary_event<HasTemp, Debug>(S, G, ln, lc, env, pi_x, pi_y, pi_z, dens, p_a, p_s, -1.0f);
+      primary_event<HasTemp, Debug>(sp, S, G, ln, lc, env, pi_x, pi_y, pi_z, dens, p_a, p_s, -1.0f);
     } else {
       env.prof(PB_SHADOW_HIT);
       // Ratio tracking with Russian roulette (worker.cpp:68-85)
@@ -1088,21 +1108,6 @@ __host__ __device__ __forceinline__ uint64_t ordered_job(uint32_t k, uint32_t T,
 // film_add(S, lane, px, py, rw).  HasTemp: the scene has a temperature grid (fire).
 // Debug: keep every counter and the job index (per-sample records).
 // ------------------------------------------------------------------------------------------------
-// The scene as the kernel reads it: a pointer into the constant address space (scalar loads).
-// opaque() hides the pointer's value from the optimiser, so loads through it are not hoisted out
-// of the state-machine loop (they would pin ~100 SGPRs for the whole kernel and spill to VGPR
-// lanes); each block re-reads the few constants it uses with s_load instead.
-#if defined(__HIP_DEVICE_COMPILE__)
-typedef const __attribute__((address_space(4))) DevScene* ScenePtr;
-#else
-typedef const DevScene* ScenePtr;
-#endif
-__host__ __device__ __forceinline__ ScenePtr opaque(ScenePtr p) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  asm volatile("" : "+s"(p));
-#endif
-  return p;
-}
 
 template <bool HasTemp, bool Debug, bool Runs, class Env>
 __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, Env& env) {
@@ -1445,7 +1450,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
     const int32_t n_eval = env.count(ln.state == ST_SAMPLE && ln.sm == SM_EVAL);
     const bool run_eval = n_eval > 0 && (n_eval >= S.gate_eval || env.count(ln.state == ST_SAMPLE && ln.sm != SM_EVAL) < S.gate_idle);
     if (!HasTemp && run_eval) wave_priority(kPrioEval);
-    if (run_eval && ln.state == ST_SAMPLE && ln.sm == SM_EVAL) eval_collision<HasTemp, Debug>(S, G, ln, env);
+    if (run_eval && ln.state == ST_SAMPLE && ln.sm == SM_EVAL) eval_collision<HasTemp, Debug>(sp, S, G, ln, env);
     if (!HasTemp) wave_priority(0);
   }
   env.tick(PT_EVAL);
