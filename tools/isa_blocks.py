@@ -6,7 +6,8 @@ priority 3, so its region is the one after `s_setprio 3`).
     python tools/isa_blocks.py /tmp/vpt.s [flags ...]
 
 flags: the kernel's template bools HasTemp, Debug, Runs, Lat, Compact, Feed as a digit string (default: every
-kernel; e.g. 001000 = the run-skipping throughput kernel C3 runs, 100000 = the temperature kernel)."""
+kernel; e.g. 000000 = the density kernel C3 runs, 001000 = its run-skipping variant, 100000 = the temperature
+kernel C4 runs)."""
 import re
 import sys
 

@@ -1,0 +1,5 @@
+#!/bin/bash
+# r05end (a): the round's closing evidence for C3 on the final kernels: PMC traffic passes, rocprofv3 kernel trace of
+# the bench, the full bench line (tools/profile_round.sh).
+set -u
+bash tools/profile_round.sh r05end c3
