@@ -61,6 +61,7 @@ struct HostEnv {
       vpt::blackbody_xyz(S, S.bb, t, X, Y, Z);
     }
   }
+  void film_commit(const vpt::DevScene&, bool) {}  // (one lane: film_add adds directly)
   void film_add(const vpt::DevScene& S, const vpt::Lane& ln, int32_t px, int32_t py, int32_t rw) {
     float* f = film + ((int64_t)py * S.W + px) * 4;
     f[3] += 1.0f;

@@ -134,6 +134,8 @@ __shared__ unsigned long long g_wg_counters[kCounterCount];
 __shared__ unsigned long long g_wg_prof[PT_COUNT + kBlockThreads / 64];
 #endif
 __shared__ float g_bb_lds[kBbFloats];
+// A finish-block pass's samples, per wavefront by rank: (pixel index << 6) | lane (KernelEnvT::film_add / film_commit).
+__shared__ uint32_t g_film_rank[kBlockThreads];
 
 // The kernel's view of its launch.  RegCold: the latency kernel's (the lane's cold state in VGPRs).  Feed: a feed
 // launch's (job ids from the host's ring, fetch_feed); other launches compile the feed protocol out.  The
@@ -349,19 +351,36 @@ struct KernelEnvT {
   // A job's last pixel is done: a staged feed counts it for its tile (the film's sample counts are the host's
   // per-tile job counts, vpt_gpu_feed_snapshot / _collect).  Once per job (64 samples); a uniform branch.
   __device__ __forceinline__ void job_end(const DevScene& S, const LaneCold& lc) {
- uint32_t* const tile_done = Feed ? args()->tile_done : nullptr;
+    uint32_t* const tile_done = Feed ? args()->tile_done : nullptr;
     if (Feed && tile_done)
       atomicAdd(tile_done + (uint32_t)(lc.y0 / S.th) * S.ntx + (uint32_t)(lc.x0 / S.tw), 1u);
   }
+  // The film's X, Y, Z: three fp32 adds per sample (the sample-count channel is added per launch by
+  // vpt_count_kernel, or per job in a staged feed).  Float atomics execute at the memory side, one request per
+  // 64-B line a wave-instruction touches: three instructions whose 64 lanes add to 64 different pixels are 192
+  // requests, ~17x the cost of the same bytes contiguous (MI355X_MICROARCH.md § Global float atomics); with
+  // them C3 took 348 ms against 328 without any film writes, C4 97 against 77 (r05ab7).  So the kernels with
+  // the lane state in LDS regroup a finish pass's samples: film_add only ranks the lane in g_film_rank, and
+  // film_commit, run by the converged wavefront, has lane 3k + c add component c of the k-th sample -- one
+  // wave-instruction carries 21 samples, each sample's three adds one request.  The latency kernel (state in
+  // VGPRs, few samples at a time) adds from the lane itself.
+  __device__ __forceinline__ static bool film_regroup(const DevScene& S) {
+    return !RegCold && (uint64_t)S.W * (uint64_t)S.H < (1ULL << 26);  // (pixel index << 6 | lane fits 32 bits)
+  }
   __device__ __forceinline__ void film_add(const DevScene& S, const Lane& ln, int32_t px, int32_t py, int32_t rw) {
-    float* f = args()->film + ((int64_t)py * S.W + px) * 4;
-    const float r = S.imaging_ratio;
+    const uint32_t pixel = (uint32_t)py * (uint32_t)S.W + (uint32_t)px;
     const LaneCold& lc = cold();
-    // The sample-count channel (w += 1 per sample) is added per launch by vpt_count_kernel: each fp32
-    // atomic here costs ~2 % of the C3 frame (it stays in vmcnt until the memory side acks it).
-    atomicAdd(f + 0, r * lc.L[0]);
-    atomicAdd(f + 1, r * lc.L[1]);
-    atomicAdd(f + 2, r * lc.L[2]);
+    if (film_regroup(S)) {
+      const uint64_t m = __builtin_amdgcn_ballot_w64(true);  // this pass's finishing lanes
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      g_film_rank[(threadIdx.x & ~63u) + rank] = (pixel << 6) | (threadIdx.x & 63u);
+    } else {
+      float* f = args()->film + (uint64_t)pixel * 4;
+      const float r = S.imaging_ratio;
+      atomicAdd(f + 0, r * lc.L[0]);
+      atomicAdd(f + 1, r * lc.L[1]);
+      atomicAdd(f + 2, r * lc.L[2]);
+    }
 #ifdef VPT_JOB_LOG
     if (false) {
 #else
@@ -372,6 +391,30 @@ struct KernelEnvT {
       rec[0] = lc.L[0];
       rec[1] = lc.L[1];
       rec[2] = lc.L[2];
+    }
+  }
+  // fin: this lane ran film_add in the pass just ended.  Called by every lane still in the loop; the lanes that
+  // have left it (their jobs done) are not there to add, so the 3 n adds go to the active lanes by rank, as many
+  // per wave-instruction as there are active lanes (adds 3k, 3k + 1, 3k + 2: sample k's X, Y, Z).
+  __device__ __forceinline__ void film_commit(const DevScene& S, bool fin) {
+    if (!film_regroup(S)) return;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(fin);
+    if (m == 0) return;
+    const uint64_t a = __builtin_amdgcn_ballot_w64(true);
+    const uint32_t adds = 3u * (uint32_t)__popcll(m), na = (uint32_t)__popcll(a);
+    const uint32_t ai = __builtin_amdgcn_mbcnt_hi((uint32_t)(a >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a, 0u));
+    float* const film = args()->film;
+    const float r = S.imaging_ratio;
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));  // (else tid & ~63 is hoisted out of the state-machine loop into a VGPR)
+    const uint32_t w0 = tid & ~63u;
+    for (uint32_t i0 = 0; i0 < adds; i0 += na) {  // (uniform)
+      const uint32_t i = i0 + ai;
+      if (i < adds) {
+        const uint32_t k = i / 3u, c = i - 3u * k;
+        const uint32_t e = g_film_rank[w0 + k];
+        atomicAdd(film + (uint64_t)(e >> 6) * 4 + c, r * g_lane_cold[w0 + (e & 63u)].L[c]);
+      }
     }
   }
 };

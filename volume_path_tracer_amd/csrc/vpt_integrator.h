@@ -1175,7 +1175,8 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
     const DevScene S = *opaque(sp);
     const DevGrid& G = S.density;
     (void)G;
-    if (go2(ST_FINISH, ST_FINISH_T)) {
+    const bool fin = go2(ST_FINISH, ST_FINISH_T);
+    if (fin) {
       env.prof(PB_FINISH);
       if (ln.state == ST_FINISH) {  // not terminated (worker.cpp:198-200)
         lc.L[0] = lc.L[0] + S.le_inf[0];
@@ -1189,6 +1190,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       env.tally(CNT_SAMPLES, 1);
       ln.state = ST_PIXEL;
     }
+    env.film_commit(S, fin);  // (the converged wavefront: see KernelEnvT::film_add)
   }
   env.tick(PT_FINISH);
   {
