@@ -1240,8 +1240,9 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   // Scheduling defaults from tools/tune.py sweeps on MI355X (C3, 256 spp): rare states run for >= 6
   // waiting lanes, density evaluations (with the deferred exact draw) for >= 36, everything runs when
   // < 8 lanes are walking; the walk loops while >= 4 lanes walk (r02 sweep: 6:8:36:4 363.7 ms vs
-  // 6:12:32:4 366.6 ms, C4 103.7 vs 104.4).
-  ctx->scene.gate_min = 6;
+  // 6:12:32:4 366.6 ms, C4 103.7 vs 104.4).  The temperature kernel's rare blocks wait for 8 lanes since the film
+  // regroup (C4 83.3-83.6 vs 83.9-84.3 ms over 4 alternating runs, profiles/r05gates2_c4_gate_min.txt).
+  ctx->scene.gate_min = temperature ? 8 : 6;
   ctx->scene.gate_idle = 8;
   ctx->scene.gate_eval = 36;
   ctx->scene.gate_walk = 4;
