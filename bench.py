@@ -132,8 +132,9 @@ def film_parity(wl, dens, temp, ref_film, waves: int, device: int) -> dict:
     """north_star's parity criterion on the bench's own frame: the production kernel renders the waves the CPU
     baseline just rendered with the oracle's worker pool (waves 1..k, the same jobs and PCG streams), and the
     per-pixel radiance (film XYZ / sample count) is compared -- RMSE over every pixel and channel against the
-    stated bound of 1e-4, the largest difference, and the sample counts (which must be equal).  Only the fp32
-    order of the film's atomic adds differs from the oracle's per-pixel wave order."""
+    stated bound of 1e-4, the largest difference, and the sample counts (which must be equal).  With the ordered
+    film (the default, vpt_gpu_set_film_order) the GPU adds each pixel's samples in wave order, the oracle's
+    order, so the two films are compared bit for bit too (`bit_identical`, `pixels_differing`)."""
     import numpy as np
     import torch
 
@@ -143,7 +144,9 @@ def film_parity(wl, dens, temp, ref_film, waves: int, device: int) -> dict:
     it.render_waves(1, waves)
     torch.cuda.synchronize()
     gpu = it.film_host()
+    film_mode = it.film_order_info()
     del it
+    differ = int((gpu.view(np.uint32) != ref_film.view(np.uint32)).any(axis=-1).sum())
     counts_equal = bool(np.array_equal(gpu[..., 3], ref_film[..., 3]))
     n = np.maximum(ref_film[..., 3:4].astype(np.float64), 1.0)
     lg, lr = gpu[..., :3].astype(np.float64) / n, ref_film[..., :3].astype(np.float64) / n
@@ -151,6 +154,8 @@ def film_parity(wl, dens, temp, ref_film, waves: int, device: int) -> dict:
     return {"waves": waves, "pixels": int(lg.shape[0] * lg.shape[1]), "counts_equal": counts_equal,
             "rmse_per_pixel": rmse, "max_abs_diff": float(np.abs(lg - lr).max()),
             "mean_radiance": float(np.abs(lr).mean()), "bound": 1e-4, "ok": counts_equal and rmse < 1e-4,
+            "bit_identical": differ == 0, "pixels_differing": differ,
+            "film_order": "ordered (wave order)" if film_mode["mode"] == 1 else "atomic",
             "vs": "oracle worker pool (tests/oracle_lib.py render_pool), same waves and seeds"}
 
 
@@ -478,6 +483,9 @@ def main():
     ap.add_argument("--compaction", type=int, default=None,
                     help="live-path compaction period on partly filled latency launches (A/B runs; default: the "
                          "library's, off)")
+    ap.add_argument("--film-order", choices=["ordered", "atomic"], default="ordered",
+                    help="ordered (default): each pixel's samples added in wave order, the reference's film bit for bit "
+                         "(vpt_gpu_set_film_order); atomic: fp32 atomics in completion order (A/B runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the reference-API (drop-in) frame timing")
     ap.add_argument("--dropin-frames", type=int, default=3)
@@ -534,6 +542,8 @@ def main():
         lat_info = it.latency_kernel_info()
     if args.compaction is not None:
         it.set_compaction(args.compaction)
+    if args.film_order == "atomic":
+        it.set_film_order(_capi.VPT_FILM_ATOMIC)
     log(f"[rank {rank}] grids ready in {time.time() - t0:.1f}s: {dens.leaf_count} leaves, "
         f"launch {it.launch_info()}, latency kernel {lat_info}")
 
@@ -598,6 +608,7 @@ def main():
                        "jobs_per_step_per_gpu": jobs_rank, "volume": f"synthetic {wl.grid_n}^3 kind {wl.density_kind}",
                        "parallelism": f"wave-sharded x{world} ({args.mode}), RCCL film all-reduce" if world > 1 else "1 GPU",
                        "rng_mode": args.rng_mode, "latency_kernel": args.latency_kernel,
+                       "film_order": args.film_order,
                        **({"compaction": args.compaction} if args.compaction is not None else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,

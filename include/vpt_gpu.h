@@ -203,8 +203,9 @@ int vpt_gpu_job_space(const vpt_gpu_ctx* ctx, uint64_t* jobs_per_wave, uint64_t*
 /* Render jobs [jid_begin, jid_begin + jid_count) asynchronously on `hip_stream`
  * (a hipStream_t; NULL = the null stream, as everywhere in HIP), accumulating into `film_device`:
  * a device float[H][W][4] (X, Y, Z, sample count; image.hpp:40-60) — NULL = the context's own
- * film.  Film adds are fp32 atomics, so the per-pixel sum order may differ from the
- * reference's wave order (≈1e-7 relative).
+ * film.  With the ordered film (the default, vpt_gpu_set_film_order) each pixel's samples are
+ * added in wave order, the reference's order, so a film rendered from zero equals the reference's
+ * bit for bit; with VPT_FILM_ATOMIC they are fp32 atomics in completion order (≈1e-7 relative).
  *
  * Concurrency: launches of one context may be in flight on several streams at once.  Each launch
  * takes its own job counter from a ring of 64 per context; a ring slot is reused only after the
@@ -216,6 +217,29 @@ int vpt_gpu_job_space(const vpt_gpu_ctx* ctx, uint64_t* jobs_per_wave, uint64_t*
  * made from a second thread while the first is inside vpt_gpu_render_jobs is not supported. */
 int vpt_gpu_render_jobs(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count,
                         float* film_device, void* hip_stream);
+
+/* How launches add into the film.  The reference's film receives each pixel's samples in wave order:
+ * TileProvider::next() hands a tile's wave out only after its previous wave is released
+ * (tile_provider.cpp:40-60), and a job adds each pixel's sample as it is traced (worker.cpp:203-204:
+ * w += 1, xyz += imaging_ratio * L).
+ *   VPT_FILM_ORDERED (default): a production launch stores every sample's L into a device buffer of
+ *     jid_count * tile_w*tile_h * 12 bytes (plain stores, regrouped through the wavefront as the atomics
+ *     were), then vpt_film_order_kernel adds them into the film pixel by pixel in wave order: a film
+ *     rendered from zero by one launch -- or by launches of consecutive job ranges in jid order -- equals
+ *     the reference's bit for bit, and every run gives the same film.  The buffer is the context's (kept
+ *     between launches; C3: 6.4 GB, C5 on one GPU: 102 GB); ordered launches of a context run one at a time
+ *     (each waits for the previous one's film pass on its stream).  max_bytes caps the buffer (0 = auto:
+ *     3/4 of the device's free memory when it grows): a larger launch is split into consecutive launches,
+ *     whole waves at a time where the range allows -- the same film.
+ *   VPT_FILM_ATOMIC: fp32 atomics as samples complete (the order varies run to run, ≈1e-7 relative).
+ * Debug launches (records, events) and feeds always add atomically; so does a launch whose buffer would
+ * have to grow while a feed of the context is open.  Takes effect at the next launch; VPT_FILM_ATOMIC
+ * frees the buffer. */
+enum { VPT_FILM_ATOMIC = 0, VPT_FILM_ORDERED = 1 };
+int vpt_gpu_set_film_order(vpt_gpu_ctx* ctx, int mode, uint64_t max_bytes);
+/* The film mode, the sample buffer's size and the launches that ran ordered / atomic (feeds not counted). */
+int vpt_gpu_film_order_info(const vpt_gpu_ctx* ctx, int* mode, uint64_t* buffer_bytes, uint64_t* ordered_launches,
+                            uint64_t* atomic_launches);
 
 /* Like vpt_gpu_render_jobs but also writes every sample's radiance L (before the
  * imaging_ratio scale) to records_device[(jid - jid_begin) * tile_w*tile_h + y_local*rect_w + x_local][3]
@@ -451,6 +475,17 @@ int vpt_gpu_profile(vpt_gpu_ctx* ctx, uint64_t* out, int n, int reset);
 int vpt_gpu_launch_info(const vpt_gpu_ctx* ctx, int* grid_blocks, int* block_threads);
 /* Number of HIP devices (0 without a GPU: VPT_OK, *count = 0). */
 int vpt_gpu_device_count(int* count);
+/* The drop-in's seed recovery on the GPU: the u32 seeds s (ascending, at most max_seeds written) whose job-0
+ * stream -- pcg32_fast seeded with hash(s, 0) (hash.hpp:20-67, random.hpp:93-95) -- starts with the outputs
+ * out0, out1; *n_found = how many exist (normally 1).  The reference's RandomNumberGenerator keeps its seed
+ * private (random.hpp:86-115), so include/vpt_run.hpp finds it from two draws: all 2^32 candidates in one
+ * launch on `device` (a few ms; the same scan took 1-3 s on 8-16 host threads).  Synchronous. */
+int vpt_gpu_find_seeds(int device, uint32_t out0, uint32_t out1, uint32_t* seeds, int max_seeds, int* n_found);
+/* What vpt_gpu_create and the first cost pass took (ms), n <= 5 of: [0] grid flatten + leaf-majorant fix (host),
+ * [1] grid upload, [2] the rest of the context (tables, buffers, occupancy, scene constants), [3] the tile-cost
+ * pass (vpt_gpu_tile_costs / the first cost-ordered launch), [4] binding the device (hipSetDevice: the HIP
+ * runtime's start when it is the process's first HIP call). */
+int vpt_gpu_setup_timings(const vpt_gpu_ctx* ctx, double* ms, int n);
 
 /* ---- synthetic stand-in volumes (the reference's .nvdb files are not available) ---------- */
 

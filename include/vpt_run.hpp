@@ -162,14 +162,26 @@ class FeedPipeline {
     if (err_ != VPT_OK) return err_;
     queue_.insert(queue_.end(), runs.begin(), runs.end());
     queued_ += n;
+    added_.fetch_add(n, std::memory_order_relaxed);
     return VPT_OK;
+  }
+  // Jobs given to this pipeline and not yet started on the GPU: queued and held on the host, plus the feed's
+  // backlog as the pusher last read it (drain_devices routes each batch to the GPU with the fewest).
+  uint64_t pending() {
+    std::lock_guard<std::mutex> l(mu_);
+    return queued_ + held_ + backlog_seen_.load(std::memory_order_relaxed);
+  }
+  uint64_t added() const { return added_.load(std::memory_order_relaxed); }  // jobs given to add()
+  uint64_t lanes() const { return lanes_; }  // the launch's lanes: it starts once that many jobs are pushed
+  // No more add(): the pusher pushes what it holds and closes the feed (finish() then waits for the launch).
+  // drain_devices ends every GPU's input first, so no pipeline's last push waits for another one's launch.
+  void end_input() {
+    std::lock_guard<std::mutex> l(mu_);
+    no_more_ = true;
   }
   // No more jobs: the pusher pushes what it holds and closes the feed; then the rest of the film is added.
   int finish() {
-    {
-      std::lock_guard<std::mutex> l(mu_);
-      no_more_ = true;
-    }
+    end_input();
     if (pusher_.joinable()) pusher_.join();
     stop_threads();  // no snapshot starts once the feed is closed: the collect adds the rest
     detail::drain_trace("taker_blocked_ms", blocked_s_ * 1e3);
@@ -220,6 +232,11 @@ class FeedPipeline {
   int top_up(std::vector<uint64_t>& hold, size_t& head) {
     uint64_t b = 0;
     if (int rc = vpt_gpu_feed_backlog(feed_, &b)) return rc;
+    struct Seen {  // (the backlog after this call's pushes, for pending())
+      std::atomic<uint64_t>& to;
+      const uint64_t& b;
+      ~Seen() { to.store(b, std::memory_order_relaxed); }
+    } seen{backlog_seen_, b};
     const uint64_t mark = pushed_ < lanes_ ? std::max(backlog_, lanes_) : backlog_;
     while (head < hold.size() && b < mark) {
       const uint64_t n = std::min<uint64_t>(kChunk, hold.size() - head);
@@ -344,6 +361,7 @@ class FeedPipeline {
   bool no_more_ = false;
   int err_ = VPT_OK;
   std::atomic<bool> film_stop_{false};
+  std::atomic<uint64_t> added_{0}, backlog_seen_{0};
 };
 
 namespace detail {

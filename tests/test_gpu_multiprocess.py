@@ -73,6 +73,62 @@ def test_hip_integrator_world2_gloo(mode, tmp_path):
     for f in (got, single):
         np.testing.assert_array_equal(f[..., 3], float(total))
         np.testing.assert_allclose(f[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
+    # one process, one launch: the ordered film is the oracle's bit for bit (the reduced film sums two ranks'
+    # partial films, a different fp32 association)
+    assert single.tobytes() == ref.tobytes()
+
+
+def _rccl_worker(rank, world, port, out_dir):
+    sys.path[:0] = [str(ROOT), str(ROOT / "tests")]
+    import torch
+    import torch.distributed as dist
+
+    from volume_path_tracer_amd import distributed as D
+    from volume_path_tracer_amd.render import Integrator
+    from volume_path_tracer_amd.scenes import SynthGrid, workload
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)  # as bench.init_rank does
+    wl = workload("c3", width=W, height=H, spp=3, grid_n=GRID)
+    it = Integrator(wl.cfg, SynthGrid(1, GRID).grid(), None, device=0)
+    D.render_rank(it, rank, world, 3, "weak")
+    torch.cuda.synchronize()
+    before = it.film.clone()
+    # the collectives the multi-GPU path issues: the film's device-pointer all-reduce (reduce_film's call) and the
+    # bench's scalar MAX / SUM reductions on the device
+    dist.all_reduce(it.film, op=dist.ReduceOp.SUM)
+    t = torch.tensor([2.5], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    n = torch.tensor([7.0], dtype=torch.float64, device=dev)
+    dist.all_reduce(n, op=dist.ReduceOp.SUM)
+    torch.cuda.synchronize()
+    info = {"backend": dist.get_backend(), "film_unchanged": bool(torch.equal(before, it.film)),
+            "max": float(t.item()), "sum": float(n.item()),
+            "rccl_version": ".".join(str(x) for x in torch.cuda.nccl.version())}
+    (Path(out_dir) / "rccl.json").write_text(json.dumps(info))
+    np.save(Path(out_dir) / "film.npy", it.film.cpu().numpy())
+    dist.destroy_process_group()
+
+
+def test_rccl_one_rank_film_all_reduce(tmp_path):
+    """RCCL itself on the MI355X: a one-rank "nccl" process group bound to device 0 -- the
+    library load, communicator init and the device-pointer all-reduce of an Integrator's film that
+    distributed.reduce_film issues on a node (RCCL refuses two ranks on one GPU, so world 1 is what one box can
+    run).  The film comes back unchanged, the counts exact and the film the oracle's bit for bit."""
+    import torch.multiprocessing as mp
+
+    assert_hip_untouched()
+    mp.start_processes(_rccl_worker, args=(1, _free_port(), str(tmp_path)), nprocs=1, start_method="spawn")
+    info = json.loads((tmp_path / "rccl.json").read_text())
+    print("rccl:", info)
+    assert info["backend"] == "nccl" and info["film_unchanged"] and info["max"] == 2.5 and info["sum"] == 7.0
+    film = np.load(tmp_path / "film.npy")
+    wl = workload("c3", width=W, height=H, spp=3, grid_n=GRID)
+    ref, _, _ = O.render_jobs(wl.cfg, O.OracleGrid(SynthGrid(1, GRID).grid()), None, 0, wl.cfg.jobs_per_wave() * 3)
+    np.testing.assert_array_equal(film[..., 3], 3.0)
+    assert film.tobytes() == ref.tobytes()
 
 
 def test_bench_gpus2_spawns_two_ranks(tmp_path):

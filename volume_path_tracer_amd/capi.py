@@ -97,6 +97,7 @@ DDA_ROW_DTYPE = np.dtype([("ijk", "<i4", (3,)), ("t", "<f4"), ("value", "<f4"), 
 assert DDA_ROW_DTYPE.itemsize == 36
 VPT_RNG_REFERENCE, VPT_RNG_PIXEL = 0, 1
 VPT_ORDER_JID, VPT_ORDER_COST_WAVE_MAJOR, VPT_ORDER_COST_TILE_MAJOR, VPT_ORDER_COST_TAIL = 0, 1, 2, 3
+VPT_FILM_ATOMIC, VPT_FILM_ORDERED = 0, 1
 EVENT_NAMES = ("new_ray", "sampled_point", "null", "scatter_terminated", "scatter", "absorbed")
 
 
@@ -252,6 +253,10 @@ def lib() -> C.CDLL:
         L.vpt_gpu_set_pixel_chunk.argtypes = [vp, C.c_int]
     L.vpt_gpu_set_run_skipping.argtypes = [vp, C.c_int]
     L.vpt_gpu_kernel_variant.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    if hasattr(L, "vpt_gpu_set_film_order"):
+        L.vpt_gpu_set_film_order.argtypes = [vp, C.c_int, C.c_uint64]
+        L.vpt_gpu_film_order_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_uint64),
+                                              C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.vpt_gpu_set_job_order.argtypes = [vp, C.c_int]
     L.vpt_gpu_set_job_order_tail.argtypes = [vp, C.c_int]
     L.vpt_gpu_tile_costs.argtypes = [vp, fp, C.POINTER(C.c_uint32)]

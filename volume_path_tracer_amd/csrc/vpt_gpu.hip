@@ -125,6 +125,10 @@ struct KernelArgs {
   uint32_t feed_hint_mask;           // hint slots - 1
   uint32_t* tile_done;               // a staged feed: jobs completed per tile (device memory), else nullptr
   uint32_t compact_every;            // the compacting latency kernel: outer iterations between two meetings
+  // The ordered film (vpt_gpu_set_film_order): every sample's L, plain stores, at
+  // samples[(j * tile_area + local pixel) * 3 + c] (j = the job's index in the launch, the records layout);
+  // vpt_film_order_kernel then adds them into the film pixel by pixel in wave order.  nullptr: film atomics.
+  float* samples;
 };
 typedef const __attribute__((address_space(4))) KernelArgs* ArgsPtr;
 // This workgroup's event counters and (VPT_PROFILE builds) section cycles; the temperature kernel's LDS copy of
@@ -364,16 +368,28 @@ struct KernelEnvT {
   // film_commit, run by the converged wavefront, has lane 3k + c add component c of the k-th sample -- one
   // wave-instruction carries 21 samples, each sample's three adds one request.  The latency kernel (state in
   // VGPRs, few samples at a time) adds from the lane itself.
-  __device__ __forceinline__ static bool film_regroup(const DevScene& S) {
-    return !RegCold && (uint64_t)S.W * (uint64_t)S.H < (1ULL << 26);  // (pixel index << 6 | lane fits 32 bits)
+  //
+  // The ordered film (args()->samples, vpt_gpu_set_film_order): the same regroup with plain stores of each
+  // sample's L into the launch's sample buffer (job j's pixel q at (j * tile_area + q) * 3: three lanes store one
+  // sample's 12 contiguous bytes, one request), the rank word holding (q << 6) | lane and the job index coming
+  // from the source lane's cold state (item_lo, set at its fetch); the film itself is written only by
+  // vpt_film_order_kernel, in wave order.
+  __device__ __forceinline__ bool film_regroup(const DevScene& S) const {
+    return !RegCold && (args()->samples != nullptr || (uint64_t)S.W * (uint64_t)S.H < (1ULL << 26));  // (index << 6 | lane fits 32 bits)
   }
   __device__ __forceinline__ void film_add(const DevScene& S, const Lane& ln, int32_t px, int32_t py, int32_t rw) {
-    const uint32_t pixel = (uint32_t)py * (uint32_t)S.W + (uint32_t)px;
     const LaneCold& lc = cold();
+    float* const samples = args()->samples;
+    const uint32_t pixel = samples ? (uint32_t)((py - lc.y0) * rw + (px - lc.x0)) : (uint32_t)py * (uint32_t)S.W + (uint32_t)px;
     if (film_regroup(S)) {
       const uint64_t m = __builtin_amdgcn_ballot_w64(true);  // this pass's finishing lanes
       const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
       g_film_rank[(threadIdx.x & ~63u) + rank] = (pixel << 6) | (threadIdx.x & 63u);
+    } else if (samples) {  // (the latency kernel: from the lane itself)
+      float* s = samples + ((uint64_t)lc.item_lo * S.tile_area + pixel) * 3;
+      s[0] = lc.L[0];
+      s[1] = lc.L[1];
+      s[2] = lc.L[2];
     } else {
       float* f = args()->film + (uint64_t)pixel * 4;
       const float r = S.imaging_ratio;
@@ -404,6 +420,7 @@ struct KernelEnvT {
     const uint32_t adds = 3u * (uint32_t)__popcll(m), na = (uint32_t)__popcll(a);
     const uint32_t ai = __builtin_amdgcn_mbcnt_hi((uint32_t)(a >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a, 0u));
     float* const film = args()->film;
+    float* const samples = args()->samples;
     const float r = S.imaging_ratio;
     uint32_t tid = threadIdx.x;
     asm volatile("" : "+v"(tid));  // (else tid & ~63 is hoisted out of the state-machine loop into a VGPR)
@@ -413,7 +430,11 @@ struct KernelEnvT {
       if (i < adds) {
         const uint32_t k = i / 3u, c = i - 3u * k;
         const uint32_t e = g_film_rank[w0 + k];
-        atomicAdd(film + (uint64_t)(e >> 6) * 4 + c, r * g_lane_cold[w0 + (e & 63u)].L[c]);
+        const LaneCold& src = g_lane_cold[w0 + (e & 63u)];
+        if (samples)
+          samples[((uint64_t)src.item_lo * S.tile_area + (e >> 6)) * 3 + c] = src.L[c];
+        else
+          atomicAdd(film + (uint64_t)(e >> 6) * 4 + c, r * src.L[c]);
       }
     }
   }
@@ -621,6 +642,71 @@ __global__ void vpt_tile_count_kernel(const DevScene* scene, float* film, const 
   if (S.single_pixel_enabled && (px != S.sp_x || py != S.sp_y)) return;
   const uint32_t n = counts[(uint64_t)(py / S.th) * S.ntx + (uint64_t)(px / S.tw)];
   if (n) atomicAdd(film + p * 4 + 3, (float)n);
+}
+
+// The ordered film (vpt_gpu_set_film_order): adds the samples of the launch's jobs [jid_begin, jid_begin +
+// jid_count) into the film pixel by pixel in wave order -- the order the reference's film receives them: a
+// tile's waves are handed out one at a time (TileProvider::next waits for the tile's previous wave,
+// tile_provider.cpp:40-60) and each job adds its pixels' samples as it traces them (worker.cpp:203-204:
+// w += 1, xyz += imaging_ratio * L).  So the film equals the reference's bit for bit, whatever order the
+// launch ran its jobs in.  One thread per (tile, local pixel), so a wavefront reads one job's samples as one
+// contiguous run (12 B per pixel) per wave; the film's float4 is read and written once.
+__global__ void vpt_film_order_kernel(const DevScene* scene, float* film, const float* samples, uint64_t jid_begin,
+                                      uint64_t jid_count) {
+  const DevScene& S = *scene;
+  const uint32_t area = S.tile_area;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= S.T * (uint64_t)area) return;
+  const uint64_t t = i / area;
+  const uint32_t q = (uint32_t)(i - t * area);
+  const int32_t x0 = (int32_t)(t % S.ntx) * S.tw, y0 = (int32_t)(t / S.ntx) * S.th;
+  const int32_t rw = min(S.W - x0, S.tw), rh = min(S.H - y0, S.th);
+  if ((int32_t)q >= rw * rh) return;
+  const int32_t yl = (int32_t)q / rw, px = x0 + ((int32_t)q - yl * rw), py = y0 + yl;
+  if (S.single_pixel_enabled && (px != S.sp_x || py != S.sp_y)) return;  // (no sample: worker.cpp:113-116)
+  const uint64_t T = S.T, end = jid_begin + jid_count;
+  const uint64_t k0 = jid_begin > t ? (jid_begin - t + T - 1) / T : 0;
+  if (t + k0 * T >= end) return;
+  float4* const f = reinterpret_cast<float4*>(film) + ((uint64_t)py * (uint64_t)S.W + (uint64_t)px);
+  float4 a = *f;
+  const float r = S.imaging_ratio;
+  const float* s = samples + ((t + k0 * T - jid_begin) * area + q) * 3;
+  const uint64_t step = T * area * 3;
+  const uint64_t n = (end - 1 - t) / T - k0 + 1;
+#pragma unroll 8
+  for (uint64_t k = 0; k < n; ++k, s += step) {
+    a.w = a.w + 1.0f;
+    a.x = a.x + r * s[0];
+    a.y = a.y + r * s[1];
+    a.z = a.z + r * s[2];
+  }
+  *f = a;
+}
+
+// The drop-in's seed recovery (include/vpt_run.hpp rng_seed): the reference's RandomNumberGenerator keeps its u32
+// seed private (random.hpp:86-115), so the seeds s whose job-0 stream starts with the outputs (a, b) are found by
+// trying all 2^32: hash(s, 0) (hash.hpp:20-67; with jid 0 its k term is 0) | 3 is pcg32_fast's state, whose
+// output (xsh_rs: (st ^ st >> 22) >> (22 + st >> 61)) is taken before each multiply (pcg_random.hpp).  Each
+// thread tries `per_thread` consecutive seeds; a hit (normally one in 2^32) is appended with an atomic.
+__global__ void vpt_seed_search_kernel(uint32_t a, uint32_t b, uint32_t per_thread, uint32_t* found, uint32_t* count,
+                                       uint32_t cap) {
+  constexpr uint64_t m = 0xc6a4a7935bd1e995ULL, mult = 6364136223846793005ULL;
+  const uint64_t first = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * per_thread;
+  for (uint32_t i = 0; i < per_thread; ++i) {
+    const uint64_t s = first + i;
+    if (s >> 32) break;
+    uint64_t h = s ^ (8ULL * m);
+    h *= m;
+    h ^= h >> 47;
+    h *= m;
+    h ^= h >> 47;
+    const uint64_t st = h | 3ULL;
+    if ((uint32_t)((st ^ (st >> 22)) >> (22 + (uint32_t)(st >> 61))) != a) continue;
+    const uint64_t s2 = st * mult;
+    if ((uint32_t)((s2 ^ (s2 >> 22)) >> (22 + (uint32_t)(s2 >> 61))) != b) continue;
+    const uint32_t k = atomicAdd(count, 1u);
+    if (k < cap) found[k] = (uint32_t)s;
+  }
 }
 
 // Volume::log_majorant_trace (src/volume.cpp:176-192) of one world ray, on one lane: every
@@ -836,6 +922,18 @@ struct vpt_gpu_ctx {
   int lat_per_cu = 1;              // resident blocks per CU of the latency kernel
   int compact_every = 0;           // live-path compaction on partly filled latency launches: meeting period (0 off)
   int compact_per_cu = 0;          // resident blocks per CU of the compacting kernel (its LDS exchange)
+  // The ordered film (vpt_gpu_set_film_order): the sample buffer of ordered launches (one at a time: each
+  // waits for the previous one's vpt_film_order_kernel, samples_done), and the largest buffer a launch may use
+  // (0 = auto, 3/4 of the device's free memory when it grows; larger launches are split).
+  int film_order = VPT_FILM_ORDERED;
+  uint64_t film_order_max = 0;
+  float* samples = nullptr;
+  uint64_t samples_bytes = 0;
+  hipEvent_t samples_done = nullptr;
+  bool samples_used = false;
+  uint64_t ordered_launches = 0, atomic_launches = 0;  // (vpt_gpu_film_order_info)
+  // vpt_gpu_create's phases (ms): grid flatten + majorant fix, grid upload, the rest, the tile-cost pass, device bind
+  double setup_ms[5] = {};
 };
 
 namespace {
@@ -931,6 +1029,8 @@ void destroy(vpt_gpu_ctx* ctx) {
   (void)hipFree(ctx->scene_lat_dev);
   (void)hipFree(ctx->order);
   (void)hipFree(ctx->perm);
+  (void)hipFree(ctx->samples);
+  if (ctx->samples_done) (void)hipEventDestroy(ctx->samples_done);
   for (uint32_t i = 0; i < kLaunchSlots; ++i)
     if (ctx->slot_done[i]) (void)hipEventDestroy(ctx->slot_done[i]);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -960,6 +1060,12 @@ int rank_tiles(vpt_gpu_ctx* ctx) {
 // Tile costs (vpt_tile_cost_kernel) and the descending-cost tile ranks, once per context.
 int ensure_order(vpt_gpu_ctx* ctx) {
   if (ctx->order) return VPT_OK;
+  const auto t0 = std::chrono::steady_clock::now();
+  struct Lap {  // (the cost pass's time, vpt_gpu_setup_timings)
+    vpt_gpu_ctx* c;
+    std::chrono::steady_clock::time_point t0;
+    ~Lap() { c->setup_ms[3] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+  } lap{ctx, t0};
   if (ctx->open_feeds.load() > 0)  // the cost pass and its copy would wait for the feed's launch
     return vpt::set_error(VPT_E_STATE, "tile costs: a feed of this context is open (compute them before)");
   const uint64_t T = ctx->scene.T;
@@ -975,6 +1081,43 @@ int ensure_order(vpt_gpu_ctx* ctx) {
   return rank_tiles(ctx);
 }
 
+// The ordered film's sample buffer for a launch of `bytes`: the context's, grown if needed.  nullptr (VPT_OK)
+// when it must grow while a feed of the context is open -- freeing or allocating device memory could wait for
+// the feed's launch -- and that launch then adds into the film with atomics.
+int ensure_samples(vpt_gpu_ctx* ctx, uint64_t bytes, float*& out) {
+  out = nullptr;
+  if (ctx->samples_bytes >= bytes) {
+    out = ctx->samples;
+    return VPT_OK;
+  }
+  if (ctx->open_feeds.load() > 0) return VPT_OK;
+  if (ctx->samples_used) VPT_HIP(hipEventSynchronize(ctx->samples_done));  // (ordered launches are serialised)
+  if (ctx->samples) {
+    (void)hipFree(ctx->samples);
+    ctx->samples = nullptr;
+    ctx->samples_bytes = 0;
+  }
+  const hipError_t e = hipMalloc((void**)&ctx->samples, bytes);
+  if (e != hipSuccess) {
+    ctx->samples = nullptr;
+    (void)hipGetLastError();
+    return vpt::set_error(VPT_E_NOMEM, "ordered film: " + std::to_string(bytes >> 20) + " MiB sample buffer: " +
+                                           hipGetErrorString(e) + " (vpt_gpu_set_film_order's max_bytes splits launches)");
+  }
+  ctx->samples_bytes = bytes;
+  out = ctx->samples;
+  return VPT_OK;
+}
+
+// The largest sample buffer an ordered launch may use (bytes).
+uint64_t ordered_cap(vpt_gpu_ctx* ctx, uint64_t want) {
+  if (ctx->film_order_max) return ctx->film_order_max;
+  if (want <= ctx->samples_bytes) return ctx->samples_bytes;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return ctx->samples_bytes;
+  return (uint64_t)(free_b + ctx->samples_bytes) / 4 * 3;
+}
+
 int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film, float* records, void* stream_ptr,
            vpt_event* events = nullptr, uint64_t event_cap = 0, uint32_t* slot_out = nullptr,
            const vpt::FeedLaunch* feed = nullptr) {
@@ -984,6 +1127,22 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   if (jid_count == 0) return VPT_OK;
   if (feed && (ctx->scene.pixel_mode || records || events))
     return vpt::set_error(VPT_E_INVALID, "render: feeds run the reference RNG mode's production kernels only");
+  // The ordered film: production launches of the reference RNG mode (debug launches and feeds add atomically).
+  // A launch whose sample buffer would exceed the cap is rendered as consecutive launches (whole waves where it
+  // can); each adds its own waves in order, so the film is the same.
+  const uint64_t per_job = (uint64_t)ctx->scene.tile_area * 3 * sizeof(float);
+  const bool ordered = ctx->film_order == VPT_FILM_ORDERED && !feed && !records && !events && !ctx->scene.pixel_mode;
+  if (ordered) {
+    const uint64_t max_jobs = std::min<uint64_t>(ordered_cap(ctx, jid_count * per_job) / per_job, 0xffffffffULL);
+    if (max_jobs == 0) return vpt::set_error(VPT_E_NOMEM, "ordered film: no room for one job's samples");
+    if (jid_count > max_jobs) {
+      const uint64_t T = ctx->scene.T;
+      const uint64_t chunk = max_jobs >= T ? max_jobs / T * T : max_jobs;
+      for (uint64_t b = 0; b < jid_count; b += chunk)
+        if ((rc = render(ctx, jid_begin + b, std::min(chunk, jid_count - b), film, nullptr, stream_ptr))) return rc;
+      return VPT_OK;
+    }
+  }
   const uint64_t total = ctx->scene.T * (uint64_t)ctx->cfg.num_waves;
   (void)total;  // jids beyond num_waves are valid jobs too (TileProvider only stops at requested_waves)
   hipStream_t s = (hipStream_t)stream_ptr;  // NULL = the null stream (HIP convention)
@@ -1082,6 +1241,15 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
     env.order_tail_k0 = (n - tail) * (uint32_t)T;
   }
   if (!feed && ctx->perm && ctx->perm_n == jid_count && !ctx->scene.pixel_mode) env.perm = ctx->perm;
+  float* samples = nullptr;
+  if (ordered && (rc = ensure_samples(ctx, jid_count * per_job, samples))) return rc;
+  env.samples = samples;
+  if (samples) {
+    ++ctx->ordered_launches;
+    if (ctx->samples_used) VPT_HIP(hipStreamWaitEvent(s, ctx->samples_done, 0));  // the buffer's previous launch
+  } else if (!feed) {
+    ++ctx->atomic_launches;
+  }
   uint32_t slot = 0;
   if ((rc = take_slot(ctx, s, slot))) return rc;
   env.job_counter = ctx->job_counter + 2 * slot;
@@ -1126,7 +1294,14 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   }
   VPT_HIP(hipGetLastError());
   const uint64_t npix = (uint64_t)ctx->scene.W * (uint64_t)ctx->scene.H;
-  if (!feed) {  // a feed adds its sample counts when it is closed (vpt_tile_count_kernel)
+  if (samples) {  // the film, pixel by pixel in wave order (sample counts included)
+    const uint64_t threads = ctx->scene.T * (uint64_t)ctx->scene.tile_area;
+    hipLaunchKernelGGL(vpt::vpt_film_order_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+                       ctx->scene_dev, env.film, samples, jid_begin, jid_count);
+    VPT_HIP(hipGetLastError());
+    VPT_HIP(hipEventRecord(ctx->samples_done, s));
+    ctx->samples_used = true;
+  } else if (!feed) {  // a feed adds its sample counts when it is closed (vpt_tile_count_kernel)
     hipLaunchKernelGGL(vpt::vpt_count_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, ctx->scene_dev,
                        env.film, jid_begin, jid_count);
     VPT_HIP(hipGetLastError());
@@ -1149,6 +1324,40 @@ int vpt_gpu_device_count(int* count) {
   return VPT_OK;
 }
 
+int vpt_gpu_find_seeds(int device, uint32_t out0, uint32_t out1, uint32_t* seeds, int max_seeds, int* n_found) {
+  if (!n_found || max_seeds < 0 || (max_seeds > 0 && !seeds))
+    return vpt::set_error(VPT_E_INVALID, "vpt_gpu_find_seeds: bad argument");
+  *n_found = 0;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return vpt::set_error(VPT_E_HIP, "vpt_gpu_find_seeds: no HIP device");
+  if (device < 0 || device >= ndev) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_find_seeds: bad device index");
+  VPT_HIP(hipSetDevice(device));
+  constexpr uint32_t kCap = 64, kPerThread = 1024, kThreads = 256;
+  hipStream_t s = nullptr;
+  VPT_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  uint32_t* d = nullptr;
+  uint32_t host[kCap + 1] = {};
+  hipError_t e = hipMalloc((void**)&d, (kCap + 1) * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemsetAsync(d, 0, (kCap + 1) * sizeof(uint32_t), s);
+  if (e == hipSuccess) {
+    const uint64_t blocks = ((1ULL << 32) / kPerThread + kThreads - 1) / kThreads;
+    hipLaunchKernelGGL(vpt::vpt_seed_search_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, s, out0, out1, kPerThread,
+                       d + 1, d, kCap);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(host, d, sizeof host, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(d);
+  (void)hipStreamDestroy(s);
+  if (e != hipSuccess) return vpt::set_error(VPT_E_HIP, std::string("vpt_gpu_find_seeds: ") + hipGetErrorString(e));
+  const uint32_t n = std::min(host[0], kCap);
+  std::sort(host + 1, host + 1 + n);
+  for (uint32_t i = 0; i < n && (int)i < max_seeds; ++i) seeds[i] = host[1 + i];
+  *n_found = (int)host[0];
+  return VPT_OK;
+}
+
 int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, const vpt_grid_desc* temperature,
                    const float* blackbody_500x3, int device, vpt_gpu_ctx** out) {
   if (!cfg || !density || !out) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_create: null argument");
@@ -1161,8 +1370,16 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   std::unique_ptr<vpt_gpu_ctx, void (*)(vpt_gpu_ctx*)> ctx(new vpt_gpu_ctx(), destroy);
   ctx->device = device;
   ctx->cfg = *cfg;
+  using clk = std::chrono::steady_clock;
+  auto t = clk::now();
+  auto lap = [&](int i) {  // setup phases (vpt_gpu_setup_timings)
+    const auto now = clk::now();
+    ctx->setup_ms[i] += std::chrono::duration<double, std::milli>(now - t).count();
+    t = now;
+  };
   int rc = ctx_device(ctx.get());
   if (rc) return rc;
+  lap(4);
   if ((rc = vpt::build_scene(*cfg, ctx->scene))) return rc;
 
   // Volume::Volume: fix the density majorants (volume.cpp:162-170); temperature is only sampled.
@@ -1170,12 +1387,16 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
     vpt::HostGrid h;
     if ((rc = vpt::build_host_grid(*density, true, 0, h))) return rc;
     vpt::compute_runs(h, 0);
+    lap(0);
     if ((rc = vpt::upload_grid(h, ctx->density))) return rc;
+    lap(1);
   }
   if (temperature) {
     vpt::HostGrid h;
     if ((rc = vpt::build_host_grid(*temperature, false, 0, h))) return rc;
+    lap(0);
     if ((rc = vpt::upload_grid(h, ctx->temperature))) return rc;
+    lap(1);
   }
   // The run-skipping kernel variant is for grids with large equal-majorant regions (C2's constant
   // cube: 36 % of the interior cells have run radius >= 2; the 512^3 cloud: 4 %, where the variant
@@ -1211,6 +1432,7 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   VPT_HIP(hipMalloc((void**)&ctx->prof, kProfWords * sizeof(unsigned long long)));
   VPT_HIP(hipMemset(ctx->prof, 0, kProfWords * sizeof(unsigned long long)));
   VPT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+  VPT_HIP(hipEventCreateWithFlags(&ctx->samples_done, hipEventDisableTiming));
 
   // Persistent grid: as many blocks as are resident at once.
   int per_cu = 0, cus = 0;
@@ -1252,7 +1474,14 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   VPT_HIP(hipMalloc((void**)&ctx->scene_dev, sizeof(vpt::DevScene)));
   VPT_HIP(hipMalloc((void**)&ctx->scene_lat_dev, sizeof(vpt::DevScene)));
   if ((rc = push_scene(ctx.get()))) return rc;
+  lap(2);
   *out = ctx.release();
+  return VPT_OK;
+}
+
+int vpt_gpu_setup_timings(const vpt_gpu_ctx* ctx, double* ms, int n) {
+  if (!ctx || !ms || n < 0) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_setup_timings: bad argument");
+  for (int i = 0; i < n && i < 5; ++i) ms[i] = ctx->setup_ms[i];
   return VPT_OK;
 }
 
@@ -1351,6 +1580,32 @@ int vpt_gpu_kernel_variant(const vpt_gpu_ctx* ctx, int* has_temperature, int* ru
   if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
   if (has_temperature) *has_temperature = ctx->scene.has_temperature ? 1 : 0;
   if (run_skipping) *run_skipping = ctx->use_runs ? 1 : 0;
+  return VPT_OK;
+}
+
+int vpt_gpu_set_film_order(vpt_gpu_ctx* ctx, int mode, uint64_t max_bytes) {
+  if (!ctx || (mode != VPT_FILM_ATOMIC && mode != VPT_FILM_ORDERED))
+    return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_film_order: bad argument");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  ctx->film_order = mode;
+  ctx->film_order_max = max_bytes;
+  if (mode == VPT_FILM_ATOMIC && ctx->samples && ctx->open_feeds.load() == 0) {  // the buffer is not needed
+    if (ctx->samples_used) VPT_HIP(hipEventSynchronize(ctx->samples_done));
+    (void)hipFree(ctx->samples);
+    ctx->samples = nullptr;
+    ctx->samples_bytes = 0;
+  }
+  return VPT_OK;
+}
+
+int vpt_gpu_film_order_info(const vpt_gpu_ctx* ctx, int* mode, uint64_t* buffer_bytes, uint64_t* ordered_launches,
+                            uint64_t* atomic_launches) {
+  if (!ctx) return vpt::set_error(VPT_E_INVALID, "null context");
+  if (mode) *mode = ctx->film_order;
+  if (buffer_bytes) *buffer_bytes = ctx->samples_bytes;
+  if (ordered_launches) *ordered_launches = ctx->ordered_launches;
+  if (atomic_launches) *atomic_launches = ctx->atomic_launches;
   return VPT_OK;
 }
 

@@ -500,7 +500,9 @@ struct LaneCold {
   StencilCell dens_cell;  // the density sampler's last stencil cell (collision evaluation only)
   float Tr;               // shadow-ray transmittance (< 0: sample_Ld returns zero)
   float y_draw;           // 1 - u of a free-flight draw whose exact distance is pending (SM_EVAL)
-  uint32_t item_lo, item_hi;  // throughput mode: jid * tile_area of the lane's job (its pixels' streams)
+  uint32_t item_lo, item_hi;  // throughput mode: jid * tile_area of the lane's job (its pixels' streams);
+                              // reference mode: item_lo = the job's index in the launch (the ordered film);
+                              // feeds: the reserved item while the lane waits for it
 #ifdef VPT_JOB_LOG
   uint32_t t_start;       // diagnostic build: s_memrealtime at the job's fetch
   uint32_t job;           // and the job's index in the launch
@@ -1235,6 +1237,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
         lc.item_hi = (uint32_t)(base >> 32);
       } else {
         ln.rng = job_seed(S.seed, jid);
+        lc.item_lo = (uint32_t)j;  // the job's index in the launch: its slot in the ordered film's samples
       }
       uint64_t tile = jid % S.T;
       lc.x0 = (int32_t)(tile % S.ntx) * S.tw;  // TileProvider::compute_tile_rect

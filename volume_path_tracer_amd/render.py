@@ -214,6 +214,19 @@ class Integrator:
         capi.check(capi.lib().vpt_gpu_kernel_variant(self.h, C.byref(t), C.byref(r)), "vpt_gpu_kernel_variant")
         return {"has_temperature": bool(t.value), "run_skipping": bool(r.value)}
 
+    def set_film_order(self, mode: int, max_bytes: int = 0) -> None:
+        """capi.VPT_FILM_ORDERED (default: every pixel's samples added in wave order, the reference's film bit
+        for bit; `max_bytes` caps the sample buffer, 0 = auto) or capi.VPT_FILM_ATOMIC (fp32 atomics in
+        completion order).  See include/vpt_gpu.h vpt_gpu_set_film_order."""
+        capi.check(capi.lib().vpt_gpu_set_film_order(self.h, int(mode), int(max_bytes)), "vpt_gpu_set_film_order")
+
+    def film_order_info(self) -> dict:
+        m, b, o, a = C.c_int(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+        capi.check(capi.lib().vpt_gpu_film_order_info(self.h, C.byref(m), C.byref(b), C.byref(o), C.byref(a)),
+                   "vpt_gpu_film_order_info")
+        return {"mode": int(m.value), "buffer_bytes": int(b.value), "ordered_launches": int(o.value),
+                "atomic_launches": int(a.value)}
+
     def set_job_order(self, mode: int) -> None:
         """Scheduling order of whole-wave launches: capi.VPT_ORDER_JID (TileProvider order),
         VPT_ORDER_COST_WAVE_MAJOR, VPT_ORDER_COST_TILE_MAJOR or VPT_ORDER_COST_TAIL (default).
