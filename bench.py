@@ -204,7 +204,10 @@ def dropin_frames(wl, frames: int = 3, timeout_s: int = 300):
             t = subprocess.run(base + [f"out={tmp}/x", "mode=tokens"], capture_output=True, text=True, timeout=60)
         except subprocess.TimeoutExpired:
             t = None
+        first = first_call(wl, base, tmp, timeout_s)
     ms = [float(l.split()[-1]) for l in r.stdout.splitlines() if "render_ms" in l]
+    if not ms:  # (a harness that printed no frame time is recorded, not fatal)
+        return {"error": "no render_ms lines", "stdout_tail": r.stdout[-500:]}
     med = sorted(ms)[len(ms) // 2]
     rec = {"path": "vpt_gpu::drain (include/vpt_run.hpp) behind the restated TileProvider, main.cpp:46-87 headless "
                    "(tests/native/run_gpu_harness), 1 worker thread, 0.2-s progressive film",
@@ -216,6 +219,53 @@ def dropin_frames(wl, frames: int = 3, timeout_s: int = 300):
             parts = line.replace(",", "").split()
             rec["provider_alone_ms"] = float(parts[parts.index("tokens_ms") + 1])
             rec["provider_alone_Mtokens_per_s"] = float(parts[parts.index("M") - 1])
+    rec["first_call"] = first
+    return rec
+
+
+def first_call(wl, base, tmp, timeout_s):
+    """What a reference caller's run() costs: main.cpp renders one frame per process and times the
+    whole vpt::run call ("Rendering complete in N ms", main.cpp:65-84).  A fresh child process runs
+    vpt_gpu::run (include/vpt_run.hpp) with the reference's own argument types -- the volume as NanoGrid<float>
+    bytes, the seed private to the RandomNumberGenerator -- from the scene's num_workers threads (the first
+    drives the GPU, the others return), and reports the call's phases: the HIP runtime's start, the first
+    batch of tokens, the seed recovery (one GPU launch over 2^32 candidates), reading the NanoGrids, the
+    context (flatten + leaf-majorant fix, upload, the rest, the tile-cost pass), and the frame."""
+    import subprocess
+
+    from volume_path_tracer_amd import nvdb
+    from volume_path_tracer_amd.scenes import SynthGrid
+
+    t0 = time.time()
+    dg = SynthGrid(wl.density_kind, wl.grid_n)
+    (Path(tmp) / "density.grid").write_bytes(nvdb.buffer_from_grid(dg.grid(copy=False), "density"))
+    extra = [f"gridbuf={tmp}/density.grid"]
+    if wl.temperature:
+        tg = SynthGrid(2, wl.grid_n)
+        (Path(tmp) / "temperature.grid").write_bytes(nvdb.buffer_from_grid(tg.grid(copy=False), "temperature"))
+        extra.append(f"tempbuf={tmp}/temperature.grid")
+    prep_s = time.time() - t0
+    args = [a for a in base if not a.startswith("threads=")] + extra + [f"out={tmp}/first.f32", "mode=run",
+                                                                         f"threads={wl.cfg.num_workers or 1}"]
+    try:
+        r = subprocess.run(args, capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timeout {timeout_s} s"}
+    if r.returncode != 0:
+        return {"error": r.returncode, "stderr_tail": r.stderr[-500:]}
+    rec = {"path": "vpt_gpu::run (include/vpt_run.hpp) in a fresh process, main.cpp:63-68's call with the reference's "
+                   "types (tests/native/run_gpu_harness mode=run): NanoGrid<float> bytes, private seed",
+           "worker_threads": wl.cfg.num_workers, "grid_bytes_written_s": round(prep_s, 2)}
+    for line in r.stdout.splitlines():
+        if "phases" in line:
+            for kv in line.split("phases", 1)[1].split():
+                k, _, v = kv.partition("=")
+                rec[k] = float(v) if "." in v else int(v)
+    W, H = wl.cfg.width, wl.cfg.height
+    film = __import__("numpy").fromfile(f"{tmp}/first.f32", "float32").reshape(H, W, 4)
+    rec["film_counts_exact"] = bool((film[..., 3] == wl.spp).all())
+    rec["note"] = ("total_ms = the whole run() call as main.cpp times it; the grid load itself (NanoVDB file read, "
+                   "Volume ctor) happens before it in main.cpp:40-41 and is not in it")
     return rec
 
 

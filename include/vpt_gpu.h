@@ -402,9 +402,15 @@ int vpt_gpu_feed_destroy(vpt_gpu_feed* feed);
 /* Jobs pushed and not yet taken by a lane -- an estimate: the lanes report every 1 024th job they take into
  * 4 words of the pinned block (their posted writes land in any order; the largest counts); before the launch
  * every pushed job counts.  It can read high, never for long while the lanes wait: a wavefront that finds
- * every published job taken stores the job count it saw, and a count >= the published one reads as 0.
+ * every published job taken stores the job count it saw (again every ~5 ms while it waits), and a count >= the
+ * published one reads as 0; hints that have not moved for 10 ms read as 0 too.
  * Cheap: a read of one cache line. */
 int vpt_gpu_feed_backlog(vpt_gpu_feed* feed, uint64_t* backlog);
+/* Test hook for the backlog estimate's words (tests/test_gpu_integration.py): op 0 reads the "waiting" word into
+ * *value, op 1 writes *value into it, op 2 writes *value into every reservation hint (and the host's view of
+ * them) -- a stale value landing last, which waiting wavefronts overwrite within ~5 ms (they store the count they
+ * see every 2^19 ticks of s_memrealtime) and the estimate ignores after 10 ms without a new hint. */
+int vpt_gpu_feed_debug(vpt_gpu_feed* feed, int op, uint64_t* value);
 /* A staged feed renders into film_device (NULL = the context's own film), which must be zero, on hip_stream
  * (NULL = a stream of the feed's own), and counts the jobs it completes per tile; its film reaches the host through the copy engines, which run beside a launch
  * that holds every CU (r05), so nothing in its life waits for CUs another feed's launch holds.
@@ -412,9 +418,13 @@ int vpt_gpu_feed_backlog(vpt_gpu_feed* feed, uint64_t* backlog);
  *     floats, the reference's [H][W][4] layout) what the launch has rendered since the previous snapshot --
  *     the completed jobs' sample counts and the film's radiance as copied (~2 ms for a 1080p film).  A
  *     progressive film (main.cpp:101-132's 5-FPS window): every snapshot's additions telescope to the final
- *     film.  The caller serialises writers of film_host.
- *   vpt_gpu_feed_collect -- closes if needed, waits for the launch, adds the rest (exact: the whole film
- *     then equals the launch's), clears film_device and frees the feed like destroy.
+ *     film (to fp32 rounding, see collect).  The caller serialises writers of film_host.
+ *   vpt_gpu_feed_collect -- closes if needed, waits for the launch, adds the rest, clears film_device and
+ *     frees the feed like destroy.  The sample counts then end exact (whole jobs per tile); the radiance ends
+ *     equal to the launch's film within fp32 rounding (each snapshot adds a rounded difference, and several
+ *     drivers may share film_host).  An intermediate snapshot's radiance includes samples of jobs still
+ *     running while their counts arrive only when each job ends, so a progressive frame reads slightly bright
+ *     until its jobs complete.
  * vpt_gpu_feed_prepare allocates a feed's memory (the ring, and with staged != 0 the copy buffers) into the
  * context's pool ahead of the first open, e.g. right after vpt_gpu_create, so that no allocation runs while a
  * launch holds the device. */

@@ -22,13 +22,14 @@
 //   * RandomNumberGenerator       its seed: rng.seed() when the type has one; the reference keeps it
 //                                 private (random.hpp:86-115), so otherwise the u32 seed whose job-0
 //                                 stream starts with the same two outputs is found by search (2^32
-//                                 candidates of hash + pcg32_fast, 1-3 s on 8-16 threads, once per
-//                                 process and stream start)
-// Threads: main.cpp starts num_workers threads that all call run().  A caller claims a free GPU for
-// the length of its run() (one context per device, one host thread per context); callers that find
-// every device taken return at once, and the device threads drain the provider.  The context is
-// built only after the caller's first batch of tokens, so a late caller that finds the provider
-// drained returns without building one.  Errors: the reference exits
+//                                 candidates of hash + pcg32_fast in one GPU launch, vpt_gpu_find_seeds:
+//                                 a few ms; once per process and stream start)
+// Threads: main.cpp starts num_workers threads that all call run().  The first caller drives every GPU
+// of the process from one token-taking thread (drain_devices: a context and a feed pipeline per GPU, each
+// batch of tokens routed to the GPU that needs it); callers that find it driving return at once -- the
+// provider's one job counter makes a second taker slower, not faster (r05: 13-16x per token).  The
+// contexts are built only after the caller's first batch of tokens, so a late caller that finds the
+// provider drained returns without building one.  Errors: the reference exits
 // through vptFATAL (exit(1), logging.hpp:16); run() prints vpt_last_error() and exits with 1 too
 // (run_checked returns the code instead).
 #pragma once
@@ -43,6 +44,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <utility>
@@ -216,20 +218,71 @@ class FeedPipeline {
     taker_cv_.notify_all();
   }
   int push(const uint64_t* ids, uint64_t n) { return n ? vpt_gpu_feed_push(feed_, ids, n) : VPT_OK; }
-  // ids[0..n) costliest tile class first (a counting sort; the order taken within a class: consecutive items
-  // are different tiles of one wave), into sorted_.
-  const uint64_t* by_cost(const uint64_t* ids, uint64_t n) {
+  // The jobs taken and not yet pushed, as contiguous (jid, count) runs in the order taken (the pusher's): the
+  // takers hand over runs (a batch of tokens is one or two), and the pusher expands them into job ids only as
+  // it pushes them -- one pass over the ids, no division per job (r06: the pusher, not the taker, set the
+  // drop-in's pace once a frame's jobs outran what it could expand, sort and push per second).
+  struct Held {
+    JobRuns runs;
+    size_t head = 0;
+    uint64_t n = 0;
+    void add(const JobRuns& rs) {
+      for (const auto& r : rs) {
+        if (!r.second) continue;
+        if (head < runs.size() && runs.back().first + runs.back().second == r.first)
+          runs.back().second += r.second;
+        else
+          runs.push_back(r);
+        n += r.second;
+      }
+    }
+    // The first (up to) k jobs into out; their count.
+    uint64_t take(uint64_t k, JobRuns& out) {
+      out.clear();
+      uint64_t got = 0;
+      while (got < k && head < runs.size()) {
+        auto& r = runs[head];
+        const uint64_t c = std::min(k - got, r.second);
+        out.emplace_back(r.first, c);
+        r.first += c;
+        r.second -= c;
+        got += c;
+        if (!r.second) ++head;
+      }
+      n -= got;
+      if (head == runs.size()) {
+        runs.clear();
+        head = 0;
+      } else if (head > 4096 && head * 2 > runs.size()) {
+        runs.erase(runs.begin(), runs.begin() + (ptrdiff_t)head);
+        head = 0;
+      }
+      return got;
+    }
+  };
+  // A chunk's n jobs into ids_: in the order taken, or costliest tile class first (a counting sort; the order
+  // taken within a class: consecutive items are different tiles of one wave).  Each job's tile is stepped along
+  // its run (jid + 1 is tile + 1, mod T).
+  const uint64_t* emit(const JobRuns& chunk, uint64_t n, bool sort) {
+    ids_.resize(n);
+    uint64_t* out = ids_.data();
+    if (!sort) {
+      for (const auto& r : chunk)
+        for (uint64_t k = 0; k < r.second; ++k) *out++ = r.first + k;
+      return ids_.data();
+    }
     const uint64_t T = cls_.size();
     uint64_t start[kClasses + 1] = {};
-    for (uint64_t i = 0; i < n; ++i) ++start[cls_[ids[i] % T] + 1];
+    for (const auto& r : chunk)
+      for (uint64_t k = 0, t = r.first % T; k < r.second; ++k, t = t + 1 == T ? 0 : t + 1) ++start[cls_[t] + 1];
     for (int c = 0; c < kClasses; ++c) start[c + 1] += start[c];
-    sorted_.resize(n);
-    for (uint64_t i = 0; i < n; ++i) sorted_[start[cls_[ids[i] % T]]++] = ids[i];
-    return sorted_.data();
+    for (const auto& r : chunk)
+      for (uint64_t k = 0, t = r.first % T; k < r.second; ++k, t = t + 1 == T ? 0 : t + 1) out[start[cls_[t]]++] = r.first + k;
+    return ids_.data();
   }
   // Pushes held jobs, oldest first, while the feed's backlog is below its mark -- and, until the launch has
   // started (it starts once a lane's worth of jobs is pushed, vpt_gpu_feed_push), below the lanes.
-  int top_up(std::vector<uint64_t>& hold, size_t& head) {
+  int top_up(Held& hold) {
     uint64_t b = 0;
     if (int rc = vpt_gpu_feed_backlog(feed_, &b)) return rc;
     struct Seen {  // (the backlog after this call's pushes, for pending())
@@ -238,30 +291,20 @@ class FeedPipeline {
       ~Seen() { to.store(b, std::memory_order_relaxed); }
     } seen{backlog_seen_, b};
     const uint64_t mark = pushed_ < lanes_ ? std::max(backlog_, lanes_) : backlog_;
-    while (head < hold.size() && b < mark) {
-      const uint64_t n = std::min<uint64_t>(kChunk, hold.size() - head);
-      const uint64_t* ids = hold.data() + head;
+    while (hold.n > 0 && b < mark) {
       // (the launch's first lane's worth goes unsorted: every lane takes one of those jobs at once, so their order
       // changes nothing, and sorting them would delay the launch -- ~3 ms of C3's 458 752)
       const bool sort = cost_chunks_ && !cls_.empty() && pushed_ >= lanes_;
-      if (int rc = push(sort ? by_cost(ids, n) : ids, n)) return rc;
-      head += n;
+      const uint64_t n = hold.take(kChunk, chunk_);
+      if (int rc = push(emit(chunk_, n, sort), n)) return rc;
       b += n;
       pushed_ += n;
-    }
-    if (head == hold.size()) {
-      hold.clear();
-      head = 0;
-    } else if (head > (1u << 20) && head * 2 > hold.size()) {
-      hold.erase(hold.begin(), hold.begin() + (ptrdiff_t)head);
-      head = 0;
     }
     return VPT_OK;
   }
   void pusher_main() {
     (void)vpt_gpu_bind_thread_near(ctx_, nullptr);  // the ring is in the GPU's node's memory
-    std::vector<uint64_t> hold;  // taken, not pushed: hold[head..] in the order taken
-    size_t head = 0;
+    Held hold;  // taken, not pushed, in the order taken
     auto last_push = std::chrono::steady_clock::now();
     JobRuns batch;
     for (;;) {
@@ -277,35 +320,30 @@ class FeedPipeline {
       // nothing new: the lanes take jobs meanwhile (the backlog check below); a timed condition-variable wait
       // would do the same, but ThreadSanitizer (gcc 11) does not model pthread_cond_clockwait
       if (batch.empty() && !last) std::this_thread::sleep_for(std::chrono::microseconds(50));
-      for (const auto& r : batch)
-        for (uint64_t i = 0; i < r.second; ++i) hold.push_back(r.first + i);
+      hold.add(batch);
       batch.clear();
       if (last) break;
-      const size_t before = hold.size() - head;
-      const uint64_t pushed_before = pushed_;
-      if (int rc = top_up(hold, head)) return fail(rc);
+      const uint64_t before = hold.n, pushed_before = pushed_;
+      if (int rc = top_up(hold)) return fail(rc);
       if (pushed_ != pushed_before) {
         last_push = std::chrono::steady_clock::now();
       } else if (std::chrono::steady_clock::now() - last_push > std::chrono::seconds(1)) {
-        detail::drain_trace("nopush", (double)(hold.size() - head), (double)pushed_);  // (diagnostics)
+        detail::drain_trace("nopush", (double)hold.n, (double)pushed_);  // (diagnostics)
         last_push = std::chrono::steady_clock::now();
       }
-      if (hold.size() - head != before) {
+      if (hold.n != before) {
         std::lock_guard<std::mutex> l(mu_);
-        held_ = hold.size() - head;
+        held_ = hold.n;
         taker_cv_.notify_all();
       }
     }
     // The provider is dry: the held jobs, costliest tile class first (jid order within a class: consecutive
     // items are different tiles of one wave), then the end of the feed.
-    std::vector<uint64_t> rest(hold.begin() + (ptrdiff_t)head, hold.end());
-    detail::drain_trace("final_hold", (double)rest.size(), (double)pushed_);
-    if (cost_tail_ && !cls_.empty() && !rest.empty()) {
-      by_cost(rest.data(), rest.size());
-      rest.swap(sorted_);
-    }
-    for (size_t i = 0; i < rest.size(); i += kChunk)
-      if (int rc = push(rest.data() + i, std::min<uint64_t>(kChunk, rest.size() - i))) return fail(rc);
+    detail::drain_trace("final_hold", (double)hold.n, (double)pushed_);
+    const uint64_t n = hold.take(hold.n, chunk_);
+    const uint64_t* rest = emit(chunk_, n, cost_tail_ && !cls_.empty());
+    for (uint64_t i = 0; i < n; i += kChunk)
+      if (int rc = push(rest + i, std::min<uint64_t>(kChunk, n - i))) return fail(rc);
     if (int rc = vpt_gpu_feed_close(feed_)) return fail(rc);
     detail::drain_trace("closed");
     std::lock_guard<std::mutex> l(mu_);
@@ -351,7 +389,8 @@ class FeedPipeline {
   vpt_gpu_feed* feed_ = nullptr;
   std::vector<uint8_t> cls_;  // per tile: cost class (0 = costliest)
   bool cost_tail_ = true, cost_chunks_ = true;
-  std::vector<uint64_t> sorted_;  // (the pusher's)
+  std::vector<uint64_t> ids_;  // (the pusher's: a push's job ids)
+  JobRuns chunk_;              // (the pusher's: a push's runs)
   std::thread pusher_, film_;
   std::mutex mu_;  // queue_, queued_, held_, no_more_, err_
   std::condition_variable taker_cv_;
@@ -374,7 +413,7 @@ struct Helpers {
   std::mutex mu;
   std::condition_variable cv;
   std::vector<FeedPipeline*> pipes;  // pipelines that accept helpers
-  int drivers = 0;                   // threads that claimed a device and have not finished
+  int drivers = 0;                   // driving threads that have not finished (their callers count them)
   size_t next = 0;
   static Helpers& get() {
     static Helpers h;
@@ -430,6 +469,74 @@ inline int render_runs(vpt_gpu_ctx* ctx, const JobRuns& runs, float* film_host) 
   std::lock_guard<std::mutex> lock(film_mutex());
   return vpt_gpu_film_flush_to_host(ctx, nullptr, film_host);
 }
+// The same on several GPUs: the runs cut into contiguous parts of about equal job counts, one per context, all
+// launched before any is waited for (C2's 262 144 jobs: a launch per GPU of 1 / N of them).
+inline int render_runs_split(const std::vector<vpt_gpu_ctx*>& ctxs, const JobRuns& runs, float* film_host) {
+  uint64_t total = 0;
+  for (const auto& r : runs) total += r.second;
+  const uint64_t n = ctxs.size(), per = (total + n - 1) / n;
+  std::vector<JobRuns> parts(n);
+  size_t k = 0;
+  uint64_t in_part = 0;
+  for (auto r : runs)
+    while (r.second > 0) {
+      const uint64_t c = std::min(r.second, per - in_part);
+      parts[k].emplace_back(r.first, c);
+      r.first += c;
+      r.second -= c;
+      if ((in_part += c) == per && k + 1 < n) {
+        ++k;
+        in_part = 0;
+      }
+    }
+  for (size_t i = 0; i < n; ++i)
+    for (const auto& r : parts[i])
+      if (int rc = vpt_gpu_render_jobs(ctxs[i], r.first, r.second, nullptr, nullptr)) return rc;
+  for (size_t i = 0; i < n; ++i) {
+    if (int rc = vpt_gpu_sync(ctxs[i])) return rc;
+    std::lock_guard<std::mutex> lock(film_mutex());
+    if (int rc = vpt_gpu_film_flush_to_host(ctxs[i], nullptr, film_host)) return rc;
+  }
+  return VPT_OK;
+}
+// The jobs taken before a pipeline starts (`first`, then up to the launch's lanes -- opt.direct_below): true
+// when the provider ran dry before that, a small frame (rendered by jid-range launches instead of a feed).
+// A provider with the reference's progress() (percent of its jobs handed out, tile_provider.hpp:72-74) tells a
+// large frame after a few batches: the pipeline then starts at once, its pusher filling the ring while the
+// rest of the launch's first lane's worth is taken.  (Starting the launch itself earlier than a lane's worth
+// was measured 5-15x slower: tools/experiments/r05_wave_cas_early_launch.patch.)
+template <class Provider>
+int take_head(vpt_gpu_ctx* ctx, Provider& tp, uint64_t batch_jobs, const DrainOptions& opt, const JobRuns* first,
+              JobRuns& head, bool& small) {
+  small = false;
+  head.clear();
+  int blocks = 0, threads = 0;
+  if (int rc = vpt_gpu_launch_info(ctx, &blocks, &threads)) return rc;
+  const uint64_t direct = opt.direct_below ? opt.direct_below : (uint64_t)blocks * (uint64_t)threads;
+  uint64_t have = 0;
+  if (first) {
+    head = *first;
+    for (const auto& r : head) have += r.second;
+  }
+  const uint64_t probe = std::min<uint64_t>(direct, kDirectProbe);
+  JobRuns runs;
+  while (have < direct) {
+    const uint64_t n = take_jobs(tp, std::min<uint64_t>(std::max<uint64_t>(1, batch_jobs), direct - have), runs, [](auto&) {});
+    if (n == 0) {  // the provider is dry: a small frame
+      small = true;
+      return VPT_OK;
+    }
+    append_runs(head, runs);
+    have += n;
+    if constexpr (requires { tp.progress(); }) {
+      if (have >= probe && have < direct) {
+        const uint64_t pct = (uint64_t)tp.progress();  // floor: the frame has >= have * 100 / (pct + 1) jobs
+        if (pct == 0 || have * 100 / (pct + 1) >= direct) break;
+      }
+    }
+  }
+  return VPT_OK;
+}
 }  // namespace detail
 
 template <class Provider>
@@ -437,37 +544,17 @@ int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs,
           const JobRuns* first = nullptr, bool share = false) {
   JobRuns head;  // the jobs taken before the pipeline starts
   if (!share) {  // (a shared pipeline takes helpers' jobs: it always runs)
-    int blocks = 0, threads = 0;
-    if (int rc = vpt_gpu_launch_info(ctx, &blocks, &threads)) return rc;
-    const uint64_t direct = opt.direct_below ? opt.direct_below : (uint64_t)blocks * (uint64_t)threads;
-    uint64_t have = 0;
-    if (first) {
-      head = *first;
-      for (const auto& r : head) have += r.second;
-    }
-    // A provider with the reference's progress() (percent of its jobs handed out, tile_provider.hpp:72-74)
-    // tells a large frame after a few batches: the pipeline then starts at once, its pusher filling the ring
-    // while the rest of the launch's first lane's worth is taken.  (Starting the launch itself earlier than a
-    // lane's worth was measured 5-15x slower: tools/experiments/r05_wave_cas_early_launch.patch.)
-    const uint64_t probe = std::min<uint64_t>(direct, kDirectProbe);
-    JobRuns runs;
-    while (have < direct) {
-      const uint64_t n = take_jobs(tp, std::min<uint64_t>(std::max<uint64_t>(1, batch_jobs), direct - have), runs, [](auto&) {});
-      if (n == 0) return detail::render_runs(ctx, head, film_host);  // the provider is dry: a small frame
-      detail::append_runs(head, runs);
-      have += n;
-      if constexpr (requires { tp.progress(); }) {
-        if (have >= probe && have < direct) {
-          const uint64_t pct = (uint64_t)tp.progress();  // floor: the frame has >= have * 100 / (pct + 1) jobs
-          if (pct == 0 || have * 100 / (pct + 1) >= direct) break;
-        }
-      }
-    }
+    bool small = false;
+    detail::drain_trace("drain");
+    if (int rc = detail::take_head(ctx, tp, batch_jobs, opt, first, head, small)) return rc;
+    if (small) return detail::render_runs(ctx, head, film_host);
     first = &head;
   }
+  detail::drain_trace("head_taken");
   FeedPipeline pipe(ctx);
   int rc = pipe.start(film_host, opt);
   if (rc == VPT_OK && first) rc = pipe.add(*first);
+  detail::drain_trace("started");
   detail::Helpers& hub = detail::Helpers::get();
   if (share && rc == VPT_OK) {
     std::lock_guard<std::mutex> l(hub.mu);
@@ -513,6 +600,59 @@ int help(Provider& tp, uint64_t batch_jobs) {
   return rc;
 }
 
+// One taker for every GPU of the process.  The reference's caller starts num_workers threads that
+// all call run() on one provider (main.cpp:63-68), and every next() is a fetch_add on one job counter plus a
+// seq_cst token store and notify_all (tile_provider.cpp:28, tile_provider.hpp:22-27): on the GPU box's EPYC one
+// thread takes 64-67 M tokens/s, two threads together 3.8-5.3 M/s.  So the drop-in takes tokens on ONE thread
+// and feeds every GPU from it: one FeedPipeline (staged feed, pusher and film threads) per context, each batch
+// routed to the GPU that needs it -- first to each GPU in turn until its launch has a lane's worth (a feed's
+// launch starts then), afterwards to the GPU with the fewest jobs given and not yet started (FeedPipeline::
+// pending).  The provider's token rate is the frame's floor: C3's 8.3 M tokens take 124 ms on one thread, so
+// the 8-GPU drop-in frame is ~125-145 ms however fast the GPUs are; north_star's >= 6x at 8 GPUs
+// is reachable through the C ABI's jid ranges (distributed.py, bench.py), not through a TileProvider.
+// One context: exactly drain().  Small frames (the provider dry before a lane's worth): jid-range launches
+// split across the GPUs.
+template <class Provider>
+int drain_devices(const std::vector<vpt_gpu_ctx*>& ctxs, Provider& tp, float* film_host, uint64_t batch_jobs,
+                  const DrainOptions& opt = {}, const JobRuns* first = nullptr) {
+  if (ctxs.empty()) return VPT_E_INVALID;
+  if (ctxs.size() == 1) return drain(ctxs[0], tp, film_host, batch_jobs, opt, first);
+  JobRuns head;
+  bool small = false;
+  if (int rc = detail::take_head(ctxs[0], tp, batch_jobs, opt, first, head, small)) return rc;
+  if (small) return detail::render_runs_split(ctxs, head, film_host);
+  std::vector<std::unique_ptr<FeedPipeline>> pipes;
+  int rc = VPT_OK;
+  for (vpt_gpu_ctx* c : ctxs) {
+    pipes.push_back(std::make_unique<FeedPipeline>(c));
+    if (rc == VPT_OK) rc = pipes.back()->start(film_host, opt);
+  }
+  if (rc == VPT_OK) rc = pipes[0]->add(head);  // a lane's worth: the first GPU's launch starts now
+  auto route = [&]() -> size_t {
+    for (size_t i = 0; i < pipes.size(); ++i)
+      if (pipes[i]->added() < pipes[i]->lanes()) return i;
+    size_t best = 0;
+    uint64_t least = ~0ULL;
+    for (size_t i = 0; i < pipes.size(); ++i)
+      if (const uint64_t p = pipes[i]->pending(); p < least) {
+        least = p;
+        best = i;
+      }
+    return best;
+  };
+  JobRuns runs;
+  uint64_t taken = 0;
+  for (uint64_t n; rc == VPT_OK && (n = take_jobs(tp, std::max<uint64_t>(1, batch_jobs), runs, [](auto&) {}));) {
+    taken += n;
+    rc = pipes[route()]->add(runs);
+  }
+  detail::drain_trace("taker_done", (double)taken);
+  for (auto& p : pipes) p->end_input();  // every GPU's last jobs go out before any launch is waited for
+  for (auto& p : pipes)
+    if (const int frc = p->finish(); rc == VPT_OK) rc = frc;
+  return rc;
+}
+
 namespace detail {
 
 // hash(seed, jid) (include/vpt/hash.hpp:20-67) and pcg32_fast's output (pcg_random.hpp, xsh_rs)
@@ -531,8 +671,19 @@ inline uint64_t job_state(uint64_t seed, uint64_t jid) {
 inline uint32_t pcg_out(uint64_t s) { return (uint32_t)((s ^ (s >> 22)) >> (22 + (uint32_t)(s >> 61))); }
 constexpr uint64_t kPcgMult = 6364136223846793005ULL;
 
-// The u32 seeds whose job-0 stream starts with outputs (a, b); normally exactly one.
-inline std::vector<uint32_t> seeds_for(uint32_t a, uint32_t b) {
+// The u32 seeds whose job-0 stream starts with outputs (a, b); normally exactly one.  device >= 0: one launch
+// over all 2^32 candidates (vpt_gpu_find_seeds, a few ms); device < 0 (no GPU, the host tests): host threads,
+// 1-3 s.
+inline int seeds_for(uint32_t a, uint32_t b, int device, std::vector<uint32_t>& out) {
+  out.clear();
+  if (device >= 0) {
+    uint32_t found[8];
+    int n = 0;
+    if (int rc = vpt_gpu_find_seeds(device, a, b, found, 8, &n)) return rc;
+    out.assign(found, found + std::min(n, 8));
+    if (n > 8) out.resize(9, 0);  // (more than we keep: ambiguous anyway)
+    return VPT_OK;
+  }
   const unsigned n = std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
   std::vector<std::vector<uint32_t>> found(n);
   std::vector<std::thread> pool;
@@ -545,13 +696,12 @@ inline std::vector<uint32_t> seeds_for(uint32_t a, uint32_t b) {
       }
     });
   for (auto& th : pool) th.join();
-  std::vector<uint32_t> out;
   for (auto& f : found) out.insert(out.end(), f.begin(), f.end());
-  return out;
+  return VPT_OK;
 }
 
 template <class RNG>
-int rng_seed(const RNG& rng, uint32_t& seed) {
+int rng_seed(const RNG& rng, uint32_t& seed, int device = -1) {
   if constexpr (requires { rng.seed(); }) {
     seed = (uint32_t)rng.seed();
     return VPT_OK;
@@ -563,54 +713,41 @@ int rng_seed(const RNG& rng, uint32_t& seed) {
     static std::map<std::pair<uint32_t, uint32_t>, std::vector<uint32_t>> cache;
     std::lock_guard<std::mutex> lock(mu);
     auto it = cache.find({a, b});
-    if (it == cache.end()) it = cache.emplace(std::make_pair(a, b), seeds_for(a, b)).first;
+    if (it == cache.end()) {
+      std::vector<uint32_t> found;
+      if (int rc = seeds_for(a, b, device, found)) return rc;
+      it = cache.emplace(std::make_pair(a, b), std::move(found)).first;
+    }
     if (it->second.size() != 1) return VPT_E_STATE;
     seed = it->second[0];
     return VPT_OK;
   }
 }
 
-// One GPU per worker thread: a caller claims a free device for the length of its run() (-1: no HIP
-// device, -2: every device is driven by another worker).
-struct Devices {
-  std::mutex mu;
-  std::vector<bool> busy;
-  static Devices& get() {
-    static Devices d;
-    return d;
+// The process's one driving run() call: the first caller takes every token and drives every GPU
+// (drain_devices); callers that find it taken return at once, as the reference's surplus workers would find the
+// provider dry.  Released when that call returns (a later frame's run() may lead).
+struct Leader {
+  static std::mutex& mu() {
+    static std::mutex m;
+    return m;
   }
-};
-inline int claim_device() {
-  int n = 0;
-  if (vpt_gpu_device_count(&n) || n <= 0) return -1;
-  Devices& D = Devices::get();
-  std::lock_guard<std::mutex> lock(D.mu);
-  D.busy.resize((size_t)n, false);
-  for (int d = 0; d < n; ++d)
-    if (!D.busy[d]) {
-      D.busy[d] = true;
-      // counted as a driver before any thread can find the devices taken (and help, or leave if none drives)
-      std::lock_guard<std::mutex> l(Helpers::get().mu);
-      ++Helpers::get().drivers;
-      return d;
-    }
-  return -2;
-}
-inline void release_device(int d) {
-  Devices& D = Devices::get();
-  std::lock_guard<std::mutex> lock(D.mu);
-  D.busy[(size_t)d] = false;
-}
-struct DeviceClaim {  // a driving thread counts in Helpers::drivers from its claim to its return
-  int device = claim_device();
-  ~DeviceClaim() {
-    if (device < 0) return;
-    release_device(device);
-    Helpers& h = Helpers::get();
-    std::lock_guard<std::mutex> l(h.mu);
-    --h.drivers;
-    h.cv.notify_all();
+  static bool& busy() {
+    static bool b = false;
+    return b;
   }
+  bool leads = false;
+  Leader() {
+    std::lock_guard<std::mutex> l(mu());
+    if (!busy()) busy() = leads = true;
+  }
+  ~Leader() {
+    if (!leads) return;
+    std::lock_guard<std::mutex> l(mu());
+    busy() = false;
+  }
+  Leader(const Leader&) = delete;
+  Leader& operator=(const Leader&) = delete;
 };
 
 template <class V3>
@@ -647,22 +784,56 @@ struct OwnedDesc {
   }
 };
 
+// VPT_DEVICES=n: use at most n of the process's HIP devices (A/B runs); default all of them.
+inline int device_limit(int n) {
+  const char* e = std::getenv("VPT_DEVICES");
+  return e && std::atoi(e) > 0 ? std::min(n, std::atoi(e)) : n;
+}
+
 }  // namespace detail
+
+// What the last run() that drove the GPUs spent where (ms), as main.cpp:65-84 times the whole call -- for
+// reports (the bench's `first_call`).  Written by that call's thread; read after it has returned.
+struct RunPhases {
+  int devices = 0;
+  double hip_ms = 0;          // the HIP runtime's start (the process's first HIP call: the device count)
+  double first_batch_ms = 0;  // the first batch of tokens (the tile size is read off it)
+  double seed_ms = 0;         // the RandomNumberGenerator's private seed, recovered on the GPU
+  double nanogrid_ms = 0;     // the NanoGrid<float>s read into grid descriptions (vpt_grid_from_nanovdb)
+  double contexts_ms = 0;     // vpt_gpu_create + feed memory + tile costs on every GPU (in parallel)
+  double setup_ms[5] = {};    // the first GPU's share of that: flatten + majorant fix, upload, the rest, tile costs, bind
+  double frame_ms = 0;        // drain_devices: the frame itself
+  double total_ms = 0;        // the whole run() call
+};
+inline RunPhases& run_phases() {
+  static RunPhases p;
+  return p;
+}
 
 // vpt::run with the reference's signature; returns VPT_OK or an error code (see run()).
 template <class WorkerParameters, class Volume, class Camera, class TileProvider, class Image, class RNG>
 int run_checked(const WorkerParameters& params, const Volume& vol, const Camera& camera, TileProvider& tp, Image& film,
                 RNG rng, uint64_t first_batch = 4096) {
-  const detail::DeviceClaim claim;
-  const int device = claim.device;
-  if (device == -1) {
+  const detail::Leader lead;
+  // Another worker thread drives every GPU and takes every token: return (taking tokens for it was measured
+  // 13-16x slower per token -- the provider's one job counter -- r05, vpt_run.hpp Helpers).
+  if (!lead.leads) return VPT_OK;
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  auto t = t0;
+  auto lap = [&](double& into) {
+    const auto now = clk::now();
+    into = std::chrono::duration<double, std::milli>(now - t).count();
+    t = now;
+  };
+  RunPhases ph;
+  int ndev = 0;
+  if (vpt_gpu_device_count(&ndev) || ndev <= 0) {
     std::fprintf(stderr, "vpt_gpu::run: no HIP device (the integrator has no CPU fallback)\n");
     return VPT_E_HIP;
   }
-  // Another worker thread drives each GPU: return (as r03).  Taking tokens for the drivers (help()) was
-  // measured slower, not faster: with 3 helpers the C3 drain took 4 265 ms instead of 456, C4 1 682 instead
-  // of 316 -- every token is a next() on the one provider, and contended, those calls cost more than they add.
-  if (device < 0) return VPT_OK;
+  ndev = detail::device_limit(ndev);
+  lap(ph.hip_ms);
 
   const auto size = film.size();
   const int64_t W = (int64_t)size.x(), H = (int64_t)size.y();
@@ -670,25 +841,26 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   // last column / row), then every rect must match the jid -> (tile, rect) mapping it implies.
   JobRuns runs;
   detail::TokenRects rects;
-  const uint64_t taken = take_jobs(tp, first_batch, runs, [&](auto& t) {
-    const auto r = t.compute_rect();
-    rects.push_back({(uint64_t)t.jid(), {(int64_t)r.start.x(), (int64_t)r.start.y(), (int64_t)r.size.x(), (int64_t)r.size.y()}});
+  const uint64_t taken = take_jobs(tp, first_batch, runs, [&](auto& tok) {
+    const auto r = tok.compute_rect();
+    rects.push_back({(uint64_t)tok.jid(), {(int64_t)r.start.x(), (int64_t)r.start.y(), (int64_t)r.size.x(), (int64_t)r.size.y()}});
   });
-  if (taken == 0) return VPT_OK;
+  if (taken == 0) return VPT_OK;  // the provider is dry: nothing to build
   int64_t tw = 0, th = 0;
   if (!detail::tile_size_from_rects(rects, W, H, tw, th)) {
     std::fprintf(stderr, "vpt_gpu::run: token rects do not follow one tile size (%lld x %lld)\n", (long long)tw,
                  (long long)th);
     return VPT_E_STATE;
   }
-  const uint64_t T = (uint64_t)(((W + tw - 1) / tw) * ((H + th - 1) / th));
+  lap(ph.first_batch_ms);
 
   vpt_configuration cfg;
   std::memset(&cfg, 0, sizeof cfg);
-  if (int rc = detail::rng_seed(rng, cfg.seed)) {
+  if (int rc = detail::rng_seed(rng, cfg.seed, 0)) {
     std::fprintf(stderr, "vpt_gpu::run: the RandomNumberGenerator's seed could not be determined\n");
     return rc;
   }
+  lap(ph.seed_ms);
   cfg.num_waves = 1;  // the provider decides which waves run; the context renders any job id
   cfg.num_workers = 1;
   cfg.output_size[0] = W;
@@ -721,19 +893,46 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   if (int rc = vpt_grid_from_nanovdb(&grids.density(), (size_t)grids.density().gridSize(), &dens.d)) return rc;
   if (grids.has_temperature())
     if (int rc = vpt_grid_from_nanovdb(&grids.temperature(), (size_t)grids.temperature().gridSize(), &temp.d)) return rc;
-  vpt_gpu_ctx* ctx = nullptr;
-  if (int rc = vpt_gpu_create(&cfg, dens.d, temp.d, nullptr, device, &ctx)) return rc;
-  struct Ctx {
-    vpt_gpu_ctx* c;
-    ~Ctx() { vpt_gpu_destroy(c); }
-  } guard{ctx};
-  // setup, like the grid upload: the feed's pinned ring and copy buffers, and the tile costs of its cost tail
-  if (int rc = vpt_gpu_feed_prepare(ctx, 0, 1)) return rc;
-  if (int rc = vpt_gpu_tile_costs(ctx, nullptr, nullptr)) return rc;
+  lap(ph.nanogrid_ms);
+
+  // A context per GPU, built in parallel (each flattens and uploads the grids): the feed's pinned ring and copy
+  // buffers and the tile costs of its cost tail are setup too, like the grid upload.
+  std::vector<vpt_gpu_ctx*> ctxs((size_t)ndev, nullptr);
+  struct Ctxs {
+    std::vector<vpt_gpu_ctx*>& c;
+    ~Ctxs() {
+      for (auto* x : c)
+        if (x) vpt_gpu_destroy(x);
+    }
+  } guard{ctxs};
+  std::vector<int> crc((size_t)ndev, VPT_OK);
+  auto build = [&](int d) {
+    int rc = vpt_gpu_create(&cfg, dens.d, temp.d, nullptr, d, &ctxs[(size_t)d]);
+    if (rc == VPT_OK) rc = vpt_gpu_feed_prepare(ctxs[(size_t)d], 0, 1);
+    if (rc == VPT_OK) rc = vpt_gpu_tile_costs(ctxs[(size_t)d], nullptr, nullptr);
+    if (rc != VPT_OK)  // (vpt_last_error is per thread: say it here)
+      std::fprintf(stderr, "vpt_gpu::run: device %d: %s\n", d, vpt_last_error());
+    crc[(size_t)d] = rc;
+  };
+  if (ndev == 1) {
+    build(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (int d = 0; d < ndev; ++d) pool.emplace_back(build, d);
+    for (auto& th2 : pool) th2.join();
+  }
+  for (int rc : crc)
+    if (rc) return rc;
+  lap(ph.contexts_ms);
+  (void)vpt_gpu_setup_timings(ctxs[0], ph.setup_ms, 5);
+  ph.devices = ndev;
   float* film_host = reinterpret_cast<float*>(film.data().data());  // H x W x (X, Y, Z, W)
   // the first batch is queued first; then 4096 tokens per batch (a token is one 8x8 job: 64 samples)
-  (void)T;
-  return drain(ctx, tp, film_host, 4096, DrainOptions{}, &runs);
+  const int rc = drain_devices(ctxs, tp, film_host, 4096, DrainOptions{}, &runs);
+  lap(ph.frame_ms);
+  ph.total_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  run_phases() = ph;
+  return rc;
 }
 
 template <class WorkerParameters, class Volume, class Camera, class TileProvider, class Image, class RNG>

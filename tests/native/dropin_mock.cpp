@@ -8,7 +8,15 @@
 // that cannot end that way within 5 s is reported as a deadlock.
 //
 //   dropin_mock drivers=<n> helpers=<n> w= h= waves= batch= flush_ms= hold= backlog= cost_tail= stop_after=
+//               multi=1 devices=<n> blocks= threads= cheap=1 rate=1
+//
+// multi=1: ONE thread drives `devices` mock GPUs through vpt_gpu::drain_devices (what run() does with the
+// process's GPUs); each device blocks only its own feeds.  blocks / threads: the mock launch's
+// lanes (default 3 x 7).  cheap=1: a push only records its job ids (the film is counted at the snapshots), so the
+// host protocol's own cost shows; rate=1 then also times the provider alone on one thread over the same frame
+// and prints both token rates ("rate frame <M/s> provider <M/s>").
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -24,6 +32,8 @@
 
 namespace {
 int64_t g_w = 0, g_h = 0, g_tw = 8, g_th = 8, g_ntx = 0;
+int g_blocks = 3, g_threads = 7;
+bool g_cheap = false;
 std::mutex g_mu;
 std::vector<uint32_t> g_rendered;  // per jid: times pushed into an open feed
 std::atomic<int> g_open_feeds{0}, g_max_open{0};
@@ -34,26 +44,44 @@ std::vector<struct vpt_gpu_feed*> g_dev_feeds;
 
 struct vpt_gpu_ctx {
   std::vector<float> own;
+  int device = 0;
 };
 struct vpt_gpu_feed {
   vpt_gpu_ctx* ctx;
   float* film;
   bool closed = false;
   bool staged = false;
-  std::mutex mu;              // film / shown: the pusher "renders" (push), the film thread snapshots
+  std::mutex mu;              // film / shown / jids: the pusher "renders" (push), the film thread snapshots
   std::vector<float> shown;   // a staged feed's film as already added to the host film
+  std::vector<uint64_t> jids; // cheap=1: pushed, not yet counted into the film
   uint64_t published = 0;
   std::atomic<uint64_t> backlog_calls{0};
 };
 
 namespace {
-bool complete(vpt_gpu_feed* f) {  // closed, and every feed opened before it closed (its launch has run)
+bool complete(vpt_gpu_feed* f) {  // closed, and every feed opened before it on its device closed (its launch has run)
   std::lock_guard<std::mutex> l(g_dev_mu);
   for (vpt_gpu_feed* g : g_dev_feeds) {
+    if (g->ctx->device != f->ctx->device) continue;
     if (!g->closed) return false;
     if (g == f) return true;
   }
   return true;
+}
+void count_job(float* film, uint64_t jid) {  // the job's 64 samples' count channel
+  const int64_t T = g_ntx * ((g_h + g_th - 1) / g_th);
+  const int64_t tile = (int64_t)(jid % (uint64_t)T), x0 = (tile % g_ntx) * g_tw, y0 = (tile / g_ntx) * g_th;
+  for (int64_t y = y0; y < std::min(g_h, y0 + g_th); ++y)
+    for (int64_t x = x0; x < std::min(g_w, x0 + g_tw); ++x) film[(y * g_w + x) * 4 + 3] += 1.0f;
+}
+void settle(vpt_gpu_feed* f) {  // cheap=1: the pushed jobs into the counts (under f->mu)
+  if (f->jids.empty()) return;
+  {
+    std::lock_guard<std::mutex> l(g_mu);
+    for (uint64_t j : f->jids) ++g_rendered[j];
+  }
+  for (uint64_t j : f->jids) count_job(f->film, j);
+  f->jids.clear();
 }
 int wait_complete(vpt_gpu_feed* f) {
   for (int i = 0; i < 50000 && !complete(f); ++i) std::this_thread::sleep_for(std::chrono::microseconds(100));
@@ -67,6 +95,8 @@ void dev_remove(vpt_gpu_feed* f) {
 }
 void add_delta(vpt_gpu_feed* f, float* host) {  // host += film - shown; shown = film
   std::lock_guard<std::mutex> l(f->mu);
+  settle(f);
+  if (f->shown.empty()) f->shown.assign((size_t)(g_w * g_h * 4), 0.0f);
   for (int64_t i = 0; i < g_w * g_h * 4; ++i) {
     host[i] += f->film[i] - f->shown[i];
     f->shown[i] = f->film[i];
@@ -84,11 +114,12 @@ int vpt_gpu_stream_destroy(vpt_gpu_ctx*, void* s) {
   delete static_cast<int*>(s);
   return VPT_OK;
 }
-int vpt_gpu_launch_info(const vpt_gpu_ctx*, int* blocks, int* threads) {  // a small "GPU": 3 x 7 lanes
-  *blocks = 3;
-  *threads = 7;
+int vpt_gpu_launch_info(const vpt_gpu_ctx*, int* blocks, int* threads) {  // a small "GPU": 3 x 7 lanes by default
+  *blocks = g_blocks;
+  *threads = g_threads;
   return VPT_OK;
 }
+int vpt_gpu_find_seeds(int, uint32_t, uint32_t, uint32_t*, int, int*) { return VPT_E_HIP; }  // (run() is not mocked)
 int vpt_gpu_job_space(const vpt_gpu_ctx*, uint64_t* per_wave, uint64_t* total) {
   *per_wave = (uint64_t)(g_ntx * ((g_h + g_th - 1) / g_th));
   *total = 0;
@@ -135,7 +166,8 @@ int vpt_gpu_feed_open(vpt_gpu_ctx* c, float* film, void* stream, uint64_t, vpt_g
   *out = new vpt_gpu_feed();
   (*out)->ctx = c;
   (*out)->film = film ? film : c->own.data();
-  (*out)->shown.assign((size_t)(g_w * g_h * 4), 0.0f);
+  // (shown is allocated at the first snapshot: a 1080p film's 33 MB zero-fill here would time the mock, not the
+  // protocol -- the library's feeds come from a pool prepared ahead)
   {
     std::lock_guard<std::mutex> l(g_dev_mu);
     g_dev_feeds.push_back(*out);
@@ -148,6 +180,14 @@ int vpt_gpu_feed_open(vpt_gpu_ctx* c, float* film, void* stream, uint64_t, vpt_g
 }
 int vpt_gpu_feed_push(vpt_gpu_feed* f, const uint64_t* jids, uint64_t n) {
   if (f->closed) return VPT_E_STATE;
+  if (g_cheap) {
+    for (uint64_t i = 0; i < n; ++i)
+      if (jids[i] >= g_rendered.size()) return VPT_E_INVALID;
+    std::lock_guard<std::mutex> l(f->mu);
+    f->jids.insert(f->jids.end(), jids, jids + n);
+    f->published += n;
+    return VPT_OK;
+  }
   const int64_t T = (int64_t)g_rendered.size() ? g_ntx * ((g_h + g_th - 1) / g_th) : 1;
   for (uint64_t i = 0; i < n; ++i) {
     {
@@ -165,6 +205,10 @@ int vpt_gpu_feed_push(vpt_gpu_feed* f, const uint64_t* jids, uint64_t n) {
   return VPT_OK;
 }
 int vpt_gpu_feed_backlog(vpt_gpu_feed* f, uint64_t* b) {  // alternately "starved" and "full": both pusher branches
+  if (g_cheap) {  // a GPU that takes every job at once
+    *b = 0;
+    return VPT_OK;
+  }
   *b = (f->backlog_calls++ % 4 == 0) ? 0 : f->published;
   return VPT_OK;
 }
@@ -186,6 +230,10 @@ int vpt_gpu_feed_query(vpt_gpu_feed* f, int* done, uint64_t*) {
 int vpt_gpu_feed_destroy(vpt_gpu_feed* f) {
   vpt_gpu_feed_close(f);
   const int rc = wait_complete(f);
+  {
+    std::lock_guard<std::mutex> l(f->mu);
+    settle(f);
+  }
   dev_remove(f);
   --g_open_feeds;
   delete f;
@@ -215,7 +263,8 @@ int vpt_gpu_feed_collect(vpt_gpu_feed* f, float* host) {
 int main(int argc, char** argv) {
   std::map<std::string, long long> a{{"drivers", 1}, {"helpers", 0}, {"w", 72}, {"h", 40}, {"waves", 5},
                                      {"batch", 7}, {"flush_ms", 0}, {"hold", 0}, {"backlog", 0}, {"stop_after", 0},
-                                     {"cost_tail", 1}, {"cost_chunks", 1}};
+                                     {"cost_tail", 1}, {"cost_chunks", 1}, {"multi", 0}, {"devices", 1},
+                                     {"blocks", 3}, {"threads", 7}, {"cheap", 0}, {"rate", 0}};
   for (int i = 1; i < argc; ++i) {
     const char* eq = std::strchr(argv[i], '=');
     if (eq) a[std::string(argv[i], eq - argv[i])] = std::atoll(eq + 1);
@@ -223,6 +272,39 @@ int main(int argc, char** argv) {
   g_w = a["w"];
   g_h = a["h"];
   g_ntx = (g_w + g_tw - 1) / g_tw;
+  g_blocks = (int)a["blocks"];
+  g_threads = (int)a["threads"];
+  g_cheap = a["cheap"] != 0;
+  double provider_ms = 0;
+  if (a["rate"]) {  // the provider alone, one thread: the drop-in's floor (bench.py's provider_alone)
+    vpt_headless::TileProvider tp0(g_w, g_h, (unsigned)a["waves"], g_tw, g_th);
+    struct Counting {  // (the same per-token counter as the frame's provider below)
+      vpt_headless::TileProvider& tp;
+      std::atomic<uint64_t> handed{0};
+      vpt_headless::TileProvider::token next() {
+        handed.fetch_add(1);
+        return tp.next();
+      }
+    } cp{tp0};
+    const auto r0 = std::chrono::steady_clock::now();
+    vpt_gpu::JobRuns runs;
+    uint64_t n = 0;
+    while (uint64_t k = vpt_gpu::take_jobs(cp, 4096, runs, [](auto&) {})) n += k;
+    provider_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count();
+    if (n != tp0.num_tiles() * (uint64_t)a["waves"]) return 1;
+    // the same on a thread of its own (the frame's taker is one), for reference
+    vpt_headless::TileProvider tp1(g_w, g_h, (unsigned)a["waves"], g_tw, g_th);
+    Counting cp1{tp1};
+    double ms1 = 0;
+    std::thread([&] {
+      const auto t1 = std::chrono::steady_clock::now();
+      vpt_gpu::JobRuns r1;
+      while (vpt_gpu::take_jobs(cp1, 4096, r1, [](auto&) {})) {
+      }
+      ms1 = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+    }).join();
+    std::printf("dropin_mock: provider alone %.1f ms on the main thread, %.1f ms on a new thread\n", provider_ms, ms1);
+  }
   vpt_headless::TileProvider tp(g_w, g_h, (unsigned)a["waves"], g_tw, g_th);
   const uint64_t T = tp.num_tiles(), total = T * (uint64_t)a["waves"];
   g_rendered.assign(total + 8 * T, 0);  // room for jids past a stop
@@ -231,15 +313,26 @@ int main(int argc, char** argv) {
     vpt_headless::TileProvider& tp;
     std::atomic<uint64_t>& handed;
     uint64_t stop_after;
+    uint64_t last = 0;               // rate=1: the frame's token count; the call that takes it notes the time
+    std::atomic<int64_t> dry_ns{0};
     vpt_headless::TileProvider::token next() {
-      if (handed.fetch_add(1) + 1 == stop_after) tp.stop_at_next_wave();
+      const uint64_t k = handed.fetch_add(1) + 1;
+      if (k == stop_after) tp.stop_at_next_wave();
+      if (k == last) dry_ns.store(std::chrono::steady_clock::now().time_since_epoch().count());
       return tp.next();
     }
   } sp{tp, handed, (uint64_t)a["stop_after"]};
+  sp.last = a["rate"] ? total : 0;
   std::vector<float> film((size_t)(g_w * g_h * 4), 0.0f);
-  const int drivers = (int)a["drivers"], helpers = (int)a["helpers"];
-  std::vector<vpt_gpu_ctx> ctx(drivers);
-  for (auto& c : ctx) c.own.assign(film.size(), 0.0f);
+  const bool multi = a["multi"] != 0;
+  const int drivers = multi ? 1 : (int)a["drivers"], helpers = multi ? 0 : (int)a["helpers"];
+  std::vector<vpt_gpu_ctx> ctx(multi ? (size_t)a["devices"] : (size_t)drivers);
+  for (size_t i = 0; i < ctx.size(); ++i) {
+    ctx[i].own.assign(film.size(), 0.0f);
+    ctx[i].device = multi ? (int)i : 0;  // drain(): every context on the one device, as before
+  }
+  std::vector<vpt_gpu_ctx*> ctxp;
+  for (auto& c : ctx) ctxp.push_back(&c);
   vpt_gpu::DrainOptions opt;
   opt.flush_seconds = (double)a["flush_ms"] / 1000.0;
   opt.hold_jobs = (uint64_t)a["hold"];
@@ -252,10 +345,15 @@ int main(int argc, char** argv) {
   }
   std::vector<int> rc(drivers + helpers, 0);
   std::vector<std::thread> pool;
-  for (int i = 0; i < drivers; ++i)
-    pool.emplace_back([&, i] { rc[i] = vpt_gpu::drain(&ctx[i], sp, film.data(), (uint64_t)a["batch"], opt, nullptr, helpers > 0); });
+  const auto f0 = std::chrono::steady_clock::now();
+  if (multi)
+    pool.emplace_back([&] { rc[0] = vpt_gpu::drain_devices(ctxp, sp, film.data(), (uint64_t)a["batch"], opt); });
+  else
+    for (int i = 0; i < drivers; ++i)
+      pool.emplace_back([&, i] { rc[i] = vpt_gpu::drain(&ctx[i], sp, film.data(), (uint64_t)a["batch"], opt, nullptr, helpers > 0); });
   for (int i = 0; i < helpers; ++i) pool.emplace_back([&, i] { rc[drivers + i] = vpt_gpu::help(sp, (uint64_t)a["batch"]); });
   for (int i = 0; i < drivers; ++i) pool[i].join();
+  const double frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - f0).count();
   {
     std::lock_guard<std::mutex> l(vpt_gpu::detail::Helpers::get().mu);
     vpt_gpu::detail::Helpers::get().drivers -= drivers;
@@ -282,5 +380,12 @@ int main(int argc, char** argv) {
   std::printf("dropin_mock: ok %llu waves, %llu jobs, max %d feeds open, %llu jobs in direct launches\n",
               (unsigned long long)waves, (unsigned long long)ran, g_max_open.load(),
               (unsigned long long)g_direct_jobs.load());
+  if (a["rate"]) {  // the taker's rate: tokens / (provider dry - start); frame_ms adds the pipelines' end
+    const double take_ms =
+        (double)(sp.dry_ns.load() - f0.time_since_epoch().count()) * 1e3 * std::chrono::steady_clock::period::num /
+        std::chrono::steady_clock::period::den;
+    std::printf("dropin_mock: rate frame %.2f provider %.2f M tokens/s (taken in %.1f ms, frame %.1f ms, provider alone %.1f ms)\n",
+                ran / take_ms / 1e3, ran / provider_ms / 1e3, take_ms, frame_ms, provider_ms);
+  }
   return 0;
 }

@@ -11,6 +11,8 @@
 //   vpt_gpu::drain(ctx, tp, film, batch).  The volume is nvdb= (vpt_grid_read_nvdb: "density", and
 //   "temperature" when present) or the product library's synthetic stand-in (cloud density, plus the
 //   40*base temperature grid with temperature=1).
+// multi=1 (mode=drain): one thread drives every context through vpt_gpu::drain_devices, as run() drives the GPUs.
+// mode=seed: the private seed recovered from the RNG's job-0 stream (device=-1: host threads; else that GPU).
 // mode=run: each thread calls vpt_gpu::run(params, vol, camera, tp, film, rng) with the reference's
 //   own argument types (tests/native/reference_types_headless.hpp), exactly as main.cpp:63-68 calls
 //   vpt::run; the volume is the NanoGrid<float> bytes of gridbuf= (and tempbuf=), the seed is private
@@ -152,11 +154,15 @@ int main(int argc, char** argv) {
   };
   std::thread sampler_thread;
 
-  if (mode == "seed") {  // the drop-in's seed recovery (no GPU): the RNG's seed is private
+  if (mode == "seed") {  // the drop-in's seed recovery: the RNG's seed is private (device=-1: host threads, no GPU)
     vpt_headless::RandomNumberGenerator rng(cfg.seed);
     uint32_t seed = 0;
-    const int r = vpt_gpu::detail::rng_seed(rng, seed);
-    std::printf("run_gpu_harness: seed %d %u\n", r, seed);
+    int ndev = 0;
+    if (num("device", -1) >= 0 && (vpt_gpu_device_count(&ndev) || ndev <= 0)) return fail("no HIP device");  // (runtime start: not timed)
+    const auto s0 = std::chrono::steady_clock::now();
+    const int r = vpt_gpu::detail::rng_seed(rng, seed, (int)num("device", -1));
+    std::printf("run_gpu_harness: seed %d %u %.1f ms\n", r, seed,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s0).count());
     return 0;
   }
   if (mode == "tiles") {  // the drop-in's tile-size derivation from a first batch of `batch` tokens (no GPU)
@@ -214,6 +220,13 @@ int main(int argc, char** argv) {
     for (auto& t : pool) t.join();
     for (int i = 0; i < threads; ++i)
       if (rc[i]) return fail("vpt_gpu::run");
+    // what the call cost, as main.cpp:65-84 times it (the whole run(); its phases)
+    const vpt_gpu::RunPhases& ph = vpt_gpu::run_phases();
+    std::printf("run_gpu_harness: phases devices=%d total_ms=%.1f hip_ms=%.1f first_batch_ms=%.1f seed_ms=%.1f "
+                "nanogrid_ms=%.1f contexts_ms=%.1f flatten_fix_ms=%.1f upload_ms=%.1f ctx_rest_ms=%.1f tile_costs_ms=%.1f "
+                "bind_ms=%.1f frame_ms=%.1f\n",
+                ph.devices, ph.total_ms, ph.hip_ms, ph.first_batch_ms, ph.seed_ms, ph.nanogrid_ms, ph.contexts_ms,
+                ph.setup_ms[0], ph.setup_ms[1], ph.setup_ms[2], ph.setup_ms[3], ph.setup_ms[4], ph.frame_ms);
   } else {
     vpt_grid_desc *dens = nullptr, *temp = nullptr;
     if (a.count("nvdb")) {
@@ -226,6 +239,9 @@ int main(int argc, char** argv) {
     }
     std::vector<vpt_gpu_ctx*> ctx(threads, nullptr);
     const int ndev = (int)num("devices", 1);
+    // multi=1: one thread drives all `threads` contexts (vpt_gpu::drain_devices, what run() does with the
+    // process's GPUs); contexts go to devices i % devices
+    const bool multi = num("multi", 0) != 0;
     for (int i = 0; i < threads; ++i)
       if (vpt_gpu_create(&cfg, dens, temp, nullptr, i % ndev, &ctx[i])) return fail("vpt_gpu_create");
     float* fh = reinterpret_cast<float*>(film.data().data());
@@ -251,11 +267,17 @@ int main(int argc, char** argv) {
       float* fh2 = reinterpret_cast<float*>(film2.data().data());
       const auto r0 = std::chrono::steady_clock::now();
       std::vector<std::thread> pool;
-      for (int i = 0; i < threads; ++i)
-        pool.emplace_back([&, i] {
+      if (multi)
+        pool.emplace_back([&] {
           pin_to_node(num("taker_node", -1));
-          rc[i] = vpt_gpu::drain(ctx[i], tp2, fh2, batch, opt);
+          rc[0] = vpt_gpu::drain_devices(ctx, tp2, fh2, batch, opt);
         });
+      else
+        for (int i = 0; i < threads; ++i)
+          pool.emplace_back([&, i] {
+            pin_to_node(num("taker_node", -1));
+            rc[i] = vpt_gpu::drain(ctx[i], tp2, fh2, batch, opt);
+          });
       for (auto& t : pool) t.join();
       for (int i = 0; i < threads; ++i)
         if (rc[i]) return fail("vpt_gpu::drain");
@@ -267,12 +289,19 @@ int main(int argc, char** argv) {
       if (sample_ms > 0) sampler_thread = std::thread(sampler);
       std::vector<std::thread> pool;
       // helpers=N: N more threads take tokens for the drivers (vpt_gpu::help, as run()'s non-driving threads do)
-      const int helpers = (int)num("helpers", 0);
-      for (int i = 0; i < threads; ++i)
-        pool.emplace_back([&, i] {
-          pin_to_node(num("taker_node", -1));
-          rc[i] = vpt_gpu::drain(ctx[i], sp, fh, batch, opt, nullptr, helpers > 0);
-        });
+      const int helpers = multi ? 0 : (int)num("helpers", 0);
+      if (multi)  // (pool[0] .. pool[threads - 1] are joined below: the other slots are empty threads)
+        for (int i = 0; i < threads; ++i)
+          pool.emplace_back([&, i] {
+            pin_to_node(num("taker_node", -1));
+            if (i == 0) rc[0] = vpt_gpu::drain_devices(ctx, sp, fh, batch, opt);
+          });
+      else
+        for (int i = 0; i < threads; ++i)
+          pool.emplace_back([&, i] {
+            pin_to_node(num("taker_node", -1));
+            rc[i] = vpt_gpu::drain(ctx[i], sp, fh, batch, opt, nullptr, helpers > 0);
+          });
       std::vector<int> hrc(helpers, 0);
       {
         // the drivers register their pipelines as they start; helpers wait for one (Helpers::drivers counts

@@ -289,6 +289,12 @@ def lib() -> C.CDLL:
         L.vpt_gpu_feed_snapshot.argtypes = [vp, fp]
         L.vpt_gpu_feed_backlog.argtypes = [vp, C.POINTER(C.c_uint64)]
         L.vpt_gpu_feed_prepare.argtypes = [vp, C.c_uint64, C.c_int]
+    if hasattr(L, "vpt_gpu_feed_debug"):
+        L.vpt_gpu_feed_debug.argtypes = [vp, C.c_int, C.POINTER(C.c_uint64)]
+    if hasattr(L, "vpt_gpu_find_seeds"):
+        L.vpt_gpu_find_seeds.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.c_int,
+                                         C.POINTER(C.c_int)]
+        L.vpt_gpu_setup_timings.argtypes = [vp, C.POINTER(C.c_double), C.c_int]
     _lib = L
     return L
 

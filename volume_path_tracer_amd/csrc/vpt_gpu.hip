@@ -76,6 +76,9 @@ constexpr uint64_t kFeedEmpty = ~0ULL;
 constexpr int32_t kFeedPending = -2;
 constexpr int32_t kFeedWait = -3;
 constexpr uint32_t kFeedDeadline = 3000000000u;
+// A waiting wavefront stores the job count it sees again every kWaitingRefresh ticks (~5 ms) while it waits: a
+// posted write of an older count may land after a newer one, and the refresh overwrites it.
+constexpr uint32_t kWaitingRefresh = 1u << 19;
 // Every kStartedHint-th reserved item is reported to the host (the feed's backlog, vpt_gpu_feed_backlog):
 // one posted write per 1 024 jobs.
 constexpr uint64_t kStartedHint = 1024;
@@ -302,19 +305,26 @@ struct KernelEnvT {
       const uint64_t c = __hip_atomic_load(job_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (c >= published) {
         if (w & kFeedClosed) return 0;
+        // The lanes have taken every item published: say so (one lane per wavefront, as it starts waiting, and
+        // again every kWaitingRefresh ticks while it waits -- lc.y0, free while the lane has no job, holds the
+        // last store's time).  The host's backlog estimate comes from hints that may land out of order; a count
+        // >= its published count here means the lanes wait for it, whatever the hints say
+        // (vpt_gpu_feed_backlog).  The refresh overwrites a stale count that landed last.
+        bool say;
         if (lc.pix != kFeedWait) {
           lc.pix = kFeedWait;
           lc.x0 = (int32_t)now;  // wait start
-          // The lanes have taken every item published: say so (one lane per wavefront, as it starts waiting).
-          // The host's backlog estimate comes from hints that may land out of order; a count >= its published
-          // count here means the lanes wait for it, whatever the hints say (vpt_gpu_feed_backlog).
-          const uint64_t m = __builtin_amdgcn_ballot_w64(true);
-          if (A->feed_waiting && __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == (uint32_t)__builtin_ctzll(m))
-            __hip_atomic_store(A->feed_waiting, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          say = true;
         } else if (now - (uint32_t)lc.x0 > kFeedDeadline) {
           __hip_atomic_store(feed_error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // (host memory: a store)
           return 0;
+        } else {
+          say = now - (uint32_t)lc.y0 > kWaitingRefresh;
         }
+        if (say) lc.y0 = (int32_t)now;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(say);
+        if (m && A->feed_waiting && __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == (uint32_t)__builtin_ctzll(m))
+          __hip_atomic_store(A->feed_waiting, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return -1;
       }
       const uint64_t k = atomicAdd(job_counter, 1ULL);
@@ -478,9 +488,13 @@ __device__ __forceinline__ void xchg_pack(const Lane& ln, const LaneCold& lc, ui
     x[n++] = (uint32_t)ln.temp_cell.i; x[n++] = (uint32_t)ln.temp_cell.j; x[n++] = (uint32_t)ln.temp_cell.k;
   }
   if (HasTemp) x[n++] = (uint32_t)ln.temp_cell.code;
+#ifdef VPT_JOB_LOG
+  x[n++] = lc.t_start;  // (the diagnostic build's per-job fields travel too)
+  x[n++] = lc.job;
+#endif
   while (n < kXWords) x[n++] = 0;
 }
-static_assert(54 + 4 <= kXWords, "the exchange holds every state word");
+static_assert(54 + 4 + 2 <= kXWords, "the exchange holds every state word (and the job log's two)");
 template <bool HasTemp>
 __device__ __forceinline__ void xchg_unpack(Lane& ln, LaneCold& lc, const uint32_t x[kXWords]) {
   int n = 0;
@@ -502,7 +516,12 @@ __device__ __forceinline__ void xchg_unpack(Lane& ln, LaneCold& lc, const uint32
   if (HasTemp) {
     ln.temp_cell.i = (int32_t)x[n++]; ln.temp_cell.j = (int32_t)x[n++]; ln.temp_cell.k = (int32_t)x[n++];
   }
-  if (HasTemp) ln.temp_cell.code = (int32_t)x[n];
+  if (HasTemp) ln.temp_cell.code = (int32_t)x[n++];
+#ifdef VPT_JOB_LOG
+  lc.t_start = x[n++];
+  lc.job = x[n++];
+#endif
+  (void)n;
 }
 // Dynamic LDS of the compacting kernel: [kXWords / 4][kBlockThreads] uint4 (61 440 B).
 constexpr size_t kXchgBytes = (size_t)kXWords * kBlockThreads * sizeof(uint32_t);
@@ -1266,7 +1285,11 @@ int render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, float* film
   env.event_count = ctx->job_counter + 2 * slot + 1;
   env.event_cap = event_cap;
   if (slot_out) *slot_out = slot;
-  const vpt::DevScene* scene = latency || (use_lat && ctx->lat_ungated) ? ctx->scene_lat_dev : ctx->scene_dev;
+  // (a compacting launch reads the context's scene, whose wave_lanes is 64: a path moved into another thread's
+  // slot must be able to fetch there -- with fewer fetching lanes per wavefront, live paths packed into the
+  // first slots would leave the fetching slots to finished ones)
+  const vpt::DevScene* scene =
+      latency || (use_lat && ctx->lat_ungated && !compact) ? ctx->scene_lat_dev : ctx->scene_dev;
   if (use_lat) {
     env.compact_every = (uint32_t)std::max(1, ctx->compact_every);
     if (compact) {
@@ -2138,6 +2161,8 @@ int vpt_gpu_feed_push(vpt_gpu_feed* f, const uint64_t* jids, uint64_t n) {
   return VPT_OK;
 }
 
+constexpr std::chrono::milliseconds kStaleHints{10};
+
 int vpt_gpu_feed_backlog(vpt_gpu_feed* f, uint64_t* backlog) {
   if (!f || !backlog) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_backlog: null argument");
   // the newest reported reservation (the lanes' posted writes may land out of order: keep the largest)
@@ -2156,6 +2181,10 @@ int vpt_gpu_feed_backlog(vpt_gpu_feed* f, uint64_t* backlog) {
   // the lanes are waiting now.
   const uint64_t waiting = __atomic_load_n(f->waiting, __ATOMIC_RELAXED);
   if (f->launched && waiting >= f->published) *backlog = 0;
+  // And a host-side bound: hints that have not moved for kStaleHints while the estimate says jobs
+  // are queued mean either lanes too busy to take any -- pushing more only fills the ring up to its window --
+  // or an estimate stuck on a stale count: read it as empty, so the pusher never waits on it for long.
+  if (f->launched && *backlog > 0 && now - f->started_moved > kStaleHints) *backlog = 0;
   if (f->launched && *backlog > 0 && now - f->started_moved > std::chrono::seconds(1) &&
       now - f->stale_traced > std::chrono::seconds(1)) {  // (diagnostics) nothing reserved for a second
     f->stale_traced = now;
@@ -2163,6 +2192,19 @@ int vpt_gpu_feed_backlog(vpt_gpu_feed* f, uint64_t* backlog) {
     feed_trace(f, "noreserve", (double)f->published, (double)f->started_seen);
     feed_trace(f, "state", (double)__atomic_load_n(f->error, __ATOMIC_RELAXED),
                q == hipSuccess ? 1.0 : (q == hipErrorNotReady ? 0.0 : -(double)q));
+  }
+  return VPT_OK;
+}
+
+int vpt_gpu_feed_debug(vpt_gpu_feed* f, int op, uint64_t* value) {
+  if (!f || !value || op < 0 || op > 2) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_feed_debug: bad argument");
+  if (op == 0) {
+    *value = __atomic_load_n(f->waiting, __ATOMIC_RELAXED);
+  } else if (op == 1) {
+    __atomic_store_n(f->waiting, *value, __ATOMIC_RELAXED);
+  } else {
+    for (uint64_t i = 0; i < vpt::kHintSlots; ++i) __atomic_store_n(f->started + i, *value, __ATOMIC_RELAXED);
+    f->started_seen = *value;
   }
   return VPT_OK;
 }

@@ -255,23 +255,34 @@ def buffer_from_grid(g: capi.Grid, name: str) -> bytes:
     leaf_pos = {li: off_leaf + i * LEAF_SIZE for i, li in enumerate(leaf_order)}
 
     all_vals = [g.leaf_values.reshape(-1)] if n else []
-    # leaves
-    for li, p in leaf_pos.items():
-        o = g.leaf_origin[li]
-        v = g.leaf_values[li]
-        mask = g.leaf_value_mask[li]
-        bits = np.unpackbits(mask.view(np.uint8), bitorder="little").astype(bool)
-        act = np.nonzero(bits)[0]
-        if act.size:
-            c = np.stack([act >> 6, (act >> 3) & 7, act & 7], 1)
-            bmin, bdif = c.min(0), c.max(0) - c.min(0)
-        else:
-            bmin, bdif = np.zeros(3, int), np.zeros(3, int)
-        mn, _, avg, std = _stats(v)
-        struct.pack_into("<3i3BB", buf, p, *(int(o[a]) + int(bmin[a]) for a in range(3)), *(int(x) for x in bdif), 0)
-        buf[p + 16:p + 80] = mask.astype("<u8").tobytes()
-        struct.pack_into("<4f", buf, p + 80, mn, float(g.leaf_max[li]), avg, std)
-        buf[p + LEAF_VALUES:p + LEAF_SIZE] = v.astype("<f4").tobytes()
+    # leaves, all at once (in leaf_order): the active voxels' bbox, the value mask, min / stored max / mean /
+    # std of the 512 values, the values
+    if leaf_order:
+        order = np.asarray(leaf_order, np.int64)
+        lv = np.asarray(g.leaf_values).reshape(n, 512)[order]
+        lm = np.ascontiguousarray(np.asarray(g.leaf_value_mask).reshape(n, 8)[order], "<u8")
+        bits = np.unpackbits(lm.view(np.uint8).reshape(-1, 64), axis=1, bitorder="little").astype(bool).reshape(-1, 8, 8, 8)
+        lo_b, dif_b = [], []
+        for ax in ((2, 3), (1, 3), (1, 2)):  # bit n = x << 6 | y << 3 | z
+            a = bits.any(axis=ax)
+            has = a.any(1)
+            first = np.where(has, a.argmax(1), 0)
+            last = np.where(has, 7 - a[:, ::-1].argmax(1), 0)
+            lo_b.append(first)
+            dif_b.append(last - first)
+        rec = np.zeros(len(order), np.dtype([("bmin", "<i4", 3), ("bdif", "u1", 3), ("flags", "u1"), ("mask", "<u8", 8),
+                                              ("stats", "<f4", 4), ("vals", "<f4", 512)]))
+        assert rec.dtype.itemsize == LEAF_SIZE
+        rec["bmin"] = np.asarray(g.leaf_origin).reshape(n, 3)[order].astype(np.int64) + np.stack(lo_b, 1)
+        rec["bdif"] = np.stack(dif_b, 1)
+        rec["mask"] = lm
+        v64 = lv.astype(np.float64)
+        rec["stats"][:, 0] = lv.min(1)
+        rec["stats"][:, 1] = np.asarray(g.leaf_max).reshape(n)[order]
+        rec["stats"][:, 2] = v64.mean(1)
+        rec["stats"][:, 3] = v64.std(1)
+        rec["vals"] = lv
+        buf[off_leaf:off_leaf + len(order) * LEAF_SIZE] = rec.tobytes()
     # lower nodes
     for lo, p in lower_pos.items():
         tab = np.zeros(4096, "<i8")
