@@ -323,12 +323,15 @@ struct KernelEnvT {
   // wave-instruction carries 21 samples, each sample's three adds one request.  The latency kernel (state in
   // VGPRs, few samples at a time) adds from the lane itself.
   //
-  // The ordered film (args()->samples, vpt_gpu_set_film_order): the same regroup with plain stores of each
-  // sample's L into the launch's sample buffer (job j's pixel q at (j * tile_area + q) * 3: three lanes store one
-  // sample's 12 contiguous bytes, one request), the rank word holding (q << 6) | lane and the job index coming
-  // from the source lane's cold state (item_lo, set at its fetch); the film itself is written only by
-  // vpt_film_order_kernel, in wave order.
+  // The ordered film (args()->samples, vpt_gpu_set_film_order): each lane stores its sample's L into the
+  // launch's sample buffer itself -- job j's pixel q at (j * tile_area + q) * 3, j = the job's index in the launch
+  // (the cold state's item_lo, set at its fetch) -- and the film is written only by vpt_film_order_kernel, in
+  // wave order.  Plain stores complete in the L2 and need no regroup: stored from the lane they measured faster
+  // than regrouped through the wavefront as the atomics are (C3 336.1 vs 337.9 ms, C4 81.2 vs 84.2; r06f,
+  // profiles/r06f_ordered_direct_and_ray_gate_ab.txt).  (The early return and film_commit's store branch stay as
+  // measured: equivalent rewrites of these lines moved the temperature kernel from 0 to 12 bytes of spills.)
   __device__ __forceinline__ bool film_regroup(const DevScene& S) const {
+    if (args()->samples) return false;
     return !RegCold && (args()->samples != nullptr || (uint64_t)S.W * (uint64_t)S.H < (1ULL << 26));  // (index << 6 | lane fits 32 bits)
   }
   __device__ __forceinline__ void film_add(const DevScene& S, const Lane& ln, int32_t px, int32_t py, int32_t rw) {
@@ -339,7 +342,7 @@ struct KernelEnvT {
       const uint64_t m = __builtin_amdgcn_ballot_w64(true);  // this pass's finishing lanes
       const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
       g_film_rank[(threadIdx.x & ~63u) + rank] = (pixel << 6) | (threadIdx.x & 63u);
-    } else if (samples) {  // (the latency kernel: from the lane itself)
+    } else if (samples) {  // (the ordered film: from the lane itself)
       float* s = samples + ((uint64_t)lc.item_lo * S.tile_area + pixel) * 3;
       s[0] = lc.L[0];
       s[1] = lc.L[1];

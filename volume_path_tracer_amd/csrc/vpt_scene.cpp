@@ -3,8 +3,12 @@
 // Everything here runs once per context on the host, with the reference's float formulas and
 // operation order (Eigen fixed-size products/reductions restated as a0*b0 + (a1*b1 + a2*b2)),
 // so the device integrator receives bit-identical constants.
+#include <sched.h>
+
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -86,11 +90,28 @@ void blackbody_table(float* out) {  // init_blackbody_radiation_xyz (precompute_
   for (int i = 0; i < VPT_BLACKBODY_ROWS; ++i) spectrum_to_xyz((i - 1) * 100.0f, out + i * 3);
 }
 
+// Host worker threads for the grid build: the CPUs this process may run on (its affinity mask), capped by the
+// cgroup's CPU quota (cpu.max: the GPU box grants a job 16 of its 256 CPUs -- 64 threads there time-slice on 16)
+// and at 64.  Computed once.
 int default_threads() {
-  unsigned n = std::thread::hardware_concurrency();
-  if (n == 0) n = 4;
-  if (n > 64) n = 64;
-  return (int)n;
+  static const int n = [] {
+    unsigned c = std::thread::hardware_concurrency();
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0 && CPU_COUNT(&set) > 0) c = (unsigned)CPU_COUNT(&set);
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char quota[32] = {};
+      long long period = 0;
+      if (std::fscanf(f, "%31s %lld", quota, &period) == 2 && std::strcmp(quota, "max") != 0 && period > 0) {
+        const long long q = std::atoll(quota);
+        const unsigned cap = (unsigned)std::max(1LL, (q + period - 1) / period);
+        c = std::min(c, cap);
+      }
+      std::fclose(f);
+    }
+    if (c == 0) c = 4;
+    return (int)std::min(c, 64u);
+  }();
+  return n;
 }
 
 // Camera::Camera (src/camera.cpp:45-57) and the constant terms of vpt::run / sample_Ld.
