@@ -357,7 +357,7 @@ int vpt_gpu_stream_sync(vpt_gpu_ctx* ctx, void* hip_stream);
  * it is unknown or the intersection is empty, and the thread is left as it was).  A feed's pusher reads and writes the pinned ring, which sits
  * in that node's memory, a slot per job: from the other socket of a 2-socket host every access crosses the
  * socket link (C4 through the drop-in: 174-205 ms per frame with the process on the far node, 119-148 on the
- * GPU's, profiles/r05m_numa.txt).  `node` may be NULL. */
+ * GPU's, profiles/archive/r05m_numa.txt).  `node` may be NULL. */
 int vpt_gpu_bind_thread_near(vpt_gpu_ctx* ctx, int* node);
 /* An extra device film (float[H][W][4], zeroed) of the context's size, e.g. the second buffer of a
  * progressive film; release it with vpt_gpu_film_free before vpt_gpu_destroy. */

@@ -350,7 +350,7 @@ int vpt::host::render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, 
   // of a frame dealt over several): a launch lasts as long as its slowest jobs, and a job's lane runs
   // faster with fewer waves per SIMD, so the grid is sized to round(1 + 1.8 x) blocks per CU (at most
   // the resident capacity), x = items per resident lane.  Same jobs, same samples.  Measured (r03h,
-  // profiles/r03h_grid_sweep.txt; C3 frames of spp waves, 4 / 5 / 6 / 7 blocks per CU, ms): spp 16
+  // profiles/archive/r03h_grid_sweep.txt; C3 frames of spp waves, 4 / 5 / 6 / 7 blocks per CU, ms): spp 16
   // (x 1.1) 54.5 / 55.0 / 55.4 / 57.5 (3: 51.5); spp 24 (x 1.7) 57.3 / 61.0 / 64.7 / 65.7; spp 32
   // (x 2.3, the 8-GPU share) 70.4 / 66.9 / 67.5 / 71.2; spp 48 (x 3.4) 92.2 / 90.8 / 89.7 / 87.9; from
   // spp 96 on (and C5's shares) the full grid is best.  C2 (262 144 jobs, x 0.57 -> 2 blocks per CU,
@@ -381,7 +381,7 @@ int vpt::host::render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, 
   // -> 19.2-19.7 ms, r04e / r04z), and partly filled ones whose rule above gives <= lat_per_cu blocks per CU
   // with the context's gates (C2 100.0-101.3 -> 95.7-96.6 ms, the 8-GPU C3 share of 32 waves 66.1-66.6 ->
   // 65.1-65.3; with the latency gates they ran slower, 108.3-109.8 / 75.2-76.1 ms: its one-lane blocks add
-  // wave instructions to launches that are issue-bound; r04k, profiles/r04k_lat_gated_ab.txt).  lat_mode 1
+  // wave instructions to launches that are issue-bound; r04k, profiles/archive/r04k_lat_gated_ab.txt).  lat_mode 1
   // forces it.  Same jobs, same samples.
   const uint64_t lat_blocks = cus * (uint64_t)ctx->lat_per_cu;
   const bool use_lat = !dbg && !feed && ctx->lat_mode != 0 &&
@@ -633,7 +633,7 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   // waiting lanes, density evaluations (with the deferred exact draw) for >= 36, everything runs when
   // < 8 lanes are walking; the walk loops while >= 4 lanes walk (r02 sweep: 6:8:36:4 363.7 ms vs
   // 6:12:32:4 366.6 ms, C4 103.7 vs 104.4).  The temperature kernel's rare blocks wait for 8 lanes since the film
-  // regroup (C4 83.3-83.6 vs 83.9-84.3 ms over 4 alternating runs, profiles/r05gates2_c4_gate_min.txt).
+  // regroup (C4 83.3-83.6 vs 83.9-84.3 ms over 4 alternating runs, profiles/archive/r05gates2_c4_gate_min.txt).
   ctx->scene.gate_min = temperature ? 8 : 6;
   ctx->scene.gate_idle = 8;
   ctx->scene.gate_eval = 36;

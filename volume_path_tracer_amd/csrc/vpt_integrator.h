@@ -823,7 +823,7 @@ __host__ __device__ __forceinline__ bool hdda_step(const DevGrid& g, Lane& ln) {
 // Walk-loop iterations between two checks of its exit condition (the ballots).  The extra
 // iterations only delay the loop's exit, never a lane's own order of operations.  C3 at 7 waves:
 // 433.5 ms (1) / 427.2 (2) / 423.2 (3) / 424.1 (4); C4 139.8 / 136.5 / 137.3 / 136.5.
-// Re-measured on the r02g kernel (profiles/r02g_exp_walk_unroll.txt): C3 366.8-367.3 (2) / 365.2-365.8 (3)
+// Re-measured on the r02g kernel (profiles/archive/r02g_exp_walk_unroll.txt): C3 366.8-367.3 (2) / 365.2-365.8 (3)
 // / 365.3-365.5 (4) ms, C4 103.1 / 102.4 / 106.3 (the temperature kernel spills at 4).
 #ifndef VPT_WALK_UNROLL
 #define VPT_WALK_UNROLL 3

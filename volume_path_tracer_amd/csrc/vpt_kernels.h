@@ -202,7 +202,7 @@ struct KernelEnvT {
   // takes jobs until none is left.  0 = auto from x = items / wavefronts: one lane (its jobs in
   // sequence) while x < 3, else 1 + floor(x).  A second path in a wavefront slows the first ~1.6x, so
   // one lane with a few jobs in a row wins: C1 frames on the full grid (r02g,
-  // profiles/r02g_c1_lanes_sweep.txt), 1 / 2 / 3 lanes: 8 spp (x = 1.1) 23.3 / 29.3 / - ms, 16 spp
+  // profiles/archive/r02g_c1_lanes_sweep.txt), 1 / 2 / 3 lanes: 8 spp (x = 1.1) 23.3 / 29.3 / - ms, 16 spp
   // (x = 2.3) 31.7 / 32.5 / 35.6, 32 spp (x = 4.6) 51.9 / 43.1 / 42.1 (5 lanes: 41.5).
   // Feed mode: a fetching lane of this wavefront holds a reserved item it has not read (it pins a ring slot
   // until it does), so the fetch block runs now rather than when enough lanes wait (see fetch_feed).
@@ -402,7 +402,7 @@ struct KernelEnvT {
 // The latency kernel's partly filled launches (C2: 2 blocks per CU, 2 jobs per lane) are issue-bound on
 // divergent wave instructions: the HDDA step takes 85 % of the wave time and runs at 32.5 of 64 lanes, and per
 // walk-loop iteration a wavefront holds 32.7 walking, 14.9 parked (a collision waiting for its batched
-// evaluation) and 12.5 finished paths (r05f census, profiles/r05f_c2_census.txt).  Every `compact_every` outer
+// evaluation) and 12.5 finished paths (r05f census, profiles/archive/r05f_c2_census.txt).  Every `compact_every` outer
 // iterations the block's four wavefronts meet (two barriers), count their walking / other live paths with
 // ballots, and -- when packing would leave fewer wavefronts holding walkers, or live paths -- move every path
 // (its hot Lane registers and its cold state, which this kernel keeps in VGPRs: 54 words, 58 with a temperature grid) through LDS so
