@@ -195,6 +195,13 @@ typedef struct vpt_counters {
 int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density,
                    const vpt_grid_desc* temperature, const float* blackbody_500x3, int device,
                    vpt_gpu_ctx** out);
+/* The same context on each of n devices (devices[i]; out[n]) with the grids flattened and majorant-fixed once on
+ * the host and uploaded to every device in parallel (the multi-GPU drop-in's setup: one flatten instead of n
+ * competing for the host's CPUs).  On failure no context is left (out[] NULL) and vpt_last_error() names the
+ * device. */
+int vpt_gpu_create_many(const vpt_configuration* cfg, const vpt_grid_desc* density,
+                        const vpt_grid_desc* temperature, const float* blackbody_500x3, const int* devices, int n,
+                        vpt_gpu_ctx** out);
 int vpt_gpu_destroy(vpt_gpu_ctx* ctx);
 
 /* Jobs per wave T and total jobs num_waves*T of the context's configuration. */

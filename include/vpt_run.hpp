@@ -895,8 +895,9 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
     if (int rc = vpt_grid_from_nanovdb(&grids.temperature(), (size_t)grids.temperature().gridSize(), &temp.d)) return rc;
   lap(ph.nanogrid_ms);
 
-  // A context per GPU, built in parallel (each flattens and uploads the grids): the feed's pinned ring and copy
-  // buffers and the tile costs of its cost tail are setup too, like the grid upload.
+  // A context per GPU: the grids flattened and majorant-fixed once, uploaded to every device in parallel
+  // (vpt_gpu_create_many); the feed's pinned ring and copy buffers and the tile costs of its cost tail are setup
+  // too, like the grid upload.
   std::vector<vpt_gpu_ctx*> ctxs((size_t)ndev, nullptr);
   struct Ctxs {
     std::vector<vpt_gpu_ctx*>& c;
@@ -905,20 +906,22 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
         if (x) vpt_gpu_destroy(x);
     }
   } guard{ctxs};
+  std::vector<int> devices((size_t)ndev);
+  for (int d = 0; d < ndev; ++d) devices[(size_t)d] = d;
+  if (int rc = vpt_gpu_create_many(&cfg, dens.d, temp.d, nullptr, devices.data(), ndev, ctxs.data())) return rc;
   std::vector<int> crc((size_t)ndev, VPT_OK);
-  auto build = [&](int d) {
-    int rc = vpt_gpu_create(&cfg, dens.d, temp.d, nullptr, d, &ctxs[(size_t)d]);
-    if (rc == VPT_OK) rc = vpt_gpu_feed_prepare(ctxs[(size_t)d], 0, 1);
+  auto prepare = [&](int d) {
+    int rc = vpt_gpu_feed_prepare(ctxs[(size_t)d], 0, 1);
     if (rc == VPT_OK) rc = vpt_gpu_tile_costs(ctxs[(size_t)d], nullptr, nullptr);
     if (rc != VPT_OK)  // (vpt_last_error is per thread: say it here)
       std::fprintf(stderr, "vpt_gpu::run: device %d: %s\n", d, vpt_last_error());
     crc[(size_t)d] = rc;
   };
   if (ndev == 1) {
-    build(0);
+    prepare(0);
   } else {
     std::vector<std::thread> pool;
-    for (int d = 0; d < ndev; ++d) pool.emplace_back(build, d);
+    for (int d = 0; d < ndev; ++d) pool.emplace_back(prepare, d);
     for (auto& th2 : pool) th2.join();
   }
   for (int rc : crc)

@@ -186,3 +186,20 @@ def test_fullres_frame_waves_bit_identical_to_the_worker_pool(name):
     f_g = it.film_host()
     f_o, _, _ = O.render_pool(wl.cfg, *_oracle(dens, temp), 2, 16)
     _assert_bitwise(f_g, f_o, f"{name} waves 1..2")
+
+
+def test_contexts_from_one_flatten():
+    """vpt_gpu_create_many (the multi-GPU drop-in's setup): the grids flattened once and uploaded to each device --
+    here two contexts on the box's one GPU.  Both render the oracle's 4-wave film bit for bit, and both report the
+    same flatten time (one build)."""
+    from volume_path_tracer_amd.render import Integrator
+
+    wl = workload("c4", width=40, height=32, spp=4, grid_n=64)
+    dens, temp = _grids(wl)
+    its = Integrator.create_many(wl.cfg, dens, temp, devices=(0, 0))
+    T = wl.cfg.jobs_per_wave()
+    f_o, _, _ = O.render_jobs(wl.cfg, *_oracle(dens, temp), 0, 4 * T)
+    for it in its:
+        _assert_bitwise(_film(it, 0, 4 * T), f_o, "create_many context")
+    t0, t1 = (it.setup_timings() for it in its)
+    assert t0["flatten_fix"] == t1["flatten_fix"] > 0 and t0["upload"] > 0

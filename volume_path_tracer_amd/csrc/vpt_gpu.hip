@@ -528,18 +528,35 @@ int vpt_gpu_find_seeds(int device, uint32_t out0, uint32_t out1, uint32_t* seeds
   return VPT_OK;
 }
 
-int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, const vpt_grid_desc* temperature,
-                   const float* blackbody_500x3, int device, vpt_gpu_ctx** out) {
-  if (!cfg || !density || !out) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_create: null argument");
+}  // extern "C"
+
+namespace {
+// The host side of Volume::Volume: the grids flattened (leaf-slot and walk tables, the stencil pool) with the
+// density's majorants fixed for interpolation (volume.cpp:162-170; temperature is only sampled).  ms[0] += the
+// time taken.
+struct HostGrids {
+  vpt::HostGrid density, temperature;
+  bool has_temperature = false;
+};
+int build_grids(const vpt_grid_desc* density, const vpt_grid_desc* temperature, HostGrids& g, double* ms) {
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = vpt::build_host_grid(*density, true, 0, g.density);
+  if (rc) return rc;
+  vpt::compute_runs(g.density, 0);
+  if (temperature && (rc = vpt::build_host_grid(*temperature, false, 0, g.temperature))) return rc;
+  g.has_temperature = temperature != nullptr;
+  if (ms) *ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return VPT_OK;
+}
+
+// A context on `device` from grids already flattened (vpt_gpu_create, vpt_gpu_create_many).
+int create_on(const vpt_configuration* cfg, const HostGrids& grids, const vpt_grid_desc* temperature,
+              const float* blackbody_500x3, int device, double flatten_ms, vpt_gpu_ctx** out) {
   *out = nullptr;
-  int ndev = 0;
-  hipError_t e = hipGetDeviceCount(&ndev);
-  if (e != hipSuccess || ndev <= 0)
-    return vpt::set_error(VPT_E_HIP, "vpt_gpu_create: no HIP device (the integrator has no CPU fallback)");
-  if (device < 0 || device >= ndev) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_create: bad device index");
   std::unique_ptr<vpt_gpu_ctx, void (*)(vpt_gpu_ctx*)> ctx(new vpt_gpu_ctx(), destroy);
   ctx->device = device;
   ctx->cfg = *cfg;
+  ctx->setup_ms[0] = flatten_ms;
   using clk = std::chrono::steady_clock;
   auto t = clk::now();
   auto lap = [&](int i) {  // setup phases (vpt_gpu_setup_timings)
@@ -551,32 +568,19 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   if (rc) return rc;
   lap(4);
   if ((rc = vpt::build_scene(*cfg, ctx->scene))) return rc;
-
-  // Volume::Volume: fix the density majorants (volume.cpp:162-170); temperature is only sampled.
-  {
-    vpt::HostGrid h;
-    if ((rc = vpt::build_host_grid(*density, true, 0, h))) return rc;
-    vpt::compute_runs(h, 0);
-    lap(0);
-    if ((rc = vpt::upload_grid(h, ctx->density))) return rc;
-    lap(1);
-  }
-  if (temperature) {
-    vpt::HostGrid h;
-    if ((rc = vpt::build_host_grid(*temperature, false, 0, h))) return rc;
-    lap(0);
-    if ((rc = vpt::upload_grid(h, ctx->temperature))) return rc;
-    lap(1);
-  }
+  if ((rc = vpt::upload_grid(grids.density, ctx->density))) return rc;
+  if (grids.has_temperature && (rc = vpt::upload_grid(grids.temperature, ctx->temperature))) return rc;
+  lap(1);
+  const bool has_temperature = grids.has_temperature;
   // The run-skipping kernel variant is for grids with large equal-majorant regions (C2's constant
   // cube: 36 % of the interior cells have run radius >= 2; the 512^3 cloud: 4 %, where the variant
   // would cost more than it skips).  vpt_gpu_set_run_skipping overrides the choice.
-  ctx->use_runs = !temperature && ctx->density.run_fraction >= 0.25;
+  ctx->use_runs = !has_temperature && ctx->density.run_fraction >= 0.25;
   ctx->scene.density = ctx->density.dev;
   vpt::scene_finalize(ctx->scene);  // uses only the density map (host copy of the values)
   ctx->scene.temperature = ctx->temperature.dev;
-  ctx->scene.has_temperature = temperature ? 1 : 0;
-  ctx->scene.bb_lds_ok = temperature ? vpt::blackbody_rows_suffice(*temperature, cfg->volume_parameters.temperature_scale,
+  ctx->scene.has_temperature = has_temperature ? 1 : 0;
+  ctx->scene.bb_lds_ok = has_temperature ? vpt::blackbody_rows_suffice(*temperature, cfg->volume_parameters.temperature_scale,
                                                                     cfg->volume_parameters.temperature_offset, vpt::kBbLdsRows)
                                      : 0;
 
@@ -608,7 +612,7 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   int per_cu = 0, cus = 0;
   // sized for the production kernel of this scene; the debug variant is launched with the same grid
   VPT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu, temperature ? vpt::vpt_integrate_kernel<true, false, false>
+      &per_cu, has_temperature ? vpt::vpt_integrate_kernel<true, false, false>
                            : (ctx->use_runs ? vpt::vpt_integrate_kernel<false, false, true> : vpt::vpt_integrate_kernel<false, false, false>),
       vpt::kBlockThreads, 0));
   VPT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
@@ -616,14 +620,14 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   ctx->grid_blocks = per_cu * cus;
   int lat_per_cu = 0;
   VPT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &lat_per_cu, temperature ? vpt::vpt_integrate_kernel<true, false, false, true>
+      &lat_per_cu, has_temperature ? vpt::vpt_integrate_kernel<true, false, false, true>
                                : (ctx->use_runs ? vpt::vpt_integrate_kernel<false, false, true, true>
                                                 : vpt::vpt_integrate_kernel<false, false, false, true>),
       vpt::kBlockThreads, 0));
   ctx->lat_per_cu = std::max(1, std::min(lat_per_cu, per_cu));
   int compact_per_cu = 0;
   VPT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &compact_per_cu, temperature ? vpt::vpt_integrate_kernel<true, false, false, true, true>
+      &compact_per_cu, has_temperature ? vpt::vpt_integrate_kernel<true, false, false, true, true>
                                    : (ctx->use_runs ? vpt::vpt_integrate_kernel<false, false, true, true, true>
                                                     : vpt::vpt_integrate_kernel<false, false, false, true, true>),
       vpt::kBlockThreads, vpt::kXchgBytes));
@@ -634,7 +638,7 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   // < 8 lanes are walking; the walk loops while >= 4 lanes walk (r02 sweep: 6:8:36:4 363.7 ms vs
   // 6:12:32:4 366.6 ms, C4 103.7 vs 104.4).  The temperature kernel's rare blocks wait for 8 lanes since the film
   // regroup (C4 83.3-83.6 vs 83.9-84.3 ms over 4 alternating runs, profiles/archive/r05gates2_c4_gate_min.txt).
-  ctx->scene.gate_min = temperature ? 8 : 6;
+  ctx->scene.gate_min = has_temperature ? 8 : 6;
   ctx->scene.gate_idle = 8;
   ctx->scene.gate_eval = 36;
   ctx->scene.gate_walk = 4;
@@ -646,6 +650,60 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   if ((rc = push_scene(ctx.get()))) return rc;
   lap(2);
   *out = ctx.release();
+  return VPT_OK;
+}
+
+int check_device(int device, const char* what) {
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev <= 0)
+    return vpt::set_error(VPT_E_HIP, std::string(what) + ": no HIP device (the integrator has no CPU fallback)");
+  if (device < 0 || device >= ndev) return vpt::set_error(VPT_E_INVALID, std::string(what) + ": bad device index");
+  return VPT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, const vpt_grid_desc* temperature,
+                   const float* blackbody_500x3, int device, vpt_gpu_ctx** out) {
+  if (!cfg || !density || !out) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_create: null argument");
+  *out = nullptr;
+  if (int rc = check_device(device, "vpt_gpu_create")) return rc;
+  HostGrids g;
+  double ms = 0;
+  if (int rc = build_grids(density, temperature, g, &ms)) return rc;
+  return create_on(cfg, g, temperature, blackbody_500x3, device, ms, out);
+}
+
+int vpt_gpu_create_many(const vpt_configuration* cfg, const vpt_grid_desc* density, const vpt_grid_desc* temperature,
+                        const float* blackbody_500x3, const int* devices, int n, vpt_gpu_ctx** out) {
+  if (!cfg || !density || !out || !devices || n <= 0) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_create_many: bad argument");
+  for (int i = 0; i < n; ++i) out[i] = nullptr;
+  for (int i = 0; i < n; ++i)
+    if (int rc = check_device(devices[i], "vpt_gpu_create_many")) return rc;
+  HostGrids g;
+  double ms = 0;
+  if (int rc = build_grids(density, temperature, g, &ms)) return rc;
+  // one thread per device: each uploads the same host grids (vpt_last_error is per thread: the first failure's
+  // message is carried back)
+  std::vector<int> rcs((size_t)n, VPT_OK);
+  std::vector<std::string> msgs((size_t)n);
+  std::vector<std::thread> pool;
+  for (int i = 0; i < n; ++i)
+    pool.emplace_back([&, i] {
+      rcs[(size_t)i] = create_on(cfg, g, temperature, blackbody_500x3, devices[i], ms, &out[i]);
+      if (rcs[(size_t)i]) msgs[(size_t)i] = vpt_last_error();
+    });
+  for (auto& th : pool) th.join();
+  for (int i = 0; i < n; ++i)
+    if (rcs[(size_t)i]) {
+      for (int k = 0; k < n; ++k) {
+        destroy(out[k]);
+        out[k] = nullptr;
+      }
+      return vpt::set_error(rcs[(size_t)i], "device " + std::to_string(devices[i]) + ": " + msgs[(size_t)i]);
+    }
   return VPT_OK;
 }
 

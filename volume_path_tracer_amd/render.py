@@ -110,11 +110,45 @@ class Integrator:
                                     C.byref(temp_desc) if temp_desc is not None else None,
                                     bb.ctypes.data_as(C.POINTER(C.c_float)) if bb is not None else None,
                                     self.device, C.byref(h)), "vpt_gpu_create")
+        self._attach(h)
+
+    def _attach(self, h) -> None:
         self.h = h
         jpw, tot = C.c_uint64(), C.c_uint64()
-        capi.check(L.vpt_gpu_job_space(h, C.byref(jpw), C.byref(tot)), "vpt_gpu_job_space")
+        capi.check(capi.lib().vpt_gpu_job_space(h, C.byref(jpw), C.byref(tot)), "vpt_gpu_job_space")
         self.jobs_per_wave, self.total_jobs = int(jpw.value), int(tot.value)
-        self.film = torch.zeros((self.cfg.height, self.cfg.width, 4), dtype=torch.float32, device=self.dev)
+        self.film = self.torch.zeros((self.cfg.height, self.cfg.width, 4), dtype=self.torch.float32, device=self.dev)
+
+    @classmethod
+    def create_many(cls, cfg: capi.Configuration, density, temperature=None, devices=(0,)) -> list:
+        """One Integrator per device with the grids flattened once (vpt_gpu_create_many, what the multi-GPU drop-in
+        uses); devices may repeat (several contexts on one GPU)."""
+        import torch
+
+        L = capi.lib()
+        dens_desc = density.desc if hasattr(density, "desc") else density
+        temp_desc = None if temperature is None else (temperature.desc if hasattr(temperature, "desc") else temperature)
+        n = len(devices)
+        devs = (C.c_int * n)(*[int(d) for d in devices])
+        hs = (C.c_void_p * n)()
+        cfg_c = cfg.copy()
+        capi.check(L.vpt_gpu_create_many(C.byref(cfg_c), C.byref(dens_desc),
+                                         C.byref(temp_desc) if temp_desc is not None else None, None, devs, n, hs),
+                   "vpt_gpu_create_many")
+        out = []
+        for d, h in zip(devices, hs):
+            it = cls.__new__(cls)
+            it.torch, it.cfg, it.device = torch, cfg.copy(), int(d)
+            it.dev = torch.device("cuda", it.device)
+            it._attach(C.c_void_p(h))
+            out.append(it)
+        return out
+
+    def setup_timings(self) -> dict:
+        """vpt_gpu_setup_timings (ms): flatten + majorant fix, upload, the rest, tile costs, device bind."""
+        ms = (C.c_double * 5)()
+        capi.check(capi.lib().vpt_gpu_setup_timings(self.h, ms, 5), "vpt_gpu_setup_timings")
+        return dict(zip(("flatten_fix", "upload", "rest", "tile_costs", "bind"), (float(x) for x in ms)))
 
     def __del__(self):
         try:
