@@ -240,8 +240,10 @@ int vpt_gpu_render_jobs(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count
  *     whole waves at a time where the range allows -- the same film.
  *   VPT_FILM_ATOMIC: fp32 atomics as samples complete (the order varies run to run, ≈1e-7 relative).
  * Debug launches (records, events) and feeds always add atomically; so does a launch whose buffer would
- * have to grow while a feed of the context is open.  Takes effect at the next launch; VPT_FILM_ATOMIC
- * frees the buffer. */
+ * have to grow while a feed of the context is open.  Growing the buffer frees and allocates device memory,
+ * which may wait for the whole device (see the feeds below): with feeds of other contexts open on the same
+ * device, size it beforehand (a first ordered launch of the largest range, or max_bytes).  Takes effect at
+ * the next launch; VPT_FILM_ATOMIC frees the buffer. */
 enum { VPT_FILM_ATOMIC = 0, VPT_FILM_ORDERED = 1 };
 int vpt_gpu_set_film_order(vpt_gpu_ctx* ctx, int mode, uint64_t max_bytes);
 /* The film mode, the sample buffer's size and the launches that ran ordered / atomic (feeds not counted). */
