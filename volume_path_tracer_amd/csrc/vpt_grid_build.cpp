@@ -459,7 +459,8 @@ int build_host_grid(const vpt_grid_desc& d, bool fix, int threads, HostGrid& out
   G.root = out.root.data();
 
   // --- bricks: 8^3 leaf voxels + the +1 apron ------------------------------------------------
-  out.bricks.assign((size_t)nleaf * 729, 0.0f);  // 9^3 apron bricks first (expanded into stencils below)
+  // 9^3 apron bricks first (expanded into stencils below); every element is written below (interior, then apron)
+  out.bricks.resize((size_t)nleaf * 729);
   G.bricks = out.bricks.data();
   // interior first (the apron reads neighbours' interiors through value_at)
   parallel_for((int64_t)nleaf, threads, [&](int64_t b, int64_t e) {
@@ -490,9 +491,9 @@ int build_host_grid(const vpt_grid_desc& d, bool fix, int threads, HostGrid& out
 
   {
     // expand the apron bricks into square rows (per row (y, z) the 2x2 squares of x = 0..8)
-    std::vector<float> apron;
+    std::vector<float, NoInitAllocator<float>> apron;
     apron.swap(out.bricks);
-    out.bricks.assign((size_t)nleaf * kBrickVox, 0.0f);
+    out.bricks.resize((size_t)nleaf * kBrickVox);  // (every square of every row is written below)
     parallel_for((int64_t)nleaf, threads, [&](int64_t b, int64_t e) {
       for (int64_t n = b; n < e; ++n) {
         const float* src = apron.data() + (size_t)n * 729;

@@ -2,7 +2,9 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/vpt_gpu.h"
@@ -13,12 +15,34 @@ namespace vpt {
 // Thread-local error message behind vpt_last_error().
 int set_error(int code, const std::string& msg);
 
+// An allocator whose value-less construct() leaves the element uninitialised: resize() of a large buffer that
+// is written in full afterwards (the stencil pool: 0.84 GB for the 512^3 cloud) skips a serial zero-fill, and its
+// pages are first touched by the threads that fill them.
+template <class T>
+struct NoInitAllocator : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInitAllocator<U>;
+  };
+  NoInitAllocator() = default;
+  template <class U>
+  NoInitAllocator(const NoInitAllocator<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
+};
+
 // A grid flattened for the GPU (host copies; vpt_gpu.hip uploads them).
 struct HostGrid {
   DevGrid dev{};  // pointers are filled in after upload
   std::vector<int2> cells8, cells128;
   std::vector<RootTileDev> root;
-  std::vector<float> bricks;     // [leaf][729]
+  std::vector<float, NoInitAllocator<float>> bricks;  // [leaf][kBrickVox] square rows (built via [leaf][729] aprons)
   std::vector<float> leaf_max;   // fixed majorants
   std::vector<uint8_t> runs8;    // run radius per cells8 entry (compute_runs; empty until then)
   std::vector<uint32_t> walk8;   // HDDA fast-path table (build_walk_table)
@@ -67,8 +91,9 @@ int blackbody_rows_suffice(const vpt_grid_desc& t, float scale, float offset, in
 struct OwnedGrid {
   vpt_grid_desc d{};
   std::vector<int32_t> leaf_origin, tile_origin, tile_level, lower_origin, upper_origin;
-  std::vector<float> leaf_values, leaf_max, tile_value;
-  std::vector<uint64_t> leaf_mask;
+  std::vector<float, NoInitAllocator<float>> leaf_values;  // (filled by copies: no zero-fill first)
+  std::vector<float> leaf_max, tile_value;
+  std::vector<uint64_t, NoInitAllocator<uint64_t>> leaf_mask;
   std::vector<uint8_t> tile_active;
   void finish();  // points d's arrays at the vectors
 };

@@ -100,6 +100,13 @@ int flatten(const Buf& b, OwnedGrid& o) {
   if (!b.has(root + (int64_t)kRootData, (size_t)table * kRootTile)) return bad("root table outside the buffer");
   if (table > (1u << 20)) return bad("implausible root table size");
   const float bg = d.background;
+  {  // TreeData::mNodeCount[0], the leaf count: room for the leaves' copies up front (capped by the buffer)
+    const uint64_t leaves = std::min<uint64_t>(b.at<uint32_t>(kGridData + 32), b.n / kLeafSize);
+    o.leaf_values.reserve(leaves * 512);
+    o.leaf_mask.reserve(leaves * 8);
+    o.leaf_max.reserve(leaves);
+    o.leaf_origin.reserve(leaves * 3);
+  }
   for (uint32_t t = 0; t < table; ++t) {
     const int64_t e = root + (int64_t)kRootData + (int64_t)t * kRootTile;
     const uint64_t key = b.at<uint64_t>(e);
