@@ -796,9 +796,10 @@ inline int device_limit(int n) {
 // reports (the bench's `first_call`).  Written by that call's thread; read after it has returned.
 struct RunPhases {
   int devices = 0;
-  double hip_ms = 0;          // the HIP runtime's start (the process's first HIP call: the device count)
   double first_batch_ms = 0;  // the first batch of tokens (the tile size is read off it)
-  double seed_ms = 0;         // the RandomNumberGenerator's private seed, recovered on the GPU
+  double hip_ms = 0;          // the HIP runtime's start (the process's first HIP call: the device count) and
+  double seed_ms = 0;         // the RandomNumberGenerator's private seed, recovered on the GPU -- both on a helper
+                              // thread, beside:
   double nanogrid_ms = 0;     // the NanoGrid<float>s read into grid descriptions (vpt_grid_from_nanovdb)
   double contexts_ms = 0;     // vpt_gpu_create + feed memory + tile costs on every GPU (in parallel)
   double setup_ms[5] = {};    // the first GPU's share of that: flatten + majorant fix, upload, the rest, tile costs, bind
@@ -827,14 +828,6 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
     t = now;
   };
   RunPhases ph;
-  int ndev = 0;
-  if (vpt_gpu_device_count(&ndev) || ndev <= 0) {
-    std::fprintf(stderr, "vpt_gpu::run: no HIP device (the integrator has no CPU fallback)\n");
-    return VPT_E_HIP;
-  }
-  ndev = detail::device_limit(ndev);
-  lap(ph.hip_ms);
-
   const auto size = film.size();
   const int64_t W = (int64_t)size.x(), H = (int64_t)size.y();
   // First batch of tokens: the tile size is the largest rect (tile_provider.cpp:95-105 clips only the
@@ -854,13 +847,34 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   }
   lap(ph.first_batch_ms);
 
+  // The HIP runtime's start and the seed recovery (one GPU launch) run on a helper thread while this one reads
+  // the NanoGrids (host work): their phases overlap.
   vpt_configuration cfg;
   std::memset(&cfg, 0, sizeof cfg);
-  if (int rc = detail::rng_seed(rng, cfg.seed, 0)) {
-    std::fprintf(stderr, "vpt_gpu::run: the RandomNumberGenerator's seed could not be determined\n");
-    return rc;
-  }
-  lap(ph.seed_ms);
+  int ndev = 0, gpu_rc = VPT_OK;
+  std::thread gpu_side([&] {
+    auto g0 = clk::now();
+    if (vpt_gpu_device_count(&ndev) || ndev <= 0) {
+      std::fprintf(stderr, "vpt_gpu::run: no HIP device (the integrator has no CPU fallback)\n");
+      gpu_rc = VPT_E_HIP;
+      return;
+    }
+    ph.hip_ms = std::chrono::duration<double, std::milli>(clk::now() - g0).count();
+    g0 = clk::now();
+    if ((gpu_rc = detail::rng_seed(rng, cfg.seed, 0)))  // (vpt_last_error is per thread: say it here)
+      std::fprintf(stderr, "vpt_gpu::run: the RandomNumberGenerator's seed could not be determined (%s)\n", vpt_last_error());
+    ph.seed_ms = std::chrono::duration<double, std::milli>(clk::now() - g0).count();
+  });
+  const auto& grids = vol.grids();
+  detail::OwnedDesc dens, temp;
+  int grid_rc = vpt_grid_from_nanovdb(&grids.density(), (size_t)grids.density().gridSize(), &dens.d);
+  if (grid_rc == VPT_OK && grids.has_temperature())
+    grid_rc = vpt_grid_from_nanovdb(&grids.temperature(), (size_t)grids.temperature().gridSize(), &temp.d);
+  lap(ph.nanogrid_ms);
+  gpu_side.join();
+  if (grid_rc) return grid_rc;
+  if (gpu_rc) return gpu_rc;
+  ndev = detail::device_limit(ndev);  // (contexts_ms below includes any wait for the helper)
   cfg.num_waves = 1;  // the provider decides which waves run; the context renders any job id
   cfg.num_workers = 1;
   cfg.output_size[0] = W;
@@ -888,12 +902,6 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   cfg.volume_parameters = vpt_volume_params{vp.henyey_greenstein_g, vp.le_scale,          vp.sigma_a,
                                             vp.sigma_s,             vp.temperature_offset, vp.temperature_scale};
 
-  const auto& grids = vol.grids();
-  detail::OwnedDesc dens, temp;
-  if (int rc = vpt_grid_from_nanovdb(&grids.density(), (size_t)grids.density().gridSize(), &dens.d)) return rc;
-  if (grids.has_temperature())
-    if (int rc = vpt_grid_from_nanovdb(&grids.temperature(), (size_t)grids.temperature().gridSize(), &temp.d)) return rc;
-  lap(ph.nanogrid_ms);
 
   // A context per GPU: the grids flattened and majorant-fixed once, uploaded to every device in parallel
   // (vpt_gpu_create_many); the feed's pinned ring and copy buffers and the tile costs of its cost tail are setup
