@@ -801,7 +801,9 @@ struct RunPhases {
   double seed_ms = 0;         // the RandomNumberGenerator's private seed, recovered on the GPU -- both on a helper
                               // thread, beside:
   double nanogrid_ms = 0;     // the NanoGrid<float>s read into grid descriptions (vpt_grid_from_nanovdb)
-  double contexts_ms = 0;     // vpt_gpu_create + feed memory + tile costs on every GPU (in parallel)
+  double wait_ms = 0;         // then the wait for the helper thread
+  double contexts_ms = 0;     // vpt_gpu_create_many + feed memory + tile costs on every GPU (in parallel)
+  double feeds_ms = 0;        // the share of contexts_ms after vpt_gpu_create_many: feed memory + tile costs
   double setup_ms[5] = {};    // the first GPU's share of that: flatten + majorant fix, upload, the rest, tile costs, bind
   double frame_ms = 0;        // drain_devices: the frame itself
   double total_ms = 0;        // the whole run() call
@@ -872,9 +874,10 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
     grid_rc = vpt_grid_from_nanovdb(&grids.temperature(), (size_t)grids.temperature().gridSize(), &temp.d);
   lap(ph.nanogrid_ms);
   gpu_side.join();
+  lap(ph.wait_ms);
   if (grid_rc) return grid_rc;
   if (gpu_rc) return gpu_rc;
-  ndev = detail::device_limit(ndev);  // (contexts_ms below includes any wait for the helper)
+  ndev = detail::device_limit(ndev);
   cfg.num_waves = 1;  // the provider decides which waves run; the context renders any job id
   cfg.num_workers = 1;
   cfg.output_size[0] = W;
@@ -917,6 +920,7 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   std::vector<int> devices((size_t)ndev);
   for (int d = 0; d < ndev; ++d) devices[(size_t)d] = d;
   if (int rc = vpt_gpu_create_many(&cfg, dens.d, temp.d, nullptr, devices.data(), ndev, ctxs.data())) return rc;
+  const auto t_feeds = clk::now();
   std::vector<int> crc((size_t)ndev, VPT_OK);
   auto prepare = [&](int d) {
     int rc = vpt_gpu_feed_prepare(ctxs[(size_t)d], 0, 1);
@@ -934,6 +938,7 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   }
   for (int rc : crc)
     if (rc) return rc;
+  ph.feeds_ms = std::chrono::duration<double, std::milli>(clk::now() - t_feeds).count();
   lap(ph.contexts_ms);
   (void)vpt_gpu_setup_timings(ctxs[0], ph.setup_ms, 5);
   ph.devices = ndev;

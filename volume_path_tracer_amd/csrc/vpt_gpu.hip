@@ -540,13 +540,42 @@ struct HostGrids {
 };
 int build_grids(const vpt_grid_desc* density, const vpt_grid_desc* temperature, HostGrids& g, double* ms) {
   const auto t0 = std::chrono::steady_clock::now();
+  // The temperature grid is flattened on a thread of its own beside the density's: each build has serial
+  // stretches (node sets, leaf loops) and page-faults its fresh tables in (vpt_last_error is per thread: the
+  // temperature's message is carried back).
+  int trc = VPT_OK;
+  std::string tmsg;
+  std::thread temp_build;
+  if (temperature)
+    temp_build = std::thread([&] {
+      if ((trc = vpt::build_host_grid(*temperature, false, 0, g.temperature))) tmsg = vpt_last_error();
+    });
   int rc = vpt::build_host_grid(*density, true, 0, g.density);
+  if (rc == VPT_OK) vpt::compute_runs(g.density, 0);
+  if (temp_build.joinable()) temp_build.join();
   if (rc) return rc;
-  vpt::compute_runs(g.density, 0);
-  if (temperature && (rc = vpt::build_host_grid(*temperature, false, 0, g.temperature))) return rc;
+  if (trc) return vpt::set_error(trc, tmsg);
   g.has_temperature = temperature != nullptr;
   if (ms) *ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return VPT_OK;
+}
+
+// The host copies of the flattened grids (~1 GB for the 512^3 stand-ins: the stencil pool, the cell and walk
+// tables) are released on a thread of their own once every context has its upload: unmapping that many freshly
+// faulted pages is not free, and the caller (a reference run(): frame next) need not wait for it.  The thread is
+// joined before the next release and at exit.
+void release_later(std::unique_ptr<HostGrids> g) {
+  struct Reaper {
+    std::mutex m;
+    std::thread th;
+    ~Reaper() {
+      if (th.joinable()) th.join();
+    }
+  };
+  static Reaper r;
+  std::lock_guard<std::mutex> lk(r.m);
+  if (r.th.joinable()) r.th.join();
+  r.th = std::thread([q = std::move(g)]() mutable { q.reset(); });
 }
 
 // A context on `device` from grids already flattened (vpt_gpu_create, vpt_gpu_create_many).
@@ -670,10 +699,12 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   if (!cfg || !density || !out) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_create: null argument");
   *out = nullptr;
   if (int rc = check_device(device, "vpt_gpu_create")) return rc;
-  HostGrids g;
+  auto g = std::make_unique<HostGrids>();
   double ms = 0;
-  if (int rc = build_grids(density, temperature, g, &ms)) return rc;
-  return create_on(cfg, g, temperature, blackbody_500x3, device, ms, out);
+  if (int rc = build_grids(density, temperature, *g, &ms)) return rc;
+  const int rc = create_on(cfg, *g, temperature, blackbody_500x3, device, ms, out);
+  release_later(std::move(g));
+  return rc;
 }
 
 int vpt_gpu_create_many(const vpt_configuration* cfg, const vpt_grid_desc* density, const vpt_grid_desc* temperature,
@@ -682,7 +713,8 @@ int vpt_gpu_create_many(const vpt_configuration* cfg, const vpt_grid_desc* densi
   for (int i = 0; i < n; ++i) out[i] = nullptr;
   for (int i = 0; i < n; ++i)
     if (int rc = check_device(devices[i], "vpt_gpu_create_many")) return rc;
-  HostGrids g;
+  auto gp = std::make_unique<HostGrids>();
+  HostGrids& g = *gp;
   double ms = 0;
   if (int rc = build_grids(density, temperature, g, &ms)) return rc;
   // one thread per device: each uploads the same host grids (vpt_last_error is per thread: the first failure's
@@ -704,6 +736,7 @@ int vpt_gpu_create_many(const vpt_configuration* cfg, const vpt_grid_desc* densi
       }
       return vpt::set_error(rcs[(size_t)i], "device " + std::to_string(devices[i]) + ": " + msgs[(size_t)i]);
     }
+  release_later(std::move(gp));
   return VPT_OK;
 }
 
