@@ -202,6 +202,16 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density,
 int vpt_gpu_create_many(const vpt_configuration* cfg, const vpt_grid_desc* density,
                         const vpt_grid_desc* temperature, const float* blackbody_500x3, const int* devices, int n,
                         vpt_gpu_ctx** out);
+/* The two halves of vpt_gpu_create_many, for a caller that flattens the grids while the HIP runtime starts
+ * (vpt_gpu::run: the flatten is host work and needs no device).  vpt_grids_flatten: the host side of
+ * Volume::Volume -- the grids flattened and the density's majorants fixed (no HIP call; the caller's arrays may be
+ * freed afterwards).  vpt_gpu_create_from: a context per device from those grids, as vpt_gpu_create_many.  The
+ * grids stay the caller's until vpt_grids_free. */
+typedef struct vpt_host_grids vpt_host_grids;
+int vpt_grids_flatten(const vpt_grid_desc* density, const vpt_grid_desc* temperature, vpt_host_grids** out);
+int vpt_gpu_create_from(const vpt_configuration* cfg, const vpt_host_grids* grids, const float* blackbody_500x3,
+                        const int* devices, int n, vpt_gpu_ctx** out);
+void vpt_grids_free(vpt_host_grids* grids);
 int vpt_gpu_destroy(vpt_gpu_ctx* ctx);
 
 /* Jobs per wave T and total jobs num_waves*T of the context's configuration. */

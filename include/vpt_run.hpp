@@ -783,6 +783,10 @@ struct OwnedDesc {
     if (d) vpt_grid_free(d);
   }
 };
+struct OwnedGrids {
+  vpt_host_grids* g = nullptr;
+  ~OwnedGrids() { vpt_grids_free(g); }
+};
 
 // VPT_DEVICES=n: use at most n of the process's HIP devices (A/B runs); default all of them.
 inline int device_limit(int n) {
@@ -800,11 +804,13 @@ struct RunPhases {
   double hip_ms = 0;          // the HIP runtime's start (the process's first HIP call: the device count) and
   double seed_ms = 0;         // the RandomNumberGenerator's private seed, recovered on the GPU -- both on a helper
                               // thread, beside:
-  double nanogrid_ms = 0;     // the NanoGrid<float>s read into grid descriptions (vpt_grid_from_nanovdb)
+  double nanogrid_ms = 0;     // the NanoGrid<float>s read into grid descriptions (vpt_grid_from_nanovdb) and
+  double flatten_ms = 0;      // the grids flattened + the density's majorants fixed (vpt_grids_flatten)
   double wait_ms = 0;         // then the wait for the helper thread
-  double contexts_ms = 0;     // vpt_gpu_create_many + feed memory + tile costs on every GPU (in parallel)
-  double feeds_ms = 0;        // the share of contexts_ms after vpt_gpu_create_many: feed memory + tile costs
-  double setup_ms[5] = {};    // the first GPU's share of that: flatten + majorant fix, upload, the rest, tile costs, bind
+  double contexts_ms = 0;     // vpt_gpu_create_from + feed memory + tile costs on every GPU (in parallel)
+  double feeds_ms = 0;        // the share of contexts_ms after vpt_gpu_create_from: feed memory + tile costs
+  double setup_ms[5] = {};    // the first GPU's context: flatten + majorant fix (= flatten_ms), upload, the rest,
+                              // tile costs, bind
   double frame_ms = 0;        // drain_devices: the frame itself
   double total_ms = 0;        // the whole run() call
 };
@@ -850,7 +856,7 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   lap(ph.first_batch_ms);
 
   // The HIP runtime's start and the seed recovery (one GPU launch) run on a helper thread while this one reads
-  // the NanoGrids (host work): their phases overlap.
+  // the NanoGrids and flattens them (host work): their phases overlap.
   vpt_configuration cfg;
   std::memset(&cfg, 0, sizeof cfg);
   int ndev = 0, gpu_rc = VPT_OK;
@@ -873,6 +879,11 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   if (grid_rc == VPT_OK && grids.has_temperature())
     grid_rc = vpt_grid_from_nanovdb(&grids.temperature(), (size_t)grids.temperature().gridSize(), &temp.d);
   lap(ph.nanogrid_ms);
+  detail::OwnedGrids flat;
+  if (grid_rc == VPT_OK) grid_rc = vpt_grids_flatten(dens.d, temp.d, &flat.g);
+  lap(ph.flatten_ms);
+  if (grid_rc)  // (vpt_last_error is per thread: say it here)
+    std::fprintf(stderr, "vpt_gpu::run: the grids could not be read (%s)\n", vpt_last_error());
   gpu_side.join();
   lap(ph.wait_ms);
   if (grid_rc) return grid_rc;
@@ -906,8 +917,8 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
                                             vp.sigma_s,             vp.temperature_offset, vp.temperature_scale};
 
 
-  // A context per GPU: the grids flattened and majorant-fixed once, uploaded to every device in parallel
-  // (vpt_gpu_create_many); the feed's pinned ring and copy buffers and the tile costs of its cost tail are setup
+  // A context per GPU: the grids flattened and majorant-fixed once (above), uploaded to every device in parallel
+  // (vpt_gpu_create_from); the feed's pinned ring and copy buffers and the tile costs of its cost tail are setup
   // too, like the grid upload.
   std::vector<vpt_gpu_ctx*> ctxs((size_t)ndev, nullptr);
   struct Ctxs {
@@ -919,7 +930,9 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   } guard{ctxs};
   std::vector<int> devices((size_t)ndev);
   for (int d = 0; d < ndev; ++d) devices[(size_t)d] = d;
-  if (int rc = vpt_gpu_create_many(&cfg, dens.d, temp.d, nullptr, devices.data(), ndev, ctxs.data())) return rc;
+  if (int rc = vpt_gpu_create_from(&cfg, flat.g, nullptr, devices.data(), ndev, ctxs.data())) return rc;
+  vpt_grids_free(flat.g);  // (the host copies: the devices hold theirs)
+  flat.g = nullptr;
   const auto t_feeds = clk::now();
   std::vector<int> crc((size_t)ndev, VPT_OK);
   auto prepare = [&](int d) {

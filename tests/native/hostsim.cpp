@@ -99,7 +99,7 @@ extern "C" int vpths_render_jobs_order(const vpt_configuration* cfg, const vpt_g
     if ((rc = vpt::build_host_grid(*temperature, false, 0, ht))) return rc;
     S.temperature = ht.dev;
     S.has_temperature = 1;
-    S.bb_lds_ok = vpt::blackbody_rows_suffice(*temperature, cfg->volume_parameters.temperature_scale,
+    S.bb_lds_ok = vpt::blackbody_rows_suffice(vpt::value_range(*temperature, 0), cfg->volume_parameters.temperature_scale,
                                               cfg->volume_parameters.temperature_offset, vpt::kBbLdsRows);
   }
   std::vector<float> bb(501 * 3, 0.0f);

@@ -223,9 +223,9 @@ int main(int argc, char** argv) {
     // what the call cost, as main.cpp:65-84 times it (the whole run(); its phases)
     const vpt_gpu::RunPhases& ph = vpt_gpu::run_phases();
     std::printf("run_gpu_harness: phases devices=%d total_ms=%.1f hip_ms=%.1f first_batch_ms=%.1f seed_ms=%.1f "
-                "nanogrid_ms=%.1f wait_ms=%.1f contexts_ms=%.1f feeds_ms=%.1f flatten_fix_ms=%.1f upload_ms=%.1f ctx_rest_ms=%.1f tile_costs_ms=%.1f "
+                "nanogrid_ms=%.1f flatten_ms=%.1f wait_ms=%.1f contexts_ms=%.1f feeds_ms=%.1f flatten_fix_ms=%.1f upload_ms=%.1f ctx_rest_ms=%.1f tile_costs_ms=%.1f "
                 "bind_ms=%.1f frame_ms=%.1f\n",
-                ph.devices, ph.total_ms, ph.hip_ms, ph.first_batch_ms, ph.seed_ms, ph.nanogrid_ms, ph.wait_ms, ph.contexts_ms,
+                ph.devices, ph.total_ms, ph.hip_ms, ph.first_batch_ms, ph.seed_ms, ph.nanogrid_ms, ph.flatten_ms, ph.wait_ms, ph.contexts_ms,
                 ph.feeds_ms, ph.setup_ms[0], ph.setup_ms[1], ph.setup_ms[2], ph.setup_ms[3], ph.setup_ms[4], ph.frame_ms);
   } else {
     vpt_grid_desc *dens = nullptr, *temp = nullptr;

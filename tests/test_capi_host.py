@@ -111,6 +111,29 @@ def test_gpu_create_fails_loudly_without_device():
     assert rc == 2 and b"no HIP device" in capi.lib().vpt_last_error()
 
 
+def test_grids_flatten_needs_no_device_and_create_from_fails_loudly_without_one():
+    """vpt_grids_flatten is host work (run() overlaps it with the HIP runtime's start); the contexts made from its
+    grids need a device, and say so without one."""
+    import torch
+    from volume_path_tracer_amd.scenes import SynthGrid, workload
+    L = capi.lib()
+    wl = workload("c4", width=16, height=16, spp=1, grid_n=32)
+    d, t = SynthGrid(1, 32), SynthGrid(2, 32)
+    g = C.c_void_p()
+    assert L.vpt_grids_flatten(C.byref(d.desc), C.byref(t.desc), C.byref(g)) == 0 and g.value
+    L.vpt_grids_free(g)
+    assert L.vpt_grids_flatten(None, None, C.byref(g)) == 1  # VPT_E_INVALID
+    g2 = C.c_void_p()
+    assert L.vpt_grids_flatten(C.byref(d.desc), None, C.byref(g2)) == 0 and g2.value
+    if not torch.cuda.is_available():
+        devs = (C.c_int * 1)(0)
+        outs = (C.c_void_p * 1)()
+        rc = L.vpt_gpu_create_from(C.byref(wl.cfg), g2, None, devs, 1, outs)
+        assert rc == 2 and b"no HIP device" in L.vpt_last_error() and not outs[0]
+    L.vpt_grids_free(g2)
+    L.vpt_grids_free(None)
+
+
 def test_tile_provider_semantics():
     tp = TileProvider((20, 10), 3, (8, 8))
     assert tp.num_tiles == 3 * 2

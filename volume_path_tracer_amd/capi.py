@@ -225,6 +225,11 @@ def lib() -> C.CDLL:
     L.vpt_gpu_create.argtypes = [cfgp, gridp, gridp, fp, C.c_int, C.POINTER(vp)]
     if hasattr(L, "vpt_gpu_create_many"):
         L.vpt_gpu_create_many.argtypes = [cfgp, gridp, gridp, fp, C.POINTER(C.c_int), C.c_int, C.POINTER(vp)]
+    if hasattr(L, "vpt_grids_flatten"):
+        L.vpt_grids_flatten.argtypes = [gridp, gridp, C.POINTER(vp)]
+        L.vpt_gpu_create_from.argtypes = [cfgp, vp, fp, C.POINTER(C.c_int), C.c_int, C.POINTER(vp)]
+        L.vpt_grids_free.argtypes = [vp]
+        L.vpt_grids_free.restype = None
     L.vpt_gpu_destroy.argtypes = [vp]
     L.vpt_gpu_job_space.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.vpt_gpu_render_jobs.argtypes = [vp, C.c_uint64, C.c_uint64, vp, vp]

@@ -530,14 +530,19 @@ int vpt_gpu_find_seeds(int device, uint32_t out0, uint32_t out1, uint32_t* seeds
 
 }  // extern "C"
 
-namespace {
 // The host side of Volume::Volume: the grids flattened (leaf-slot and walk tables, the stencil pool) with the
-// density's majorants fixed for interpolation (volume.cpp:162-170; temperature is only sampled).  ms[0] += the
-// time taken.
-struct HostGrids {
+// density's majorants fixed for interpolation (volume.cpp:162-170; temperature is only sampled) -- the ABI's
+// vpt_host_grids (vpt_grids_flatten), uploaded by create_on.
+struct vpt_host_grids {
   vpt::HostGrid density, temperature;
   bool has_temperature = false;
+  vpt::ValueRange temp_range;  // the temperature grid's value extremes (blackbody_rows_suffice)
+  double flatten_ms = 0;
 };
+
+namespace {
+using HostGrids = vpt_host_grids;
+// ms[0] += the time taken.
 int build_grids(const vpt_grid_desc* density, const vpt_grid_desc* temperature, HostGrids& g, double* ms) {
   const auto t0 = std::chrono::steady_clock::now();
   // The temperature grid is flattened on a thread of its own beside the density's: each build has serial
@@ -548,7 +553,10 @@ int build_grids(const vpt_grid_desc* density, const vpt_grid_desc* temperature, 
   std::thread temp_build;
   if (temperature)
     temp_build = std::thread([&] {
-      if ((trc = vpt::build_host_grid(*temperature, false, 0, g.temperature))) tmsg = vpt_last_error();
+      if ((trc = vpt::build_host_grid(*temperature, false, 0, g.temperature)))
+        tmsg = vpt_last_error();
+      else
+        g.temp_range = vpt::value_range(*temperature, 0);
     });
   int rc = vpt::build_host_grid(*density, true, 0, g.density);
   if (rc == VPT_OK) vpt::compute_runs(g.density, 0);
@@ -560,32 +568,14 @@ int build_grids(const vpt_grid_desc* density, const vpt_grid_desc* temperature, 
   return VPT_OK;
 }
 
-// The host copies of the flattened grids (~1 GB for the 512^3 stand-ins: the stencil pool, the cell and walk
-// tables) are released on a thread of their own once every context has its upload: unmapping that many freshly
-// faulted pages is not free, and the caller (a reference run(): frame next) need not wait for it.  The thread is
-// joined before the next release and at exit.
-void release_later(std::unique_ptr<HostGrids> g) {
-  struct Reaper {
-    std::mutex m;
-    std::thread th;
-    ~Reaper() {
-      if (th.joinable()) th.join();
-    }
-  };
-  static Reaper r;
-  std::lock_guard<std::mutex> lk(r.m);
-  if (r.th.joinable()) r.th.join();
-  r.th = std::thread([q = std::move(g)]() mutable { q.reset(); });
-}
-
 // A context on `device` from grids already flattened (vpt_gpu_create, vpt_gpu_create_many).
-int create_on(const vpt_configuration* cfg, const HostGrids& grids, const vpt_grid_desc* temperature,
-              const float* blackbody_500x3, int device, double flatten_ms, vpt_gpu_ctx** out) {
+int create_on(const vpt_configuration* cfg, const HostGrids& grids, const float* blackbody_500x3, int device,
+              vpt_gpu_ctx** out) {
   *out = nullptr;
   std::unique_ptr<vpt_gpu_ctx, void (*)(vpt_gpu_ctx*)> ctx(new vpt_gpu_ctx(), destroy);
   ctx->device = device;
   ctx->cfg = *cfg;
-  ctx->setup_ms[0] = flatten_ms;
+  ctx->setup_ms[0] = grids.flatten_ms;
   using clk = std::chrono::steady_clock;
   auto t = clk::now();
   auto lap = [&](int i) {  // setup phases (vpt_gpu_setup_timings)
@@ -609,7 +599,7 @@ int create_on(const vpt_configuration* cfg, const HostGrids& grids, const vpt_gr
   vpt::scene_finalize(ctx->scene);  // uses only the density map (host copy of the values)
   ctx->scene.temperature = ctx->temperature.dev;
   ctx->scene.has_temperature = has_temperature ? 1 : 0;
-  ctx->scene.bb_lds_ok = has_temperature ? vpt::blackbody_rows_suffice(*temperature, cfg->volume_parameters.temperature_scale,
+  ctx->scene.bb_lds_ok = has_temperature ? vpt::blackbody_rows_suffice(grids.temp_range, cfg->volume_parameters.temperature_scale,
                                                                     cfg->volume_parameters.temperature_offset, vpt::kBbLdsRows)
                                      : 0;
 
@@ -699,12 +689,9 @@ int vpt_gpu_create(const vpt_configuration* cfg, const vpt_grid_desc* density, c
   if (!cfg || !density || !out) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_create: null argument");
   *out = nullptr;
   if (int rc = check_device(device, "vpt_gpu_create")) return rc;
-  auto g = std::make_unique<HostGrids>();
-  double ms = 0;
-  if (int rc = build_grids(density, temperature, *g, &ms)) return rc;
-  const int rc = create_on(cfg, *g, temperature, blackbody_500x3, device, ms, out);
-  release_later(std::move(g));
-  return rc;
+  HostGrids g;
+  if (int rc = build_grids(density, temperature, g, &g.flatten_ms)) return rc;
+  return create_on(cfg, g, blackbody_500x3, device, out);
 }
 
 int vpt_gpu_create_many(const vpt_configuration* cfg, const vpt_grid_desc* density, const vpt_grid_desc* temperature,
@@ -713,10 +700,30 @@ int vpt_gpu_create_many(const vpt_configuration* cfg, const vpt_grid_desc* densi
   for (int i = 0; i < n; ++i) out[i] = nullptr;
   for (int i = 0; i < n; ++i)
     if (int rc = check_device(devices[i], "vpt_gpu_create_many")) return rc;
-  auto gp = std::make_unique<HostGrids>();
-  HostGrids& g = *gp;
-  double ms = 0;
-  if (int rc = build_grids(density, temperature, g, &ms)) return rc;
+  vpt_host_grids* g = nullptr;
+  if (int rc = vpt_grids_flatten(density, temperature, &g)) return rc;
+  const int rc = vpt_gpu_create_from(cfg, g, blackbody_500x3, devices, n, out);
+  vpt_grids_free(g);
+  return rc;
+}
+
+int vpt_grids_flatten(const vpt_grid_desc* density, const vpt_grid_desc* temperature, vpt_host_grids** out) {
+  if (!density || !out) return vpt::set_error(VPT_E_INVALID, "vpt_grids_flatten: null argument");
+  *out = nullptr;
+  std::unique_ptr<vpt_host_grids> g(new vpt_host_grids());
+  if (int rc = build_grids(density, temperature, *g, &g->flatten_ms)) return rc;
+  *out = g.release();
+  return VPT_OK;
+}
+
+void vpt_grids_free(vpt_host_grids* grids) { delete grids; }
+
+int vpt_gpu_create_from(const vpt_configuration* cfg, const vpt_host_grids* grids, const float* blackbody_500x3,
+                        const int* devices, int n, vpt_gpu_ctx** out) {
+  if (!cfg || !grids || !out || !devices || n <= 0) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_create_from: bad argument");
+  for (int i = 0; i < n; ++i) out[i] = nullptr;
+  for (int i = 0; i < n; ++i)
+    if (int rc = check_device(devices[i], "vpt_gpu_create_from")) return rc;
   // one thread per device: each uploads the same host grids (vpt_last_error is per thread: the first failure's
   // message is carried back)
   std::vector<int> rcs((size_t)n, VPT_OK);
@@ -724,7 +731,7 @@ int vpt_gpu_create_many(const vpt_configuration* cfg, const vpt_grid_desc* densi
   std::vector<std::thread> pool;
   for (int i = 0; i < n; ++i)
     pool.emplace_back([&, i] {
-      rcs[(size_t)i] = create_on(cfg, g, temperature, blackbody_500x3, devices[i], ms, &out[i]);
+      rcs[(size_t)i] = create_on(cfg, *grids, blackbody_500x3, devices[i], &out[i]);
       if (rcs[(size_t)i]) msgs[(size_t)i] = vpt_last_error();
     });
   for (auto& th : pool) th.join();
@@ -736,7 +743,6 @@ int vpt_gpu_create_many(const vpt_configuration* cfg, const vpt_grid_desc* densi
       }
       return vpt::set_error(rcs[(size_t)i], "device " + std::to_string(devices[i]) + ": " + msgs[(size_t)i]);
     }
-  release_later(std::move(gp));
   return VPT_OK;
 }
 

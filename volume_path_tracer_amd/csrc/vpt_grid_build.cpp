@@ -23,6 +23,7 @@
 #include <cmath>
 #include <cstring>
 #include <limits>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
@@ -537,6 +538,31 @@ int build_host_grid(const vpt_grid_desc& d, bool fix, int threads, HostGrid& out
   mark_interior(G, out.cells8, threads);
   build_walk_table(out, threads);
   return VPT_OK;
+}
+
+// The extremes of a grid's values, the leaf voxels scanned in parallel (blackbody_rows_suffice reads them: the
+// temperature grid's 46 M voxels took ~30 ms on one thread inside the context's creation).
+ValueRange value_range(const vpt_grid_desc& t, int threads) {
+  if (threads <= 0) threads = default_threads();
+  ValueRange r;
+  r.lo = r.hi = t.background;
+  r.finite = std::isfinite(t.background);
+  auto take = [](ValueRange& q, float v) {
+    q.lo = std::min(q.lo, v);
+    q.hi = std::max(q.hi, v);
+    q.finite = q.finite && std::isfinite(v);
+  };
+  for (uint64_t i = 0; i < t.tile_count; ++i) take(r, t.tile_value[i]);
+  std::mutex m;
+  parallel_for((int64_t)t.leaf_count, threads, [&](int64_t b, int64_t e) {
+    ValueRange q = r;
+    for (uint64_t i = (uint64_t)b * 512; i < (uint64_t)e * 512; ++i) take(q, t.leaf_values[i]);
+    std::lock_guard<std::mutex> lk(m);
+    r.lo = std::min(r.lo, q.lo);
+    r.hi = std::max(r.hi, q.hi);
+    r.finite = r.finite && q.finite;
+  });
+  return r;
 }
 
 // ------------------------------------------------------------------------------------------------

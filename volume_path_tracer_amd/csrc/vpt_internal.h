@@ -105,7 +105,12 @@ int default_threads();
 // trilinear value is a convex combination of getValue()s (leaf voxels, tile values, background), so
 // T = value * scale + offset (worker.cpp:152-157) lies between the extremes of those; one row of margin
 // covers the rounding of the lerps and of the two float operations.  0 for non-finite values.
-int blackbody_rows_suffice(const vpt_grid_desc& t, float scale, float offset, int rows);
+struct ValueRange {
+  float lo = 0, hi = 0;  // extremes of every getValue() of the grid (background, leaf voxels, tile values)
+  bool finite = true;    // all of them finite (lo / hi are then meaningful)
+};
+ValueRange value_range(const vpt_grid_desc& t, int threads);  // (threads <= 0: default_threads())
+int blackbody_rows_suffice(const ValueRange& r, float scale, float offset, int rows);
 
 // A vpt_grid_desc that owns its arrays (vpt_synth_grid, vpt_grid_from_nanovdb, vpt_grid_read_nvdb;
 // released by vpt_synth_free / vpt_grid_free).  d must stay the first member.

@@ -195,19 +195,9 @@ extern "C" int vpt_blackbody_table(float* out) {
 }
 
 namespace vpt {
-int blackbody_rows_suffice(const vpt_grid_desc& t, float scale, float offset, int rows) {
-  float lo = t.background, hi = t.background;
-  auto take = [&](float v) {
-    lo = std::min(lo, v);
-    hi = std::max(hi, v);
-    return std::isfinite(v);
-  };
-  if (!take(t.background)) return 0;
-  for (uint64_t i = 0; i < t.leaf_count * 512; ++i)
-    if (!take(t.leaf_values[i])) return 0;
-  for (uint64_t i = 0; i < t.tile_count; ++i)
-    if (!take(t.tile_value[i])) return 0;
-  const float tmax = std::max(lo * scale, hi * scale) + offset;
+int blackbody_rows_suffice(const ValueRange& r, float scale, float offset, int rows) {
+  if (!r.finite) return 0;
+  const float tmax = std::max(r.lo * scale, r.hi * scale) + offset;
   // rows dn and dn + 1 with dn <= floor(T / 100) + 1 (the search loops of blackbody_xyz), plus margin
   return std::isfinite(tmax) && tmax < (float)(rows - 3) * 100.0f ? 1 : 0;
 }
