@@ -931,8 +931,6 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   std::vector<int> devices((size_t)ndev);
   for (int d = 0; d < ndev; ++d) devices[(size_t)d] = d;
   if (int rc = vpt_gpu_create_from(&cfg, flat.g, nullptr, devices.data(), ndev, ctxs.data())) return rc;
-  vpt_grids_free(flat.g);  // (the host copies: the devices hold theirs)
-  flat.g = nullptr;
   const auto t_feeds = clk::now();
   std::vector<int> crc((size_t)ndev, VPT_OK);
   auto prepare = [&](int d) {
@@ -957,7 +955,12 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   ph.devices = ndev;
   float* film_host = reinterpret_cast<float*>(film.data().data());  // H x W x (X, Y, Z, W)
   // the first batch is queued first; then 4096 tokens per batch (a token is one 8x8 job: 64 samples)
+  // The host copies of the grids (the devices hold theirs) are released beside the frame: unmapping ~1 GB of
+  // pages took 58-97 ms on the box (r06o), which the GPU's first milliseconds of the frame hide.
+  std::thread release([g = flat.g] { vpt_grids_free(g); });
+  flat.g = nullptr;
   const int rc = drain_devices(ctxs, tp, film_host, 4096, DrainOptions{}, &runs);
+  release.join();
   lap(ph.frame_ms);
   ph.total_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
   run_phases() = ph;
