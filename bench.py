@@ -266,8 +266,10 @@ def first_call(wl, base, tmp, timeout_s):
     rec["film_counts_exact"] = bool((film[..., 3] == wl.spp).all())
     rec["note"] = ("total_ms = the whole run() call as main.cpp times it; the grid load itself (NanoVDB file read, "
                    "Volume ctor) happens before it in main.cpp:40-41 and is not in it. hip_ms + seed_ms run on a helper "
-                   "thread beside nanogrid_ms; wait_ms is the wait for it after the read. contexts_ms = the grids "
-                   "(flatten_fix_ms, upload_ms, ctx_rest_ms) + feeds_ms (the feed's pinned memory and tile_costs_ms)")
+                   "thread beside nanogrid_ms; wait_ms is the wait for it after the read. contexts_ms = the contexts "
+                   "(upload_ms, ctx_rest_ms) + feeds_ms (the feed's pinned memory and tile_costs_ms); flatten_ms runs "
+                   "beside the helper too. The host copies of the flattened grids are kept until the next run() or the "
+                   "process's exit, as the reference's Volume keeps its grids")
     return rec
 
 

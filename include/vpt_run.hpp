@@ -955,12 +955,13 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   ph.devices = ndev;
   float* film_host = reinterpret_cast<float*>(film.data().data());  // H x W x (X, Y, Z, W)
   // the first batch is queued first; then 4096 tokens per batch (a token is one 8x8 job: 64 samples)
-  // The host copies of the grids (the devices hold theirs) are released beside the frame: unmapping ~1 GB of
-  // pages took 58-97 ms on the box (r06o), which the GPU's first milliseconds of the frame hide.
-  std::thread release([g = flat.g] { vpt_grids_free(g); });
-  flat.g = nullptr;
+  // The host copies of the grids (the devices hold theirs) are kept until the next run() or the process's exit,
+  // as the reference's Volume keeps its grids: unmapping ~1 GB of pages took 58-97 ms on the box, and slowed the
+  // frame by 46-92 ms when done beside it (r06o, r06p: mmap-lock contention).  One run() drives the GPUs at a time
+  // (Leader), so the slot is never shared; flat now holds the previous call's copies, released at this call's end.
+  static detail::OwnedGrids kept;
+  std::swap(kept.g, flat.g);
   const int rc = drain_devices(ctxs, tp, film_host, 4096, DrainOptions{}, &runs);
-  release.join();
   lap(ph.frame_ms);
   ph.total_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
   run_phases() = ph;

@@ -2,7 +2,7 @@
 # r06l: run()'s phases with the helper-thread overlap and the two grids flattened side by side (first_call, C3 / C4),
 # and the GPU integration + film-order suites on that code (SESSION=r06m: the host grids released on a thread of
 # their own; r06n: huge pages; r06o: the flatten beside the HIP start, vpt_grids_flatten + vpt_gpu_create_from;
-# r06p: the host grids released beside the frame).
+# r06p: the host grids released beside the frame; r06q: kept until the next run() or exit).
 set -u
 export TMPDIR=/tmp
 O=gpurun_out/${SESSION:-r06l}; mkdir -p $O
