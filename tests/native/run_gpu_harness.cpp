@@ -220,6 +220,26 @@ int main(int argc, char** argv) {
     for (auto& t : pool) t.join();
     for (int i = 0; i < threads; ++i)
       if (rc[i]) return fail("vpt_gpu::run");
+    // frames=k: k - 1 more frames in this process, each with a fresh provider and film, as a caller that renders
+    // again would (the later calls release the previous call's host grid copies); `out` gets the last film
+    for (long long f = 1; f < num("frames", 1); ++f) {
+      vpt_headless::TileProvider tp2(cfg.output_size[0], cfg.output_size[1], cfg.num_waves, cfg.tile_size[0],
+                                     cfg.tile_size[1]);
+      vpt_headless::Image<float, 4> film2(cfg.output_size[0], cfg.output_size[1]);
+      const auto f0 = std::chrono::steady_clock::now();
+      std::vector<std::thread> pool2;
+      for (int i = 0; i < threads; ++i)
+        pool2.emplace_back([&, i] {
+          vpt_headless::RandomNumberGenerator rng(cfg.seed);
+          rc[i] = vpt_gpu::run_checked(params, vol, camera, tp2, film2, rng);
+        });
+      for (auto& t : pool2) t.join();
+      for (int i = 0; i < threads; ++i)
+        if (rc[i]) return fail("vpt_gpu::run (a later frame)");
+      std::printf("run_gpu_harness: frame %lld total_ms=%.1f\n", f,
+                  std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - f0).count());
+      film.px = film2.px;
+    }
     // what the call cost, as main.cpp:65-84 times it (the whole run(); its phases)
     const vpt_gpu::RunPhases& ph = vpt_gpu::run_phases();
     std::printf("run_gpu_harness: phases devices=%d total_ms=%.1f hip_ms=%.1f first_batch_ms=%.1f seed_ms=%.1f "

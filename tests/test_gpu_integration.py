@@ -218,6 +218,21 @@ def test_reference_signature_run_from_main_threads(tmp_path, scene, name):
 
 @pytest.mark.gpu
 @pytest.mark.spawns
+def test_reference_signature_run_three_frames_in_one_process(tmp_path):
+    """Three run() calls in one process, each with a fresh provider and film (a caller rendering again): the host
+    grid copies of one call are kept until the next (vpt_run.hpp) and every frame is the oracle's."""
+    w, h, waves = 48, 32, 3
+    extra = dict(mode="run", frames=3, gridbuf=_write_buffer(tmp_path, SynthGrid(1, 64).grid(copy=True), "density"),
+                 tempbuf=_write_buffer(tmp_path, SynthGrid(2, 64).grid(copy=True), "temperature"))
+    film, log = _harness(tmp_path, "fire.json", w, h, waves, 2, 0, **extra)
+    assert "frame 1 total_ms" in log and "frame 2 total_ms" in log
+    np.testing.assert_array_equal(film[..., 3], waves)
+    ref = _oracle_film("c4", w, h, waves)
+    np.testing.assert_allclose(film[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.spawns
 def test_drain_from_nvdb_file_with_tiles_at_every_level(tmp_path):
     """An .nvdb file (ZIP codec) of a grid with lower / upper / root tiles and sparse lower nodes, read
     by the C++ reader inside the harness and rendered by 2 threads, against the oracle on the grid."""
