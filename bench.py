@@ -165,7 +165,8 @@ HARNESS = ROOT / "tests" / "native" / "build" / "run_gpu_harness"
 def dropin_frames(wl, frames: int = 3, timeout_s: int = 300):
     """The reference-API path, timed: main.cpp:46-87 made headless -- the restated
     TileProvider and one worker thread calling vpt_gpu::drain (include/vpt_run.hpp: one staged feed, the
-    pusher and film threads, the 0.2-s progressive film) -- through tests/native/run_gpu_harness, on this
+    pusher and film threads, the 0.2-s progressive film, and run()'s ordered frame: the film in wave order at the
+    end, DrainOptions::ordered_frame) -- through tests/native/run_gpu_harness, on this
     config's frame: `frames` frames on one context (setup -- grid upload, tile costs, the feed's memory --
     outside the timed drains, as the harness and run_checked do it) after one untimed frame.  The median of the
     frames is the record's ms_per_frame.  Then the provider alone (mode=tokens: one
@@ -188,7 +189,7 @@ def dropin_frames(wl, frames: int = 3, timeout_s: int = 300):
             scene.write_text(json.dumps(doc))
         base = [str(HARNESS), f"config={scene}", f"w={W}", f"h={H}", f"waves={spp}", f"grid_n={wl.grid_n}",
                 f"kind={wl.density_kind}", f"dist={-wl.cfg.camera_parameters.position[2]:g}", "threads=1", "batch=4096",
-                f"temperature={1 if wl.temperature else 0}"]
+                f"temperature={1 if wl.temperature else 0}", "ordered=1"]
         try:
             r = subprocess.run(base + [f"out={tmp}/film.f32", f"frames={frames}", "warmup=1"], capture_output=True,
                                text=True, timeout=timeout_s)
@@ -210,7 +211,8 @@ def dropin_frames(wl, frames: int = 3, timeout_s: int = 300):
         return {"error": "no render_ms lines", "stdout_tail": r.stdout[-500:]}
     med = sorted(ms)[len(ms) // 2]
     rec = {"path": "vpt_gpu::drain (include/vpt_run.hpp) behind the restated TileProvider, main.cpp:46-87 headless "
-                   "(tests/native/run_gpu_harness), 1 worker thread, 0.2-s progressive film",
+                   "(tests/native/run_gpu_harness), 1 worker thread, 0.2-s progressive film, ordered frame (as run())",
+           "_film": film,
            "workload": f"{wl.name}: {W}x{H}, {spp} spp", "frames": len(ms), "warmup_frames": 1, "ms_frames": ms,
            "ms_per_frame": med,
            "value": round(W * H * spp / (med / 1e3) / 1e6, 3), "unit": "Msamples/s", "film_counts_exact": counts_ok}
@@ -571,7 +573,8 @@ def main():
 
         t0 = time.time()
         dropin = dropin_frames(_workload(args.config), args.dropin_frames)
-        log(f"bench: drop-in frames in {time.time() - t0:.1f}s: {dropin}")
+        log(f"bench: drop-in frames in {time.time() - t0:.1f}s: "
+            f"{ {k: v for k, v in dropin.items() if k != '_film'} if isinstance(dropin, dict) else dropin}")
 
     rank, world, dev, sdev = init_rank(args)
 
@@ -679,6 +682,14 @@ def main():
         if dropin is not None:
             if "ms_per_frame" in dropin:
                 dropin["vs_one_launch"] = round(out["ms_per_step"] / dropin["ms_per_frame"], 4)
+            dfilm = dropin.pop("_film", None)
+            if dfilm is not None and world == 1 and args.mode == "weak" and dfilm.shape == film.shape:
+                # the drop-in's last frame against this process's one-launch frame (both the reference's film, bit
+                # for bit, when both are in wave order)
+                import numpy as np
+                differ = int((dfilm.view(np.uint32) != film.view(np.uint32)).any(axis=-1).sum())
+                dropin["bit_identical_to_one_launch"] = differ == 0
+                dropin["pixels_differing_from_one_launch"] = differ
             out["dropin"] = dropin
         if world == 1 and not args.no_cpu_baseline:
             cb, ref_film, k = cpu_baseline(wl, dens, temp, args.cpu_budget)

@@ -260,6 +260,23 @@ int vpt_gpu_set_film_order(vpt_gpu_ctx* ctx, int mode, uint64_t max_bytes);
 int vpt_gpu_film_order_info(const vpt_gpu_ctx* ctx, int* mode, uint64_t* buffer_bytes, uint64_t* ordered_launches,
                             uint64_t* atomic_launches);
 
+/* The drop-in's ordered frame (vpt_run.hpp: vpt_gpu::run's film, bit-identical to the reference's).  A feed's jobs
+ * arrive in the provider's order and its film is progressive, so its launch adds samples with fp32 atomics; with a
+ * frame open, the context's feed launches also store the samples of the jobs of tiles [tile_lo, tile_hi) in waves
+ * jid_lo / T .. + *waves - 1 (from job jid_lo on) in the context's sample buffer (*waves * (tile_hi - tile_lo) *
+ * tile_area * 12 bytes, allocated here -- before any feed of the context is open: a running feed's launch holds the
+ * device, which an allocation may wait for; VPT_E_STATE otherwise).  *waves: asked for in, granted out -- at most
+ * what fits 3/4 of the device's free memory and 128 GiB (VPT_E_NOMEM when not one wave does).  After the feeds are collected,
+ * vpt_gpu_frame_finish adds the stored samples of jobs [jid_lo, jid_end) pixel by pixel in wave order -- w += 1,
+ * xyz += imaging_ratio * L (worker.cpp:203-204) -- onto `prior` (the host film before the frame, float[H][W][4];
+ * NULL = zeros) and writes the frame's tiles' pixels into film_host, replacing what the feeds' collects added
+ * there.  Every job of those tiles in [jid_lo, jid_end) must have been rendered by this context's feeds (one taker
+ * hands out a contiguous range); jid_end beyond the frame's waves is VPT_E_INVALID (those jobs stored nothing).
+ * waves = 0 closes the frame; finish closes it too.  While a frame is open the context's other ordered launches add
+ * with atomics (the buffer is the frame's). */
+int vpt_gpu_frame_open(vpt_gpu_ctx* ctx, uint64_t jid_lo, uint64_t* waves, uint32_t tile_lo, uint32_t tile_hi);
+int vpt_gpu_frame_finish(vpt_gpu_ctx* ctx, uint64_t jid_end, const float* prior, float* film_host);
+
 /* Like vpt_gpu_render_jobs but also writes every sample's radiance L (before the
  * imaging_ratio scale) to records_device[(jid - jid_begin) * tile_w*tile_h + y_local*rect_w + x_local][3]
  * — a debug path for bit-exact per-sample parity. */

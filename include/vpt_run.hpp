@@ -35,6 +35,7 @@
 #pragma once
 
 #include <algorithm>
+#include <bit>
 #include <array>
 #include <atomic>
 #include <chrono>
@@ -74,6 +75,12 @@ struct DrainOptions {
   // Frames the provider hands out in fewer than direct_below jobs render as jid-range launches instead of a feed
   // (detail::render_runs); 0 = auto: the launch's lanes (a feed would launch only at its close).  1: always a feed.
   uint64_t direct_below = 0;
+  // The ordered frame (vpt_gpu_frame_open / _finish): the feeds' launches also store every sample, and once they are
+  // collected each pixel's samples are added in wave order onto the film as it was before the frame -- the film the
+  // reference's workers produce, bit for bit (the feeds' fp32 atomics only make the progressive film).  It needs one
+  // taker: every job of the frame's range must reach this drain (run() sets it; drain() threads sharing a provider,
+  // or helpers, must not).  A frame larger than the device's memory keeps the atomics' film.
+  bool ordered_frame = false;
 };
 
 // Takes up to max_jobs tokens; on_token(token&) sees each before it is released.  Returns the count.
@@ -120,14 +127,34 @@ inline std::mutex& film_mutex() {  // the host film is shared by every caller
 // that thread.
 class FeedPipeline {
  public:
+  // An ordered frame (DrainOptions::ordered_frame): the jobs from jid_lo on of tiles [tile_lo, tile_hi), at most
+  // `waves` waves (the library may grant fewer), added in wave order onto `prior` (nullptr: zeros) at finish().
+  struct Frame {
+    uint64_t jid_lo = 0, waves = 0;
+    uint32_t tile_lo = 0, tile_hi = 0;
+    const float* prior = nullptr;
+  };
   std::atomic<int> helpers{0};  // help() threads attached (see detail::Helpers)
   explicit FeedPipeline(vpt_gpu_ctx* ctx) : ctx_(ctx) {}
   ~FeedPipeline() {
     stop_threads();
     if (feed_) (void)vpt_gpu_feed_destroy(feed_);
+    uint64_t none = 0;
+    if (frame_on_ && !feed_) (void)vpt_gpu_frame_open(ctx_, 0, &none, 0, 0);  // (a frame left open by an error path)
   }
-  int start(float* film_host, const DrainOptions& opt) {
+  int start(float* film_host, const DrainOptions& opt, const Frame* frame = nullptr) {
     film_host_ = film_host;
+    if (frame) {  // before the feed opens: the frame's memory is allocated now (vpt_gpu_frame_open)
+      uint64_t T = 0, total = 0, waves = frame->waves;
+      if (int rc = vpt_gpu_job_space(ctx_, &T, &total)) return rc;
+      if (vpt_gpu_frame_open(ctx_, frame->jid_lo, &waves, frame->tile_lo, frame->tile_hi) == VPT_OK) {
+        frame_ = *frame;
+        frame_on_ = true;
+        frame_end_ = (frame->jid_lo / T + waves) * T;  // jobs from here on store nothing: the atomics' film stands
+        pushed_end_ = frame->jid_lo;
+      }
+      detail::drain_trace("frame", frame_on_ ? (double)waves : -1.0, (double)frame->jid_lo);
+    }
     flush_ = opt.flush_seconds;
     int blocks = 0, threads = 0;
     if (int rc = vpt_gpu_launch_info(ctx_, &blocks, &threads)) return rc;
@@ -200,8 +227,19 @@ class FeedPipeline {
       if (frc == VPT_OK) {
         std::lock_guard<std::mutex> lock(film_mutex());
         frc = vpt_gpu_feed_collect(f, film_host_);
+        if (frame_on_) {  // the frame's tiles in wave order, over what the collect added (or the frame closed)
+          if (frc == VPT_OK && rc == VPT_OK && pushed_end_ <= frame_end_) {
+            frc = vpt_gpu_frame_finish(ctx_, pushed_end_, frame_.prior, film_host_);
+          } else {
+            uint64_t none = 0;
+            (void)vpt_gpu_frame_open(ctx_, 0, &none, 0, 0);
+          }
+          detail::drain_trace("frame_done", (double)pushed_end_, (double)frame_end_);
+        }
       } else {
         (void)vpt_gpu_feed_destroy(f);
+        uint64_t none = 0;
+        if (frame_on_) (void)vpt_gpu_frame_open(ctx_, 0, &none, 0, 0);  // (closed: the atomics' film stands)
       }
       if (rc == VPT_OK) rc = frc;
     }
@@ -218,6 +256,9 @@ class FeedPipeline {
     taker_cv_.notify_all();
   }
   int push(const uint64_t* ids, uint64_t n) { return n ? vpt_gpu_feed_push(feed_, ids, n) : VPT_OK; }
+  void note_end(const JobRuns& rs) {  // (the pusher's: one past the largest job id pushed, for the frame)
+    for (const auto& r : rs) pushed_end_ = std::max(pushed_end_, r.first + r.second);
+  }
   // The jobs taken and not yet pushed, as contiguous (jid, count) runs in the order taken (the pusher's): the
   // takers hand over runs (a batch of tokens is one or two), and the pusher expands them into job ids only as
   // it pushes them -- one pass over the ids, no division per job (r06: the pusher, not the taker, set the
@@ -296,6 +337,7 @@ class FeedPipeline {
       // changes nothing, and sorting them would delay the launch -- ~3 ms of C3's 458 752)
       const bool sort = cost_chunks_ && !cls_.empty() && pushed_ >= lanes_;
       const uint64_t n = hold.take(kChunk, chunk_);
+      note_end(chunk_);
       if (int rc = push(emit(chunk_, n, sort), n)) return rc;
       b += n;
       pushed_ += n;
@@ -341,6 +383,7 @@ class FeedPipeline {
     // items are different tiles of one wave), then the end of the feed.
     detail::drain_trace("final_hold", (double)hold.n, (double)pushed_);
     const uint64_t n = hold.take(hold.n, chunk_);
+    note_end(chunk_);
     const uint64_t* rest = emit(chunk_, n, cost_tail_ && !cls_.empty());
     for (uint64_t i = 0; i < n; i += kChunk)
       if (int rc = push(rest + i, std::min<uint64_t>(kChunk, n - i))) return fail(rc);
@@ -383,6 +426,9 @@ class FeedPipeline {
 
   vpt_gpu_ctx* ctx_;
   float* film_host_ = nullptr;
+  Frame frame_;
+  bool frame_on_ = false;
+  uint64_t frame_end_ = 0, pushed_end_ = 0;  // (pushed_end_: the pusher's, read after it has ended)
   double flush_ = 0.2;
   uint64_t hold_max_ = 0, backlog_ = 0, lanes_ = 0;
   uint64_t pushed_ = 0;  // (the pusher's)
@@ -539,20 +585,138 @@ int take_head(vpt_gpu_ctx* ctx, Provider& tp, uint64_t batch_jobs, const DrainOp
 }
 }  // namespace detail
 
+namespace detail {
+// The host film as it was before an ordered frame (vpt_gpu_frame_finish adds the frame's samples onto it), copied on
+// a thread of its own while the first tokens are taken; nullptr when it is all zeros (+0.0), the usual fresh film.
+struct PriorFilm {
+  std::vector<float> v;
+  bool zero = true;
+  std::thread th;
+  void start(vpt_gpu_ctx* ctx, const float* film) {
+    float* dev = nullptr;
+    uint64_t n = 0;
+    if (vpt_gpu_film_device_ptr(ctx, &dev, &n) != VPT_OK) return;
+    th = std::thread([this, film, n] {
+      v.assign(film, film + n);
+      zero = std::all_of(v.begin(), v.end(), [](float x) { return std::bit_cast<uint32_t>(x) == 0u; });
+    });
+  }
+  void join() {  // (before anything writes the film)
+    if (th.joinable()) th.join();
+  }
+  const float* get() {
+    join();
+    return zero ? nullptr : v.data();
+  }
+  ~PriorFilm() {
+    if (th.joinable()) th.join();
+  }
+};
+// An ordered frame is sized from the provider's progress() (percent of its jobs handed out, floored): until it
+// reads >= 1 the frame's size has no useful bound, so tokens are taken on until it does (1 % of the frame: C3 83 K
+// tokens, ~1 ms; C5 1.3 M, ~20 ms) or the provider runs dry (`dry`: the frame is what was taken).
+template <class Provider>
+int take_until_sized(Provider& tp, uint64_t batch_jobs, JobRuns& head, bool& dry) {
+  dry = false;
+  if constexpr (requires { tp.progress(); }) {
+    JobRuns more;
+    while (tp.progress() == 0) {
+      if (!take_jobs(tp, std::max<uint64_t>(1, batch_jobs), more, [](auto&) {})) {
+        dry = true;
+        break;
+      }
+      append_runs(head, more);
+    }
+  }
+  return VPT_OK;
+}
+// The frame of the jobs taken from `head` on: its first job, and how many waves it can span -- all taken (dry), or
+// bounded by progress() (the frame ends before taken * 100 / pct jobs), else as many as the device holds
+// (vpt_gpu_frame_open grants what fits).
+template <class Provider>
+FeedPipeline::Frame frame_of(Provider& tp, const JobRuns& head, uint64_t T, uint32_t tile_lo, uint32_t tile_hi,
+                             const float* prior, bool dry = false) {
+  FeedPipeline::Frame fr;
+  fr.jid_lo = head.empty() ? 0 : head.front().first;
+  uint64_t end = 0;
+  for (const auto& r : head) {
+    fr.jid_lo = std::min(fr.jid_lo, r.first);
+    end = std::max(end, r.first + r.second);
+  }
+  fr.waves = ~0ULL >> 8;
+  if (dry && T > 0 && end > fr.jid_lo) {
+    fr.waves = (end - 1) / T - fr.jid_lo / T + 1;
+  } else if constexpr (requires { tp.progress(); }) {
+    if (const uint64_t pct = (uint64_t)tp.progress(); pct > 0 && T > 0)
+      fr.waves = (end * 100 / pct - 1) / T - fr.jid_lo / T + 1;  // (end = the provider's job counter)
+  }
+  fr.tile_lo = tile_lo;
+  fr.tile_hi = tile_hi;
+  fr.prior = prior;
+  return fr;
+}
+// n bands of consecutive tiles [cut[i], cut[i + 1]) of about equal estimated cost, each at least one tile (T >= n).
+inline std::vector<uint32_t> cost_bands(const std::vector<float>& cost, size_t n) {
+  const uint64_t T = cost.size();
+  std::vector<uint32_t> cut(n + 1, 0);
+  double total = 0;
+  for (float c : cost) total += std::max(0.0f, c);
+  double acc = 0;
+  uint64_t t = 0;
+  for (size_t i = 1; i < n; ++i) {
+    const double goal = total * (double)i / (double)n;
+    while (t < T && acc + std::max(0.0f, cost[t]) <= goal) acc += std::max(0.0f, cost[t++]);
+    t = std::max<uint64_t>(t, (uint64_t)cut[i - 1] + 1);  // non-empty bands
+    t = std::min<uint64_t>(t, T - (n - i));                // room for the rest
+    cut[i] = (uint32_t)t;
+  }
+  cut[n] = (uint32_t)T;
+  return cut;
+}
+// Runs of job ids cut at the bands' tile boundaries (jid % T), each piece appended to its band's runs.
+inline void split_bands(const JobRuns& rs, uint64_t T, const std::vector<uint32_t>& cut, std::vector<JobRuns>& parts) {
+  for (auto r : rs)
+    while (r.second > 0) {
+      const uint64_t t = r.first % T;
+      const size_t b = (size_t)(std::upper_bound(cut.begin(), cut.end(), (uint32_t)t) - cut.begin()) - 1;
+      const uint64_t len = std::min<uint64_t>(r.second, (uint64_t)cut[b + 1] - t);
+      JobRuns& p = parts[b];
+      if (!p.empty() && p.back().first + p.back().second == r.first)
+        p.back().second += len;
+      else
+        p.emplace_back(r.first, len);
+      r.first += len;
+      r.second -= len;
+    }
+}
+}  // namespace detail
+
 template <class Provider>
 int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs, const DrainOptions& opt = {},
           const JobRuns* first = nullptr, bool share = false) {
+  const bool ordered = opt.ordered_frame && !share;
+  detail::PriorFilm prior;
+  if (ordered) prior.start(ctx, film_host);
   JobRuns head;  // the jobs taken before the pipeline starts
   if (!share) {  // (a shared pipeline takes helpers' jobs: it always runs)
     bool small = false;
     detail::drain_trace("drain");
     if (int rc = detail::take_head(ctx, tp, batch_jobs, opt, first, head, small)) return rc;
+    prior.join();
     if (small) return detail::render_runs(ctx, head, film_host);
     first = &head;
   }
   detail::drain_trace("head_taken");
   FeedPipeline pipe(ctx);
-  int rc = pipe.start(film_host, opt);
+  FeedPipeline::Frame frame;
+  if (ordered) {
+    uint64_t T = 0, total = 0;
+    bool dry = false;
+    if (int rc = vpt_gpu_job_space(ctx, &T, &total)) return rc;
+    if (int rc = detail::take_until_sized(tp, batch_jobs, head, dry)) return rc;
+    frame = detail::frame_of(tp, head, T, 0, (uint32_t)T, prior.get(), dry);
+  }
+  int rc = pipe.start(film_host, opt, ordered ? &frame : nullptr);
   if (rc == VPT_OK && first) rc = pipe.add(*first);
   detail::drain_trace("started");
   detail::Helpers& hub = detail::Helpers::get();
@@ -617,17 +781,44 @@ int drain_devices(const std::vector<vpt_gpu_ctx*>& ctxs, Provider& tp, float* fi
                   const DrainOptions& opt = {}, const JobRuns* first = nullptr) {
   if (ctxs.empty()) return VPT_E_INVALID;
   if (ctxs.size() == 1) return drain(ctxs[0], tp, film_host, batch_jobs, opt, first);
+  detail::PriorFilm prior;
+  if (opt.ordered_frame) prior.start(ctxs[0], film_host);
   JobRuns head;
   bool small = false;
   if (int rc = detail::take_head(ctxs[0], tp, batch_jobs, opt, first, head, small)) return rc;
+  prior.join();
   if (small) return detail::render_runs_split(ctxs, head, film_host);
   std::vector<std::unique_ptr<FeedPipeline>> pipes;
   int rc = VPT_OK;
-  for (vpt_gpu_ctx* c : ctxs) {
-    pipes.push_back(std::make_unique<FeedPipeline>(c));
-    if (rc == VPT_OK) rc = pipes.back()->start(film_host, opt);
+  // An ordered frame: each GPU owns a band of tiles (about equal estimated cost, vpt_gpu_tile_costs) and renders
+  // every job of its tiles, so each pixel's samples are on one GPU and its frame pass orders them.
+  std::vector<uint32_t> cut;
+  uint64_t T = 0;
+  bool dry = false;
+  if (opt.ordered_frame) {
+    uint64_t total = 0;
+    if ((rc = vpt_gpu_job_space(ctxs[0], &T, &total))) return rc;
+    if ((rc = detail::take_until_sized(tp, batch_jobs, head, dry))) return rc;
+    std::vector<float> cost(T);
+    if ((rc = vpt_gpu_tile_costs(ctxs[0], cost.data(), nullptr))) return rc;
+    cut = detail::cost_bands(cost, ctxs.size());
   }
-  if (rc == VPT_OK) rc = pipes[0]->add(head);  // a lane's worth: the first GPU's launch starts now
+  for (size_t i = 0; i < ctxs.size(); ++i) {
+    pipes.push_back(std::make_unique<FeedPipeline>(ctxs[i]));
+    FeedPipeline::Frame frame;
+    if (opt.ordered_frame) frame = detail::frame_of(tp, head, T, cut[i], cut[i + 1], prior.get(), dry);
+    if (rc == VPT_OK) rc = pipes.back()->start(film_host, opt, opt.ordered_frame ? &frame : nullptr);
+  }
+  std::vector<JobRuns> parts(opt.ordered_frame ? ctxs.size() : 0);
+  auto add_bands = [&](const JobRuns& rs) -> int {  // (ordered frames) each job to the GPU that owns its tile
+    for (auto& p : parts) p.clear();
+    detail::split_bands(rs, T, cut, parts);
+    for (size_t i = 0; i < parts.size(); ++i)
+      if (!parts[i].empty())
+        if (int r = pipes[i]->add(parts[i])) return r;
+    return VPT_OK;
+  };
+  if (rc == VPT_OK) rc = opt.ordered_frame ? add_bands(head) : pipes[0]->add(head);  // (one GPU's launch starts now)
   auto route = [&]() -> size_t {
     for (size_t i = 0; i < pipes.size(); ++i)
       if (pipes[i]->added() < pipes[i]->lanes()) return i;
@@ -644,7 +835,7 @@ int drain_devices(const std::vector<vpt_gpu_ctx*>& ctxs, Provider& tp, float* fi
   uint64_t taken = 0;
   for (uint64_t n; rc == VPT_OK && (n = take_jobs(tp, std::max<uint64_t>(1, batch_jobs), runs, [](auto&) {}));) {
     taken += n;
-    rc = pipes[route()]->add(runs);
+    rc = opt.ordered_frame ? add_bands(runs) : pipes[route()]->add(runs);
   }
   detail::drain_trace("taker_done", (double)taken);
   for (auto& p : pipes) p->end_input();  // every GPU's last jobs go out before any launch is waited for
@@ -961,7 +1152,13 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   // (Leader), so the slot is never shared; flat now holds the previous call's copies, released at this call's end.
   static detail::OwnedGrids kept;
   std::swap(kept.g, flat.g);
-  const int rc = drain_devices(ctxs, tp, film_host, 4096, DrainOptions{}, &runs);
+  // the film in wave order, bit-identical to the reference's (VPT_DROPIN_ORDERED=0: the feeds' atomics alone)
+  DrainOptions dopt;
+  const char* ord = std::getenv("VPT_DROPIN_ORDERED");
+  dopt.ordered_frame = !(ord && std::atoi(ord) == 0);
+  if (const char* db = std::getenv("VPT_DROPIN_DIRECT_BELOW"))  // (tests: 1 = a feed even for a small frame)
+    dopt.direct_below = (uint64_t)std::atoll(db);
+  const int rc = drain_devices(ctxs, tp, film_host, 4096, dopt, &runs);
   lap(ph.frame_ms);
   ph.total_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
   run_phases() = ph;

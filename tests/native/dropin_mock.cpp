@@ -8,13 +8,15 @@
 // that cannot end that way within 5 s is reported as a deadlock.
 //
 //   dropin_mock drivers=<n> helpers=<n> w= h= waves= batch= flush_ms= hold= backlog= cost_tail= stop_after=
-//               multi=1 devices=<n> blocks= threads= cheap=1 rate=1
+//               multi=1 devices=<n> blocks= threads= cheap=1 rate=1 ordered=1
 //
 // multi=1: ONE thread drives `devices` mock GPUs through vpt_gpu::drain_devices (what run() does with the
 // process's GPUs); each device blocks only its own feeds.  blocks / threads: the mock launch's
 // lanes (default 3 x 7).  cheap=1: a push only records its job ids (the film is counted at the snapshots), so the
 // host protocol's own cost shows; rate=1 then also times the provider alone on one thread over the same frame
-// and prints both token rates ("rate frame <M/s> provider <M/s>").
+// and prints both token rates ("rate frame <M/s> provider <M/s>").  ordered=1: DrainOptions::ordered_frame (what run()
+// sets): each mock device's frame finish checks that every job of its tile band in the frame's range was rendered
+// once, by that device, and writes the band's counts over the host film as the library writes its ordered pixels.
 #include <algorithm>
 #include <chrono>
 #include <atomic>
@@ -36,6 +38,8 @@ int g_blocks = 3, g_threads = 7;
 bool g_cheap = false;
 std::mutex g_mu;
 std::vector<uint32_t> g_rendered;  // per jid: times pushed into an open feed
+std::vector<int> g_device_of;      // per jid: the device that rendered it (-1: none)
+std::atomic<int> g_frames{0};      // ordered frames finished
 std::atomic<int> g_open_feeds{0}, g_max_open{0};
 std::atomic<uint64_t> g_direct_jobs{0};  // jobs rendered by jid-range launches (small frames), not feeds
 std::mutex g_dev_mu;            // the "device": feeds in open order
@@ -45,6 +49,8 @@ std::vector<struct vpt_gpu_feed*> g_dev_feeds;
 struct vpt_gpu_ctx {
   std::vector<float> own;
   int device = 0;
+  uint64_t frame_lo = 0, frame_waves = 0;  // an open ordered frame (frame_waves > 0): jobs from frame_lo of tiles
+  uint32_t frame_tl = 0, frame_th = 0;     // [frame_tl, frame_th)
 };
 struct vpt_gpu_feed {
   vpt_gpu_ctx* ctx;
@@ -78,7 +84,10 @@ void settle(vpt_gpu_feed* f) {  // cheap=1: the pushed jobs into the counts (und
   if (f->jids.empty()) return;
   {
     std::lock_guard<std::mutex> l(g_mu);
-    for (uint64_t j : f->jids) ++g_rendered[j];
+    for (uint64_t j : f->jids) {
+      ++g_rendered[j];
+      g_device_of[j] = f->ctx->device;
+    }
   }
   for (uint64_t j : f->jids) count_job(f->film, j);
   f->jids.clear();
@@ -132,6 +141,48 @@ int vpt_gpu_tile_costs(vpt_gpu_ctx*, float*, uint32_t* rank) {  // the last tile
   return VPT_OK;
 }
 int vpt_gpu_feed_prepare(vpt_gpu_ctx*, uint64_t, int) { return VPT_OK; }
+int vpt_gpu_film_device_ptr(vpt_gpu_ctx* c, float** film, uint64_t* count) {
+  *film = c->own.data();
+  *count = c->own.size();
+  return VPT_OK;
+}
+int vpt_gpu_frame_open(vpt_gpu_ctx* c, uint64_t jid_lo, uint64_t* waves, uint32_t tile_lo, uint32_t tile_hi) {
+  c->frame_waves = std::min<uint64_t>(*waves, 1u << 20);
+  *waves = c->frame_waves;
+  c->frame_lo = jid_lo;
+  c->frame_tl = tile_lo;
+  c->frame_th = tile_hi;
+  return VPT_OK;
+}
+int vpt_gpu_frame_finish(vpt_gpu_ctx* c, uint64_t jid_end, const float* prior, float* host) {
+  if (!c->frame_waves) return VPT_OK;
+  c->frame_waves = 0;
+  const uint64_t T = (uint64_t)(g_ntx * ((g_h + g_th - 1) / g_th));
+  std::vector<float> count(T, 0.0f);
+  {
+    std::lock_guard<std::mutex> l(g_mu);
+    for (uint64_t j = c->frame_lo; j < jid_end; ++j) {
+      const uint64_t t = j % T;
+      if (t < c->frame_tl || t >= c->frame_th) continue;
+      if (j >= g_rendered.size() || g_rendered[j] != 1 || g_device_of[j] != c->device) {
+        std::printf("dropin_mock: frame of device %d: jid %llu rendered %u times, by device %d\n", c->device,
+                    (unsigned long long)j, j < g_rendered.size() ? g_rendered[j] : 0u, j < g_device_of.size() ? g_device_of[j] : -2);
+        return VPT_E_STATE;
+      }
+      count[t] += 1.0f;
+    }
+  }
+  for (uint64_t t = c->frame_tl; t < c->frame_th; ++t) {  // the band's pixels over the host film
+    const int64_t x0 = (int64_t)(t % (uint64_t)g_ntx) * g_tw, y0 = (int64_t)(t / (uint64_t)g_ntx) * g_th;
+    for (int64_t y = y0; y < std::min(g_h, y0 + g_th); ++y)
+      for (int64_t x = x0; x < std::min(g_w, x0 + g_tw); ++x) {
+        const size_t p = (size_t)(y * g_w + x) * 4 + 3;
+        host[p] = (prior ? prior[p] : 0.0f) + count[t];
+      }
+  }
+  ++g_frames;
+  return VPT_OK;
+}
 int vpt_gpu_render_jobs(vpt_gpu_ctx* c, uint64_t begin, uint64_t count, float* film, void*) {  // a small frame's launch
   if (film) return VPT_E_INVALID;
   const int64_t T = g_ntx * ((g_h + g_th - 1) / g_th);
@@ -140,6 +191,7 @@ int vpt_gpu_render_jobs(vpt_gpu_ctx* c, uint64_t begin, uint64_t count, float* f
       std::lock_guard<std::mutex> l(g_mu);
       if (jid >= g_rendered.size()) return VPT_E_INVALID;
       ++g_rendered[jid];
+      g_device_of[jid] = c->device;
     }
     const int64_t tile = (int64_t)(jid % (uint64_t)T), x0 = (tile % g_ntx) * g_tw, y0 = (tile / g_ntx) * g_th;
     for (int64_t y = y0; y < std::min(g_h, y0 + g_th); ++y)
@@ -194,6 +246,7 @@ int vpt_gpu_feed_push(vpt_gpu_feed* f, const uint64_t* jids, uint64_t n) {
       std::lock_guard<std::mutex> l(g_mu);
       if (jids[i] >= g_rendered.size()) return VPT_E_INVALID;
       ++g_rendered[jids[i]];
+      g_device_of[jids[i]] = f->ctx->device;
     }
     const int64_t tile = (int64_t)(jids[i] % (uint64_t)T), x0 = (tile % g_ntx) * g_tw, y0 = (tile / g_ntx) * g_th;
     std::lock_guard<std::mutex> l(f->mu);
@@ -264,7 +317,7 @@ int main(int argc, char** argv) {
   std::map<std::string, long long> a{{"drivers", 1}, {"helpers", 0}, {"w", 72}, {"h", 40}, {"waves", 5},
                                      {"batch", 7}, {"flush_ms", 0}, {"hold", 0}, {"backlog", 0}, {"stop_after", 0},
                                      {"cost_tail", 1}, {"cost_chunks", 1}, {"multi", 0}, {"devices", 1},
-                                     {"blocks", 3}, {"threads", 7}, {"cheap", 0}, {"rate", 0}};
+                                     {"blocks", 3}, {"threads", 7}, {"cheap", 0}, {"rate", 0}, {"ordered", 0}};
   for (int i = 1; i < argc; ++i) {
     const char* eq = std::strchr(argv[i], '=');
     if (eq) a[std::string(argv[i], eq - argv[i])] = std::atoll(eq + 1);
@@ -308,6 +361,7 @@ int main(int argc, char** argv) {
   vpt_headless::TileProvider tp(g_w, g_h, (unsigned)a["waves"], g_tw, g_th);
   const uint64_t T = tp.num_tiles(), total = T * (uint64_t)a["waves"];
   g_rendered.assign(total + 8 * T, 0);  // room for jids past a stop
+  g_device_of.assign(g_rendered.size(), -1);
   std::atomic<uint64_t> handed{0};
   struct Stopping {
     vpt_headless::TileProvider& tp;
@@ -321,6 +375,7 @@ int main(int argc, char** argv) {
       if (k == last) dry_ns.store(std::chrono::steady_clock::now().time_since_epoch().count());
       return tp.next();
     }
+    unsigned progress() const { return tp.progress(); }  // (drain's probe; ordered frames are sized from it)
   } sp{tp, handed, (uint64_t)a["stop_after"]};
   sp.last = a["rate"] ? total : 0;
   std::vector<float> film((size_t)(g_w * g_h * 4), 0.0f);
@@ -339,6 +394,7 @@ int main(int argc, char** argv) {
   opt.backlog_jobs = (uint64_t)a["backlog"];
   opt.cost_tail = a["cost_tail"] != 0;
   opt.cost_chunks = a["cost_chunks"] != 0;
+  opt.ordered_frame = a["ordered"] != 0;
   {
     std::lock_guard<std::mutex> l(vpt_gpu::detail::Helpers::get().mu);
     vpt_gpu::detail::Helpers::get().drivers += drivers;  // (run() counts them when they claim a device)
@@ -377,9 +433,9 @@ int main(int argc, char** argv) {
       std::printf("dropin_mock: pixel %zu counts %g samples, want %llu\n", p / 4, film[p], (unsigned long long)waves);
       return 1;
     }
-  std::printf("dropin_mock: ok %llu waves, %llu jobs, max %d feeds open, %llu jobs in direct launches\n",
+  std::printf("dropin_mock: ok %llu waves, %llu jobs, max %d feeds open, %llu jobs in direct launches, %d ordered frames\n",
               (unsigned long long)waves, (unsigned long long)ran, g_max_open.load(),
-              (unsigned long long)g_direct_jobs.load());
+              (unsigned long long)g_direct_jobs.load(), g_frames.load());
   if (a["rate"]) {  // the taker's rate: tokens / (provider dry - start); frame_ms adds the pipelines' end
     const double take_ms =
         (double)(sp.dry_ns.load() - f0.time_since_epoch().count()) * 1e3 * std::chrono::steady_clock::period::num /

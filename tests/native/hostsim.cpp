@@ -50,6 +50,7 @@ struct HostEnv {
     return true;
   }
   void job_end(const vpt::DevScene&, const vpt::LaneCold&) {}  // (staged feeds' per-tile job counts: GPU only)
+  void job_start(const vpt::DevScene&, vpt::LaneCold&, uint64_t) {}  // (feeds' ordered frames: GPU only)
   const double (*logf_table() const)[2] { return vpt::math::kLogfTab; }
   void blackbody(const vpt::DevScene& S, float t, float& X, float& Y, float& Z) const {
     if (S.bb_lds_ok) {  // the kernel's LDS path: only the first kBbLdsRows rows (NaN beyond, so a

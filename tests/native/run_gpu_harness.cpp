@@ -272,6 +272,7 @@ int main(int argc, char** argv) {
     opt.cost_chunks = num("cost_chunks", opt.cost_chunks ? 1 : 0) != 0;
     opt.direct_below = (uint64_t)num("direct_below", (long long)opt.direct_below);
     opt.flush_seconds = (double)num("flush_ms", (long long)(opt.flush_seconds * 1000)) / 1000.0;
+    opt.ordered_frame = num("ordered", 0) != 0;  // (one taker only: multi=1, or one drain thread without helpers)
     if (num("grid_blocks", 0) > 0)
       for (auto* c : ctx)
         if (vpt_gpu_set_tuning(c, 0, -1, (int)num("grid_blocks", 0), 0, -1)) return fail("vpt_gpu_set_tuning");

@@ -4,7 +4,8 @@ run()'s helper threads) over a mock of the C ABI's stream / feed calls, built wi
 snapshots every millisecond, stop_at_next_wave() mid-run, tiny run-ahead bounds (hold / backlog) and the cost
 tail on and off, and small frames rendered by jid-range launches instead of a feed, every job id the TileProvider
 hands out is rendered exactly once, the host film counts every sample once, and TSan reports no race -- also with
-ONE taker feeding 2-8 mock GPUs (drain_devices, run()'s multi-GPU path).  The taker's token rate against the
+ONE taker feeding 2-8 mock GPUs (drain_devices, run()'s multi-GPU path), and with the ordered frame (each GPU's
+tile band rendered by that GPU alone).  The taker's token rate against the
 provider alone is measured on an optimised build of the same mock (dropin_mock_rate)."""
 import os
 import subprocess
@@ -37,6 +38,15 @@ CASES = [
     "multi=1 devices=2 hold=5 backlog=3 batch=7 flush_ms=1 cost_tail=0",
     "multi=1 devices=8 cheap=1 w=400 h=240 waves=8 batch=64 blocks=10 threads=64 flush_ms=1",
     "multi=1 devices=8 w=24 h=16 waves=2 batch=1",  # a small frame: jid-range launches split over the GPUs
+    # the ordered frame (DrainOptions::ordered_frame, what run() sets): every job of a GPU's tile band in the frame's
+    # range rendered once, by that GPU; its counts written over the host film
+    "ordered=1",
+    "ordered=1 flush_ms=1 batch=3 hold=5 backlog=3",
+    "ordered=1 stop_after=50 batch=2",
+    "multi=1 devices=8 ordered=1",
+    "multi=1 devices=3 ordered=1 w=200 h=120 waves=4 batch=1 flush_ms=1",
+    "multi=1 devices=8 ordered=1 stop_after=90 batch=5 hold=37 backlog=11 flush_ms=1",
+    "multi=1 devices=2 ordered=1 w=24 h=16 waves=2 batch=1",
 ]
 
 
@@ -51,6 +61,9 @@ def test_dropin_protocol_renders_every_token_once(args):
             assert ", 0 jobs in direct launches" not in r.stdout and "max 0 feeds open" in r.stdout, r.stdout
         elif "multi=1 devices=8" in args:  # every mock GPU got a feed of its own
             assert "max 8 feeds open" in r.stdout, r.stdout
+        if "ordered=1" in args and "w=24" not in args:  # a frame per GPU (none for a small frame's launches)
+            n = int(args.split("devices=")[1].split()[0]) if "multi=1" in args else 1
+            assert f", {n} ordered frames" in r.stdout, r.stdout
 
 
 RATE = MOCK.parent / "dropin_mock_rate"

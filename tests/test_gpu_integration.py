@@ -8,8 +8,9 @@ gating, tests/native/tile_provider_headless.hpp) and one shared host film, eithe
     private to the RNG -- the call main.cpp:63-68 makes, with only the function name changed.
 
 Bar: no hang (the harness runs under a timeout), every pixel's sample count equals the number of
-waves rendered, and the film equals the oracle's serial render of the same job ids to fp32
-atomic-order rounding."""
+waves rendered, and the film equals the oracle's serial render of the same job ids -- bit for bit through run()
+(its ordered frame, DrainOptions::ordered_frame), to fp32 atomic-order rounding where several drain() threads share
+the provider (their feeds add atomically)."""
 import json
 import subprocess
 from pathlib import Path
@@ -25,14 +26,21 @@ ROOT = Path(__file__).resolve().parents[1]
 HARNESS = ROOT / "tests" / "native" / "build" / "run_gpu_harness"
 
 
-def _harness(tmp_path, scene, w, h, waves, threads, batch, grid_n=64, temperature=0, stop_after=0, **extra):
+def _assert_bitwise(a, b):
+    diff = (a.view(np.uint32) != b.view(np.uint32)).any(axis=-1)
+    assert not diff.any(), f"{int(diff.sum())} of {diff.size} pixels differ from the oracle's film"
+
+
+def _harness(tmp_path, scene, w, h, waves, threads, batch, grid_n=64, temperature=0, stop_after=0, env=None, **extra):
+    import os
+
     assert_hip_untouched()
     out = tmp_path / "film.f32"
     config = scene if Path(str(scene)).is_absolute() else SCENE_DIR / scene
     args = [str(HARNESS), f"config={config}", f"out={out}", f"w={w}", f"h={h}", f"waves={waves}",
             f"threads={threads}", f"batch={batch}", f"grid_n={grid_n}", f"temperature={temperature}",
             f"stop_after={stop_after}"] + [f"{k}={v}" for k, v in extra.items()]
-    r = subprocess.run(args, capture_output=True, text=True, timeout=120)
+    r = subprocess.run(args, capture_output=True, text=True, timeout=120, env=dict(os.environ, **(env or {})))
     assert r.returncode == 0, r.stderr + r.stdout
     return np.fromfile(out, np.float32).reshape(h, w, 4), r.stdout
 
@@ -137,13 +145,15 @@ def test_drop_in_recovers_the_private_seed(tmp_path, seed, device):
 
 @pytest.mark.gpu
 @pytest.mark.spawns
+@pytest.mark.parametrize("ordered", [0, 1])
 @pytest.mark.parametrize("ctxs", [2, 3])
-def test_one_taker_drives_several_contexts(tmp_path, ctxs):
+def test_one_taker_drives_several_contexts(tmp_path, ctxs, ordered):
     """drain_devices (run()'s multi-GPU path): ONE thread takes every token and feeds 2-3
     contexts -- here all on the box's one GPU, each launch held to 8 blocks so the feeds run side by side (a
-    full-grid feed would hold every CU until it is closed).  Each context's pipeline gets a lane's worth first,
-    then the least-loaded one each batch; every pipeline closes its feed (VPT_DRAIN_TRACE), every job is rendered
-    once and the film is the oracle's to fp32 atomic-order rounding (feeds add atomically)."""
+    full-grid feed would hold every CU until it is closed).  ordered=0: each context's pipeline gets a lane's worth
+    first, then the least-loaded one each batch, and the film is the oracle's to fp32 atomic-order rounding (feeds
+    add atomically).  ordered=1 (what run() does): each context owns a band of tiles and orders its pixels' samples
+    at the end -- the film equals the oracle's bit for bit.  Every pipeline closes its feed (VPT_DRAIN_TRACE)."""
     import os
 
     assert_hip_untouched()
@@ -151,14 +161,18 @@ def test_one_taker_drives_several_contexts(tmp_path, ctxs):
     out = tmp_path / "film.f32"
     args = [str(HARNESS), f"config={SCENE_DIR / 'wdas_cloud.json'}", f"out={out}", f"w={w}", f"h={h}",
             f"waves={waves}", f"threads={ctxs}", "batch=256", "grid_n=64", "multi=1", "devices=1", "grid_blocks=8",
-            "flush_ms=20"]
+            "flush_ms=20", f"ordered={ordered}"]
     r = subprocess.run(args, capture_output=True, text=True, timeout=120, env=dict(os.environ, VPT_DRAIN_TRACE="1"))
     assert r.returncode == 0, r.stderr + r.stdout
     assert r.stderr.count(" closed ") == ctxs, r.stderr  # every context's feed ran and closed
     film = np.fromfile(out, np.float32).reshape(h, w, 4)
     np.testing.assert_array_equal(film[..., 3], waves)
     ref = _oracle_film("c3", w, h, waves)
-    np.testing.assert_allclose(film[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
+    if ordered:
+        assert r.stderr.count(" frame_done ") == ctxs, r.stderr
+        _assert_bitwise(film, ref)
+    else:
+        np.testing.assert_allclose(film[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.gpu
@@ -200,19 +214,21 @@ def _write_buffer(tmp_path, grid, name):
 
 @pytest.mark.gpu
 @pytest.mark.spawns
+@pytest.mark.parametrize("feed", ["0", "1"])
 @pytest.mark.parametrize("scene,name", [("wdas_cloud.json", "c3"), ("fire.json", "c4")])
-def test_reference_signature_run_from_main_threads(tmp_path, scene, name):
+def test_reference_signature_run_from_main_threads(tmp_path, scene, name, feed):
     """vpt_gpu::run with main.cpp's arguments from 3 worker threads on one GPU: one thread drives the
     device, the others return; the seed is recovered from the RNG (private in the reference); the
-    tile size from the tokens; the grids are read from NanoGrid<float> memory."""
+    tile size from the tokens; the grids are read from NanoGrid<float> memory.  The frame is small: jid-range
+    launches (feed 0), or through a feed and its ordered frame (feed 1: VPT_DROPIN_DIRECT_BELOW=1)."""
     w, h, waves = 72, 40, 3
     extra = dict(mode="run", gridbuf=_write_buffer(tmp_path, SynthGrid(1, 64).grid(copy=True), "density"))
     if name == "c4":
         extra["tempbuf"] = _write_buffer(tmp_path, SynthGrid(2, 64).grid(copy=True), "temperature")
-    film, log = _harness(tmp_path, scene, w, h, waves, 3, 0, **extra)
+    film, log = _harness(tmp_path, scene, w, h, waves, 3, 0, env={"VPT_DROPIN_DIRECT_BELOW": feed}, **extra)
     np.testing.assert_array_equal(film[..., 3], waves)
     ref = _oracle_film(name, w, h, waves)
-    np.testing.assert_allclose(film[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
+    _assert_bitwise(film, ref)  # (run()'s ordered frame: the reference's film bit for bit)
     assert f"{waves} waves started" in log
 
 
@@ -224,11 +240,31 @@ def test_reference_signature_run_three_frames_in_one_process(tmp_path):
     w, h, waves = 48, 32, 3
     extra = dict(mode="run", frames=3, gridbuf=_write_buffer(tmp_path, SynthGrid(1, 64).grid(copy=True), "density"),
                  tempbuf=_write_buffer(tmp_path, SynthGrid(2, 64).grid(copy=True), "temperature"))
-    film, log = _harness(tmp_path, "fire.json", w, h, waves, 2, 0, **extra)
+    film, log = _harness(tmp_path, "fire.json", w, h, waves, 2, 0, env={"VPT_DROPIN_DIRECT_BELOW": "1"}, **extra)
     assert "frame 1 total_ms" in log and "frame 2 total_ms" in log
     np.testing.assert_array_equal(film[..., 3], waves)
     ref = _oracle_film("c4", w, h, waves)
-    np.testing.assert_allclose(film[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
+    _assert_bitwise(film, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.spawns
+@pytest.mark.parametrize("ordered", ["1", "0"])
+def test_reference_signature_run_stop_at_next_wave(tmp_path, ordered):
+    """run() with stop_at_next_wave() during wave 2 (tile_provider.cpp:107-110) through a feed (VPT_DROPIN_DIRECT_BELOW):
+    every pixel holds exactly 2 samples and the film is the oracle's 2-wave film -- bit for bit with run()'s ordered
+    frame (the frame ends before its waves do), to atomic-order rounding with VPT_DROPIN_ORDERED=0."""
+    w, h, waves = 256, 160, 40
+    T = (w // 8) * (h // 8)
+    extra = dict(mode="run", gridbuf=_write_buffer(tmp_path, SynthGrid(1, 64).grid(copy=True), "density"))
+    film, log = _harness(tmp_path, "wdas_cloud.json", w, h, waves, 2, 0, stop_after=T + 5,
+                         env={"VPT_DROPIN_ORDERED": ordered, "VPT_DROPIN_DIRECT_BELOW": "1"}, **extra)
+    np.testing.assert_array_equal(film[..., 3], 2)
+    ref = _oracle_film("c3", w, h, 2)
+    if ordered == "1":
+        _assert_bitwise(film, ref)
+    else:
+        np.testing.assert_allclose(film[..., :3], ref[..., :3], rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.gpu

@@ -225,6 +225,9 @@ def lib() -> C.CDLL:
     L.vpt_gpu_create.argtypes = [cfgp, gridp, gridp, fp, C.c_int, C.POINTER(vp)]
     if hasattr(L, "vpt_gpu_create_many"):
         L.vpt_gpu_create_many.argtypes = [cfgp, gridp, gridp, fp, C.POINTER(C.c_int), C.c_int, C.POINTER(vp)]
+    if hasattr(L, "vpt_gpu_frame_open"):
+        L.vpt_gpu_frame_open.argtypes = [vp, C.c_uint64, C.POINTER(C.c_uint64), C.c_uint32, C.c_uint32]
+        L.vpt_gpu_frame_finish.argtypes = [vp, C.c_uint64, fp, fp]
     if hasattr(L, "vpt_grids_flatten"):
         L.vpt_grids_flatten.argtypes = [gridp, gridp, C.POINTER(vp)]
         L.vpt_gpu_create_from.argtypes = [cfgp, vp, fp, C.POINTER(C.c_int), C.c_int, C.POINTER(vp)]

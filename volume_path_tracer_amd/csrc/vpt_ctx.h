@@ -117,6 +117,13 @@ struct vpt_gpu_ctx {
   hipEvent_t samples_done = nullptr;
   bool samples_used = false;
   uint64_t ordered_launches = 0, atomic_launches = 0;  // (vpt_gpu_film_order_info)
+  // The drop-in's ordered frame (vpt_gpu_frame_open / _finish): its feed launches also store the samples of the
+  // frame's tiles [frame_tile_lo, + frame_tiles) from job frame_jid_lo on into the sample buffer above, frame_waves
+  // waves of those tiles (0: no frame open); the order pass writes frame_film (device, film_count floats), copied
+  // into the host film through staging.
+  uint64_t frame_waves = 0, frame_jid_lo = 0;
+  uint32_t frame_tile_lo = 0, frame_tiles = 0;
+  float* frame_film = nullptr;
   // vpt_gpu_create's phases (ms): grid flatten + majorant fix, grid upload, the rest, the tile-cost pass, device bind
   double setup_ms[5] = {};
 };

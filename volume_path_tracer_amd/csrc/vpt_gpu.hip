@@ -182,6 +182,7 @@ void destroy(vpt_gpu_ctx* ctx) {
   (void)hipFree(ctx->order);
   (void)hipFree(ctx->perm);
   (void)hipFree(ctx->samples);
+  (void)hipFree(ctx->frame_film);
   if (ctx->samples_done) (void)hipEventDestroy(ctx->samples_done);
   for (uint32_t i = 0; i < kLaunchSlots; ++i)
     if (ctx->slot_done[i]) (void)hipEventDestroy(ctx->slot_done[i]);
@@ -410,7 +411,8 @@ int vpt::host::render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, 
   }
   if (!feed && ctx->perm && ctx->perm_n == jid_count && !ctx->scene.pixel_mode) env.perm = ctx->perm;
   float* samples = nullptr;
-  if (ordered && (rc = ensure_samples(ctx, jid_count * per_job, samples))) return rc;
+  // (while the drop-in's ordered frame is open its feeds own the sample buffer: other launches add with atomics)
+  if (ordered && !ctx->frame_waves && (rc = ensure_samples(ctx, jid_count * per_job, samples))) return rc;
   env.samples = samples;
   if (samples) {
     ++ctx->ordered_launches;
@@ -430,6 +432,11 @@ int vpt::host::render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, 
   env.feed_waiting = feed ? feed->waiting : nullptr;
   env.feed_hint_mask = (uint32_t)(vpt::kHintSlots - 1);
   env.tile_done = feed ? feed->tile_done : nullptr;
+  env.frame = feed && ctx->frame_waves ? ctx->samples : nullptr;  // (the drop-in's ordered frame, vpt_gpu_frame_open)
+  env.frame_w0 = ctx->frame_jid_lo / ctx->scene.T;
+  env.frame_slots = env.frame ? ctx->frame_waves * ctx->frame_tiles : 0;
+  env.frame_tile_lo = ctx->frame_tile_lo;
+  env.frame_tiles = ctx->frame_tiles;
   env.compact_every = 0;
   env.event_count = ctx->job_counter + 2 * slot + 1;
   env.event_cap = event_cap;
@@ -1022,6 +1029,92 @@ int vpt_gpu_film_free(vpt_gpu_ctx* ctx, float* film_device) {
   int rc = ctx_device(ctx);
   if (rc) return rc;
   VPT_HIP(hipFree(film_device));
+  return VPT_OK;
+}
+
+// The largest ordered-frame buffer (the 4K, 1 024-spp C5 frame on one GPU needs 102 GB).
+constexpr uint64_t kFrameMaxBytes = 128ULL << 30;
+
+int vpt_gpu_frame_open(vpt_gpu_ctx* ctx, uint64_t jid_lo, uint64_t* waves_io, uint32_t tile_lo, uint32_t tile_hi) {
+  if (!ctx || !waves_io) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_frame_open: null argument");
+  uint64_t waves = *waves_io;
+  *waves_io = 0;
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  if (ctx->open_feeds.load() > 0)  // (allocating could wait for a running feed's launch)
+    return vpt::set_error(VPT_E_STATE, "vpt_gpu_frame_open: a feed of the context is open");
+  const vpt::DevScene& S = ctx->scene;
+  if (S.pixel_mode) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_frame_open: frames run the reference RNG mode");
+  ctx->frame_waves = 0;
+  if (waves == 0) return VPT_OK;
+  if (tile_lo >= tile_hi || tile_hi > S.T) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_frame_open: bad tile range");
+  const uint64_t per_wave = (uint64_t)(tile_hi - tile_lo) * (uint64_t)S.tile_area * 3 * sizeof(float);
+  // as many of the waves asked for as fit 3/4 of the device's free memory (the buffer already held counted in), at
+  // most kFrameMaxBytes
+  size_t free_b = 0, total_b = 0;
+  VPT_HIP(hipMemGetInfo(&free_b, &total_b));
+  const uint64_t avail = std::min<uint64_t>(kFrameMaxBytes, (uint64_t)free_b / 4 * 3 + ctx->samples_bytes);
+  waves = std::min<uint64_t>(waves, avail / per_wave);
+  if (waves == 0) return vpt::set_error(VPT_E_NOMEM, "vpt_gpu_frame_open: not one wave of the frame fits the device");
+  if (ctx->samples_used) VPT_HIP(hipEventSynchronize(ctx->samples_done));  // (an ordered launch's film pass)
+  float* buf = nullptr;
+  if ((rc = ensure_samples(ctx, waves * per_wave, buf))) return rc;
+  if (!buf) return vpt::set_error(VPT_E_STATE, "vpt_gpu_frame_open: the sample buffer cannot grow now");
+  if (!ctx->frame_film) VPT_HIP(hipMalloc((void**)&ctx->frame_film, ctx->film_count * sizeof(float)));
+  if (!ctx->staging) VPT_HIP(hipHostMalloc((void**)&ctx->staging, ctx->film_count * sizeof(float), hipHostMallocDefault));
+  ctx->frame_jid_lo = jid_lo;
+  ctx->frame_tile_lo = tile_lo;
+  ctx->frame_tiles = tile_hi - tile_lo;
+  ctx->frame_waves = waves;
+  *waves_io = waves;
+  return VPT_OK;
+}
+
+int vpt_gpu_frame_finish(vpt_gpu_ctx* ctx, uint64_t jid_end, const float* prior, float* film_host) {
+  if (!ctx || !film_host) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_frame_finish: null argument");
+  int rc = ctx_device(ctx);
+  if (rc) return rc;
+  const uint64_t waves = ctx->frame_waves, lo = ctx->frame_jid_lo;
+  if (!waves) return VPT_OK;  // no frame open
+  ctx->frame_waves = 0;       // (closed, whatever follows)
+  const vpt::DevScene& S = ctx->scene;
+  const uint64_t w0 = lo / S.T;
+  if (jid_end < lo || (jid_end > lo && (jid_end - 1) / S.T - w0 >= waves))
+    return vpt::set_error(VPT_E_INVALID, "vpt_gpu_frame_finish: jobs beyond the frame's waves");
+  if (ctx->open_feeds.load() > 0) return vpt::set_error(VPT_E_STATE, "vpt_gpu_frame_finish: a feed of the context is open");
+  if (jid_end == lo) return VPT_OK;
+  const size_t bytes = ctx->film_count * sizeof(float);
+  if (prior)
+    VPT_HIP(hipMemcpyAsync(ctx->frame_film, prior, bytes, hipMemcpyHostToDevice, ctx->stream));
+  else
+    VPT_HIP(hipMemsetAsync(ctx->frame_film, 0, bytes, ctx->stream));
+  const uint32_t tile_lo = ctx->frame_tile_lo, tiles = ctx->frame_tiles, tile_hi = tile_lo + tiles;
+  const uint64_t threads = (uint64_t)tiles * (uint64_t)S.tile_area;
+  hipLaunchKernelGGL(vpt::vpt_frame_order_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, ctx->stream,
+                     ctx->scene_dev, ctx->frame_film, ctx->samples, w0, tile_lo, tiles, lo, jid_end);
+  VPT_HIP(hipGetLastError());
+  VPT_HIP(hipEventRecord(ctx->samples_done, ctx->stream));  // (the next ordered launch waits for this pass)
+  ctx->samples_used = true;
+  VPT_HIP(hipMemcpyAsync(ctx->staging, ctx->frame_film, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  VPT_HIP(hipStreamSynchronize(ctx->stream));
+  // the tiles' pixels into the host film, one contiguous run per image row and tile row (tiles are row-major)
+  const uint64_t W = (uint64_t)S.W;
+  auto put = [&](uint64_t y, uint64_t x0, uint64_t x1) {
+    std::memcpy(film_host + (y * W + x0) * 4, ctx->staging + (y * W + x0) * 4, (x1 - x0) * 4 * sizeof(float));
+  };
+  if (S.single_pixel_enabled) {  // only that pixel has samples (worker.cpp:113-116)
+    if (S.sp_x >= 0 && S.sp_y >= 0 && S.sp_x < S.W && S.sp_y < S.H) {
+      const uint64_t t = (uint64_t)(S.sp_y / S.th) * S.ntx + (uint64_t)(S.sp_x / S.tw);
+      if (t >= tile_lo && t < tile_hi) put((uint64_t)S.sp_y, (uint64_t)S.sp_x, (uint64_t)S.sp_x + 1);
+    }
+    return VPT_OK;
+  }
+  const uint64_t ntx = (uint64_t)S.ntx;
+  for (uint64_t ty = tile_lo / ntx; ty * ntx < tile_hi; ++ty) {
+    const uint64_t a = std::max<uint64_t>(tile_lo, ty * ntx) - ty * ntx, b = std::min<uint64_t>(tile_hi, (ty + 1) * ntx) - ty * ntx;
+    const uint64_t x0 = a * (uint64_t)S.tw, x1 = std::min<uint64_t>(b * (uint64_t)S.tw, W);
+    for (uint64_t y = ty * (uint64_t)S.th; y < std::min<uint64_t>((ty + 1) * (uint64_t)S.th, (uint64_t)S.H); ++y) put(y, x0, x1);
+  }
   return VPT_OK;
 }
 

@@ -1238,6 +1238,7 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       } else {
         ln.rng = job_seed(S.seed, jid);
         lc.item_lo = (uint32_t)j;  // the job's index in the launch: its slot in the ordered film's samples
+        env.job_start(S, lc, jid);  // (a feed launch with an ordered frame: the job's slot there)
       }
       uint64_t tile = jid % S.T;
       lc.x0 = (int32_t)(tile % S.ntx) * S.tw;  // TileProvider::compute_tile_rect

@@ -76,6 +76,15 @@ struct KernelArgs {
   // samples[(j * tile_area + local pixel) * 3 + c] (j = the job's index in the launch, the records layout);
   // vpt_film_order_kernel then adds them into the film pixel by pixel in wave order.  nullptr: film atomics.
   float* samples;
+  // The drop-in's ordered frame (vpt_gpu_frame_open; feed launches only): the samples of job jid = w * T + t of the
+  // frame's tiles [frame_tile_lo, frame_tile_lo + frame_tiles) are also stored at frame + (slot * tile_area + local
+  // pixel) * 3, slot = (w - frame_w0) * frame_tiles + t - frame_tile_lo (< frame_slots, else not stored), and
+  // vpt_frame_order_kernel later adds them into the film in wave order.  nullptr: no frame (the film's atomics alone).
+  float* frame;
+  uint64_t frame_w0;
+  uint64_t frame_slots;
+  uint32_t frame_tile_lo;
+  uint32_t frame_tiles;
 };
 typedef const __attribute__((address_space(4))) KernelArgs* ArgsPtr;
 // This workgroup's event counters and (VPT_PROFILE builds) section cycles; the temperature kernel's LDS copy of
@@ -306,6 +315,25 @@ struct KernelEnvT {
     }
     return -1;
   }
+  // A job starts (its id jid): with an ordered frame, a feed lane keeps the address of the job's samples in its cold
+  // state (item_lo / item_hi: free once the job is read).  Other launches: nothing.
+  __device__ __forceinline__ void job_start(const DevScene& S, LaneCold& lc, uint64_t jid) {
+    if constexpr (Feed) {
+      if (float* const frame = args()->frame) {
+        const uint64_t w = jid / S.T;
+        const uint32_t tt = (uint32_t)(jid - w * S.T) - args()->frame_tile_lo;  // (wraps below the band: > tiles)
+        const uint64_t slot = (w - args()->frame_w0) * args()->frame_tiles + tt;
+        const bool in = tt < args()->frame_tiles && w >= args()->frame_w0 && slot < args()->frame_slots;
+        const uint64_t a = in ? (uint64_t)(frame + slot * (uint64_t)S.tile_area * 3) : 0;
+        lc.item_lo = (uint32_t)a;
+        lc.item_hi = (uint32_t)(a >> 32);
+      }
+    } else {
+      (void)S;
+      (void)lc;
+      (void)jid;
+    }
+  }
   // A job's last pixel is done: a staged feed counts it for its tile (the film's sample counts are the host's
   // per-tile job counts, vpt_gpu_feed_snapshot / _collect).  Once per job (64 samples); a uniform branch.
   __device__ __forceinline__ void job_end(const DevScene& S, const LaneCold& lc) {
@@ -336,6 +364,15 @@ struct KernelEnvT {
   }
   __device__ __forceinline__ void film_add(const DevScene& S, const Lane& ln, int32_t px, int32_t py, int32_t rw) {
     const LaneCold& lc = cold();
+    if constexpr (Feed) {  // the ordered frame's copy of the sample (the film's atomics below stay: the progressive film)
+      const uint64_t a = ((uint64_t)lc.item_hi << 32) | lc.item_lo;
+      if (args()->frame && a) {
+        float* s = reinterpret_cast<float*>(a) + (uint32_t)((py - lc.y0) * rw + (px - lc.x0)) * 3;
+        s[0] = lc.L[0];
+        s[1] = lc.L[1];
+        s[2] = lc.L[2];
+      }
+    }
     float* const samples = args()->samples;
     const uint32_t pixel = samples ? (uint32_t)((py - lc.y0) * rw + (px - lc.x0)) : (uint32_t)py * (uint32_t)S.W + (uint32_t)px;
     if (film_regroup(S)) {
@@ -639,6 +676,44 @@ __global__ void vpt_film_order_kernel(const DevScene* scene, float* film, const 
   const float* s = samples + ((t + k0 * T - jid_begin) * area + q) * 3;
   const uint64_t step = T * area * 3;
   const uint64_t n = (end - 1 - t) / T - k0 + 1;
+#pragma unroll 8
+  for (uint64_t k = 0; k < n; ++k, s += step) {
+    a.w = a.w + 1.0f;
+    a.x = a.x + r * s[0];
+    a.y = a.y + r * s[1];
+    a.z = a.z + r * s[2];
+  }
+  *f = a;
+}
+
+// The drop-in's ordered frame (vpt_gpu_frame_finish): the samples its feed launches stored for the jobs [jid_lo,
+// jid_end) of the frame's tiles [tile_lo, tile_lo + tiles) (slots as KernelArgs::frame), added pixel by pixel in
+// wave order onto film (the film before the frame, or zeros): w += 1, xyz += imaging_ratio * L per sample
+// (worker.cpp:203-204), as vpt_film_order_kernel.  Every job of those tiles in the range was rendered (one taker
+// hands out a contiguous range of job ids, vpt_run.hpp).
+__global__ void vpt_frame_order_kernel(const DevScene* scene, float* film, const float* frame, uint64_t w0, uint32_t tile_lo,
+                                       uint32_t tiles, uint64_t jid_lo, uint64_t jid_end) {
+  const DevScene& S = *scene;
+  const uint32_t area = S.tile_area;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint64_t)tiles * area) return;
+  const uint32_t tb = (uint32_t)(i / area);
+  const uint64_t t = tile_lo + tb;
+  const uint32_t q = (uint32_t)(i - (uint64_t)tb * area);
+  const int32_t x0 = (int32_t)(t % S.ntx) * S.tw, y0 = (int32_t)(t / S.ntx) * S.th;
+  const int32_t rw = min(S.W - x0, S.tw), rh = min(S.H - y0, S.th);
+  if ((int32_t)q >= rw * rh) return;
+  const int32_t yl = (int32_t)q / rw, px = x0 + ((int32_t)q - yl * rw), py = y0 + yl;
+  if (S.single_pixel_enabled && (px != S.sp_x || py != S.sp_y)) return;  // (no sample: worker.cpp:113-116)
+  const uint64_t T = S.T;
+  const uint64_t j0 = jid_lo + (t + T - jid_lo % T) % T;  // the tile's first job >= jid_lo
+  if (j0 >= jid_end) return;
+  float4* const f = reinterpret_cast<float4*>(film) + ((uint64_t)py * (uint64_t)S.W + (uint64_t)px);
+  float4 a = *f;
+  const float r = S.imaging_ratio;
+  const float* s = frame + (((j0 / T - w0) * tiles + tb) * area + q) * 3;
+  const uint64_t step = (uint64_t)tiles * area * 3;
+  const uint64_t n = (jid_end - 1 - j0) / T + 1;
 #pragma unroll 8
   for (uint64_t k = 0; k < n; ++k, s += step) {
     a.w = a.w + 1.0f;
