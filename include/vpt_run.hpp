@@ -226,9 +226,12 @@ class FeedPipeline {
           std::this_thread::sleep_for(std::chrono::microseconds(100));
       if (frc == VPT_OK) {
         std::lock_guard<std::mutex> lock(film_mutex());
-        frc = vpt_gpu_feed_collect(f, film_host_);
-        if (frame_on_) {  // the frame's tiles in wave order, over what the collect added (or the frame closed)
-          if (frc == VPT_OK && rc == VPT_OK && pushed_end_ <= frame_end_) {
+        // An ordered frame rewrites its tiles' pixels whole (this feed rendered no others): the feed's last
+        // delta is not added first, its film only cleared for the next use.  Else the collect adds it.
+        const bool order = frame_on_ && rc == VPT_OK && pushed_end_ <= frame_end_;
+        frc = order ? vpt_gpu_feed_destroy(f) : vpt_gpu_feed_collect(f, film_host_);
+        if (frame_on_) {  // the frame's tiles in wave order (or the frame closed: the atomics' film stands)
+          if (order && frc == VPT_OK) {
             frc = vpt_gpu_frame_finish(ctx_, pushed_end_, frame_.prior, film_host_);
           } else {
             uint64_t none = 0;
