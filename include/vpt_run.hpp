@@ -112,6 +112,34 @@ inline void drain_trace(const char* what, double a = 0, double b = 0) {
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   std::fprintf(stderr, "drain %10.2f ms %-10s %.0f %.0f\n", ms, what, a, b);
 }
+// The host film as it was before an ordered frame (vpt_gpu_frame_finish adds the frame's samples onto it), copied on
+// a thread of its own while the frame starts; get() is nullptr when it was all zeros (+0.0), the usual fresh film.
+// Joined (by any pipeline's thread, once) before anything writes the film: a small frame's launches, a pipeline's
+// first snapshot, its finish.
+struct PriorFilm {
+  std::vector<float> v;
+  bool zero = true;
+  std::thread th;
+  std::mutex mu;
+  void start(vpt_gpu_ctx* ctx, const float* film) {
+    float* dev = nullptr;
+    uint64_t n = 0;
+    if (vpt_gpu_film_device_ptr(ctx, &dev, &n) != VPT_OK) return;
+    th = std::thread([this, film, n] {
+      v.assign(film, film + n);
+      zero = std::all_of(v.begin(), v.end(), [](float x) { return std::bit_cast<uint32_t>(x) == 0u; });
+    });
+  }
+  void join() {
+    std::lock_guard<std::mutex> l(mu);
+    if (th.joinable()) th.join();
+  }
+  const float* get() {
+    join();
+    return zero ? nullptr : v.data();
+  }
+  ~PriorFilm() { join(); }
+};
 }  // namespace detail
 
 inline std::mutex& film_mutex() {  // the host film is shared by every caller
@@ -128,11 +156,11 @@ inline std::mutex& film_mutex() {  // the host film is shared by every caller
 class FeedPipeline {
  public:
   // An ordered frame (DrainOptions::ordered_frame): the jobs from jid_lo on of tiles [tile_lo, tile_hi), at most
-  // `waves` waves (the library may grant fewer), added in wave order onto `prior` (nullptr: zeros) at finish().
+  // `waves` waves (the library may grant fewer), added in wave order onto the film before the frame at finish().
   struct Frame {
     uint64_t jid_lo = 0, waves = 0;
     uint32_t tile_lo = 0, tile_hi = 0;
-    const float* prior = nullptr;
+    detail::PriorFilm* prior = nullptr;  // the film before the frame (joined before this pipeline writes the film)
   };
   std::atomic<int> helpers{0};  // help() threads attached (see detail::Helpers)
   explicit FeedPipeline(vpt_gpu_ctx* ctx) : ctx_(ctx) {}
@@ -144,6 +172,7 @@ class FeedPipeline {
   }
   int start(float* film_host, const DrainOptions& opt, const Frame* frame = nullptr) {
     film_host_ = film_host;
+    prior_ = frame ? frame->prior : nullptr;
     if (frame) {  // before the feed opens: the frame's memory is allocated now (vpt_gpu_frame_open)
       uint64_t T = 0, total = 0, waves = frame->waves;
       if (int rc = vpt_gpu_job_space(ctx_, &T, &total)) return rc;
@@ -224,6 +253,7 @@ class FeedPipeline {
       for (int done = 0; frc == VPT_OK && !done;)
         if ((frc = vpt_gpu_feed_query(f, &done, nullptr)) == VPT_OK && !done)
           std::this_thread::sleep_for(std::chrono::microseconds(100));
+      if (prior_) prior_->join();
       if (frc == VPT_OK) {
         std::lock_guard<std::mutex> lock(film_mutex());
         // An ordered frame rewrites its tiles' pixels whole (this feed rendered no others): the feed's last
@@ -232,7 +262,7 @@ class FeedPipeline {
         frc = order ? vpt_gpu_feed_destroy(f) : vpt_gpu_feed_collect(f, film_host_);
         if (frame_on_) {  // the frame's tiles in wave order (or the frame closed: the atomics' film stands)
           if (order && frc == VPT_OK) {
-            frc = vpt_gpu_frame_finish(ctx_, pushed_end_, frame_.prior, film_host_);
+            frc = vpt_gpu_frame_finish(ctx_, pushed_end_, frame_.prior ? frame_.prior->get() : nullptr, film_host_);
           } else {
             uint64_t none = 0;
             (void)vpt_gpu_frame_open(ctx_, 0, &none, 0, 0);
@@ -405,6 +435,7 @@ class FeedPipeline {
       }
       const auto period = std::chrono::duration_cast<std::chrono::steady_clock::duration>(std::chrono::duration<double>(flush_));
       next += period;
+      if (prior_) prior_->join();  // (the film before the frame is copied before it changes)
       {
         std::lock_guard<std::mutex> lock(film_mutex());
         if (int rc = vpt_gpu_feed_snapshot(feed_, film_host_)) return fail(rc);
@@ -430,6 +461,7 @@ class FeedPipeline {
   vpt_gpu_ctx* ctx_;
   float* film_host_ = nullptr;
   Frame frame_;
+  detail::PriorFilm* prior_ = nullptr;  // (joined before this pipeline writes the film)
   bool frame_on_ = false;
   uint64_t frame_end_ = 0, pushed_end_ = 0;  // (pushed_end_: the pusher's, read after it has ended)
   double flush_ = 0.2;
@@ -589,32 +621,6 @@ int take_head(vpt_gpu_ctx* ctx, Provider& tp, uint64_t batch_jobs, const DrainOp
 }  // namespace detail
 
 namespace detail {
-// The host film as it was before an ordered frame (vpt_gpu_frame_finish adds the frame's samples onto it), copied on
-// a thread of its own while the first tokens are taken; nullptr when it is all zeros (+0.0), the usual fresh film.
-struct PriorFilm {
-  std::vector<float> v;
-  bool zero = true;
-  std::thread th;
-  void start(vpt_gpu_ctx* ctx, const float* film) {
-    float* dev = nullptr;
-    uint64_t n = 0;
-    if (vpt_gpu_film_device_ptr(ctx, &dev, &n) != VPT_OK) return;
-    th = std::thread([this, film, n] {
-      v.assign(film, film + n);
-      zero = std::all_of(v.begin(), v.end(), [](float x) { return std::bit_cast<uint32_t>(x) == 0u; });
-    });
-  }
-  void join() {  // (before anything writes the film)
-    if (th.joinable()) th.join();
-  }
-  const float* get() {
-    join();
-    return zero ? nullptr : v.data();
-  }
-  ~PriorFilm() {
-    if (th.joinable()) th.join();
-  }
-};
 // An ordered frame is sized from the provider's progress() (percent of its jobs handed out, floored): until it
 // reads >= 1 the frame's size has no useful bound, so tokens are taken on until it does (1 % of the frame: C3 83 K
 // tokens, ~1 ms; C5 1.3 M, ~20 ms) or the provider runs dry (`dry`: the frame is what was taken).
@@ -638,7 +644,7 @@ int take_until_sized(Provider& tp, uint64_t batch_jobs, JobRuns& head, bool& dry
 // (vpt_gpu_frame_open grants what fits).
 template <class Provider>
 FeedPipeline::Frame frame_of(Provider& tp, const JobRuns& head, uint64_t T, uint32_t tile_lo, uint32_t tile_hi,
-                             const float* prior, bool dry = false) {
+                             PriorFilm* prior, bool dry = false) {
   FeedPipeline::Frame fr;
   fr.jid_lo = head.empty() ? 0 : head.front().first;
   uint64_t end = 0;
@@ -705,8 +711,10 @@ int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs,
     bool small = false;
     detail::drain_trace("drain");
     if (int rc = detail::take_head(ctx, tp, batch_jobs, opt, first, head, small)) return rc;
-    prior.join();
-    if (small) return detail::render_runs(ctx, head, film_host);
+    if (small) {
+      prior.join();  // (before the launches' films are added)
+      return detail::render_runs(ctx, head, film_host);
+    }
     first = &head;
   }
   detail::drain_trace("head_taken");
@@ -717,7 +725,7 @@ int drain(vpt_gpu_ctx* ctx, Provider& tp, float* film_host, uint64_t batch_jobs,
     bool dry = false;
     if (int rc = vpt_gpu_job_space(ctx, &T, &total)) return rc;
     if (int rc = detail::take_until_sized(tp, batch_jobs, head, dry)) return rc;
-    frame = detail::frame_of(tp, head, T, 0, (uint32_t)T, prior.get(), dry);
+    frame = detail::frame_of(tp, head, T, 0, (uint32_t)T, &prior, dry);
   }
   int rc = pipe.start(film_host, opt, ordered ? &frame : nullptr);
   if (rc == VPT_OK && first) rc = pipe.add(*first);
@@ -789,8 +797,10 @@ int drain_devices(const std::vector<vpt_gpu_ctx*>& ctxs, Provider& tp, float* fi
   JobRuns head;
   bool small = false;
   if (int rc = detail::take_head(ctxs[0], tp, batch_jobs, opt, first, head, small)) return rc;
-  prior.join();
-  if (small) return detail::render_runs_split(ctxs, head, film_host);
+  if (small) {
+    prior.join();  // (before the launches' films are added)
+    return detail::render_runs_split(ctxs, head, film_host);
+  }
   std::vector<std::unique_ptr<FeedPipeline>> pipes;
   int rc = VPT_OK;
   // An ordered frame: each GPU owns a band of tiles (about equal estimated cost, vpt_gpu_tile_costs) and renders
@@ -809,7 +819,7 @@ int drain_devices(const std::vector<vpt_gpu_ctx*>& ctxs, Provider& tp, float* fi
   for (size_t i = 0; i < ctxs.size(); ++i) {
     pipes.push_back(std::make_unique<FeedPipeline>(ctxs[i]));
     FeedPipeline::Frame frame;
-    if (opt.ordered_frame) frame = detail::frame_of(tp, head, T, cut[i], cut[i + 1], prior.get(), dry);
+    if (opt.ordered_frame) frame = detail::frame_of(tp, head, T, cut[i], cut[i + 1], &prior, dry);
     if (rc == VPT_OK) rc = pipes.back()->start(film_host, opt, opt.ordered_frame ? &frame : nullptr);
   }
   std::vector<JobRuns> parts(opt.ordered_frame ? ctxs.size() : 0);
