@@ -1059,6 +1059,24 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   }
   lap(ph.first_batch_ms);
 
+  // the film in wave order, bit-identical to the reference's (VPT_DROPIN_ORDERED=0: the feeds' atomics alone)
+  DrainOptions dopt;
+  const char* ord = std::getenv("VPT_DROPIN_ORDERED");
+  dopt.ordered_frame = !(ord && std::atoi(ord) == 0);
+  if (const char* db = std::getenv("VPT_DROPIN_DIRECT_BELOW"))  // (tests: 1 = a feed even for a small frame)
+    dopt.direct_below = (uint64_t)std::atoll(db);
+  // An ordered frame is sized from progress() (detail::take_until_sized): the tokens up to 1 % of the frame are
+  // taken on a thread of their own beside the setup below, so one GPU's frame memory is allocated with its context.
+  bool dry = false;
+  std::thread sizer;
+  if (dopt.ordered_frame) sizer = std::thread([&] { (void)detail::take_until_sized(tp, 4096, runs, dry); });
+  struct Join {
+    std::thread& t;
+    ~Join() {
+      if (t.joinable()) t.join();
+    }
+  } join_sizer{sizer};
+
   // The HIP runtime's start and the seed recovery (one GPU launch) run on a helper thread while this one reads
   // the NanoGrids and flattens them (host work): their phases overlap.
   vpt_configuration cfg;
@@ -1137,9 +1155,21 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   if (int rc = vpt_gpu_create_from(&cfg, flat.g, nullptr, devices.data(), ndev, ctxs.data())) return rc;
   const auto t_feeds = clk::now();
   std::vector<int> crc((size_t)ndev, VPT_OK);
+  if (sizer.joinable()) sizer.join();
   auto prepare = [&](int d) {
     int rc = vpt_gpu_feed_prepare(ctxs[(size_t)d], 0, 1);
     if (rc == VPT_OK) rc = vpt_gpu_tile_costs(ctxs[(size_t)d], nullptr, nullptr);
+    if (rc == VPT_OK && dopt.ordered_frame && ndev == 1) {  // the frame's memory now (drain's frame then reuses it)
+      uint64_t T = 0, total = 0, none = 0;
+      if ((rc = vpt_gpu_job_space(ctxs[0], &T, &total)) == VPT_OK) {
+        FeedPipeline::Frame fr = detail::frame_of(tp, runs, T, 0, (uint32_t)T, nullptr, dry);
+        int blocks = 0, threads = 0;
+        (void)vpt_gpu_launch_info(ctxs[0], &blocks, &threads);
+        const bool small = fr.waves < (~0ULL >> 8) && fr.waves * T < (uint64_t)blocks * (uint64_t)threads;  // (no feed)
+        if (!small && vpt_gpu_frame_open(ctxs[0], fr.jid_lo, &fr.waves, 0, (uint32_t)T) == VPT_OK)
+          (void)vpt_gpu_frame_open(ctxs[0], 0, &none, 0, 0);
+      }
+    }
     if (rc != VPT_OK)  // (vpt_last_error is per thread: say it here)
       std::fprintf(stderr, "vpt_gpu::run: device %d: %s\n", d, vpt_last_error());
     crc[(size_t)d] = rc;
@@ -1165,12 +1195,6 @@ int run_checked(const WorkerParameters& params, const Volume& vol, const Camera&
   // (Leader), so the slot is never shared; flat now holds the previous call's copies, released at this call's end.
   static detail::OwnedGrids kept;
   std::swap(kept.g, flat.g);
-  // the film in wave order, bit-identical to the reference's (VPT_DROPIN_ORDERED=0: the feeds' atomics alone)
-  DrainOptions dopt;
-  const char* ord = std::getenv("VPT_DROPIN_ORDERED");
-  dopt.ordered_frame = !(ord && std::atoi(ord) == 0);
-  if (const char* db = std::getenv("VPT_DROPIN_DIRECT_BELOW"))  // (tests: 1 = a feed even for a small frame)
-    dopt.direct_below = (uint64_t)std::atoll(db);
   const int rc = drain_devices(ctxs, tp, film_host, 4096, dopt, &runs);
   lap(ph.frame_ms);
   ph.total_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
