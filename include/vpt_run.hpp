@@ -799,7 +799,9 @@ int drain_devices(const std::vector<vpt_gpu_ctx*>& ctxs, Provider& tp, float* fi
   if (int rc = detail::take_head(ctxs[0], tp, batch_jobs, opt, first, head, small)) return rc;
   if (small) {
     prior.join();  // (before the launches' films are added)
-    return detail::render_runs_split(ctxs, head, film_host);
+    // (parts on several GPUs would add into the film one after another, not in wave order: an ordered frame's
+    // small frame renders on the first GPU)
+    return opt.ordered_frame ? detail::render_runs(ctxs[0], head, film_host) : detail::render_runs_split(ctxs, head, film_host);
   }
   std::vector<std::unique_ptr<FeedPipeline>> pipes;
   int rc = VPT_OK;

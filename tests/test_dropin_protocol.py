@@ -57,7 +57,9 @@ def test_dropin_protocol_renders_every_token_once(args):
     for _ in range(3):
         r = subprocess.run([str(MOCK), *args.split()], capture_output=True, text=True, timeout=120, env=env)
         assert r.returncode == 0 and "dropin_mock: ok" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
-        if "w=16" in args or "w=24" in args:  # the whole frame in direct launches
+        if "w=24" in args and "ordered=1" in args and "devices=" in args:  # one GPU's launches (wave order)
+            assert "max 0 feeds open" in r.stdout, r.stdout
+        elif "w=16" in args or "w=24" in args:  # the whole frame in direct launches
             assert ", 0 jobs in direct launches" not in r.stdout and "max 0 feeds open" in r.stdout, r.stdout
         elif "multi=1 devices=8" in args:  # every mock GPU got a feed of its own
             assert "max 8 feeds open" in r.stdout, r.stdout

@@ -176,6 +176,23 @@ def test_one_taker_drives_several_contexts(tmp_path, ctxs, ordered):
 
 
 @pytest.mark.gpu
+@pytest.mark.spawns
+def test_one_taker_small_ordered_frame_on_several_contexts(tmp_path):
+    """A frame smaller than one launch's lanes through drain_devices with the ordered frame: jid-range launches on
+    the first context (parts on several would add into the film one after another) -- the oracle's film bit for
+    bit."""
+    assert_hip_untouched()
+    w, h, waves = 48, 32, 3
+    out = tmp_path / "film.f32"
+    args = [str(HARNESS), f"config={SCENE_DIR / 'wdas_cloud.json'}", f"out={out}", f"w={w}", f"h={h}",
+            f"waves={waves}", "threads=3", "batch=16", "grid_n=64", "multi=1", "devices=1", "grid_blocks=8", "ordered=1"]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    film = np.fromfile(out, np.float32).reshape(h, w, 4)
+    _assert_bitwise(film, _oracle_film("c3", w, h, waves))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("devices", [1, 2, 8])
 def test_mock_taker_rate_on_the_box(devices):
     """On the GPU box's own cores (no GPU used): one taker feeding 1 / 2 / 8 mock GPUs keeps >= 0.9x the rate
