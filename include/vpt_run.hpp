@@ -782,7 +782,8 @@ int help(Provider& tp, uint64_t batch_jobs) {
 // and feeds every GPU from it: one FeedPipeline (staged feed, pusher and film threads) per context, each batch
 // routed to the GPU that needs it -- first to each GPU in turn until its launch has a lane's worth (a feed's
 // launch starts then), afterwards to the GPU with the fewest jobs given and not yet started (FeedPipeline::
-// pending).  The provider's token rate is the frame's floor: C3's 8.3 M tokens take 124 ms on one thread, so
+// pending); with the ordered frame (what run() sets) each job goes to the GPU that owns its tile (cost-balanced
+// bands of tiles, so every pixel's samples are ordered on one GPU).  The provider's token rate is the frame's floor: C3's 8.3 M tokens take 124 ms on one thread, so
 // the 8-GPU drop-in frame is ~125-145 ms however fast the GPUs are; north_star's >= 6x at 8 GPUs
 // is reachable through the C ABI's jid ranges (distributed.py, bench.py), not through a TileProvider.
 // One context: exactly drain().  Small frames (the provider dry before a lane's worth): jid-range launches
