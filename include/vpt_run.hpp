@@ -623,17 +623,22 @@ int take_head(vpt_gpu_ctx* ctx, Provider& tp, uint64_t batch_jobs, const DrainOp
 namespace detail {
 // An ordered frame is sized from the provider's progress() (percent of its jobs handed out, floored): until it
 // reads >= 1 the frame's size has no useful bound, so tokens are taken on until it does (1 % of the frame: C3 83 K
-// tokens, ~1 ms; C5 1.3 M, ~20 ms) or the provider runs dry (`dry`: the frame is what was taken).
+// tokens, ~1 ms; C5 1.3 M, ~20 ms) or the provider runs dry (`dry`: the frame is what was taken) -- at most
+// kSizeTokens of them (a frame of more than 400 M jobs is then sized by the device's memory).
+constexpr uint64_t kSizeTokens = 4u << 20;
 template <class Provider>
 int take_until_sized(Provider& tp, uint64_t batch_jobs, JobRuns& head, bool& dry) {
   dry = false;
   if constexpr (requires { tp.progress(); }) {
     JobRuns more;
-    while (tp.progress() == 0) {
-      if (!take_jobs(tp, std::max<uint64_t>(1, batch_jobs), more, [](auto&) {})) {
+    uint64_t taken = 0;
+    while (tp.progress() == 0 && taken < kSizeTokens) {
+      const uint64_t n = take_jobs(tp, std::max<uint64_t>(1, batch_jobs), more, [](auto&) {});
+      if (!n) {
         dry = true;
         break;
       }
+      taken += n;
       append_runs(head, more);
     }
   }
