@@ -22,6 +22,12 @@
       return ::vpt::set_error(VPT_E_HIP, std::string(#call " failed: ") + hipGetErrorString(e_));            \
   } while (0)
 
+// The density-only kernel takes its run-skipping variant when this share of the interior cells has a run
+// radius >= 2 (C2's cube: 1.0; the cloud: below it).
+#ifndef VPT_RUNS_MIN_FRACTION
+#define VPT_RUNS_MIN_FRACTION 0.25
+#endif
+
 namespace vpt {
 struct DeviceGrid {
   void* cells8 = nullptr;

@@ -601,7 +601,7 @@ int create_on(const vpt_configuration* cfg, const HostGrids& grids, const float*
   // The run-skipping kernel variant is for grids with large equal-majorant regions (C2's constant
   // cube: 36 % of the interior cells have run radius >= 2; the 512^3 cloud: 4 %, where the variant
   // would cost more than it skips).  vpt_gpu_set_run_skipping overrides the choice.
-  ctx->use_runs = !has_temperature && ctx->density.run_fraction >= 0.25;
+  ctx->use_runs = !has_temperature && ctx->density.run_fraction >= VPT_RUNS_MIN_FRACTION;
   ctx->scene.density = ctx->density.dev;
   vpt::scene_finalize(ctx->scene);  // uses only the density map (host copy of the values)
   ctx->scene.temperature = ctx->temperature.dev;
@@ -846,7 +846,7 @@ int vpt_gpu_set_run_skipping(vpt_gpu_ctx* ctx, int mode) {
   if (!ctx || mode < -1 || mode > 1) return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_run_skipping: bad argument");
   if (mode == 1 && ctx->scene.has_temperature)
     return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_run_skipping: no run-skipping variant with a temperature grid");
-  ctx->use_runs = mode < 0 ? (!ctx->scene.has_temperature && ctx->density.run_fraction >= 0.25) : mode == 1;
+  ctx->use_runs = mode < 0 ? (!ctx->scene.has_temperature && ctx->density.run_fraction >= VPT_RUNS_MIN_FRACTION) : mode == 1;
   return VPT_OK;
 }
 

@@ -141,17 +141,31 @@ __host__ __device__ __forceinline__ int32_t cell8_code(int32_t x) {
 }
 __host__ __device__ __forceinline__ bool cell8_interior(int32_t x) { return ((x ^ (x << 1)) & (1 << 31)) != 0; }
 
+// Row-major index (a * n1 + b) * n2 + c of a table cell (a, b, c inside the table).  Experiment
+// (VPT_WALK_MAD24_ASM): two full-rate v_mad_u32_u24, whose operands are below 2^24 for tables of up to 4096
+// cells a side; the compiler otherwise emits v_mad_u64_u32 for these.
+__host__ __device__ __forceinline__ uint32_t mad_index(int32_t a, int32_t b, int32_t c, const int32_t n[3]) {
+#if defined(__HIP_DEVICE_COMPILE__) && VPT_WALK_MAD24_ASM
+  uint32_t ab, idx;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(ab) : "v"(a), "s"(n[1]), "v"(b));
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(idx) : "v"(ab), "s"(n[2]), "v"(c));
+  return idx;
+#else
+  return ((uint32_t)a * (uint32_t)n[1] + (uint32_t)b) * (uint32_t)n[2] + (uint32_t)c;
+#endif
+}
+
 __host__ __device__ __forceinline__ Cell cell_at(const DevGrid& g, int32_t i, int32_t j, int32_t k) {
   int32_t a = (i - g.r8_org[0]) >> 3, b = (j - g.r8_org[1]) >> 3, c = (k - g.r8_org[2]) >> 3;
   if ((uint32_t)a < (uint32_t)g.r8_n[0] && (uint32_t)b < (uint32_t)g.r8_n[1] && (uint32_t)c < (uint32_t)g.r8_n[2]) {
-    int2 e = g.cells8[((uint32_t)a * (uint32_t)g.r8_n[1] + (uint32_t)b) * (uint32_t)g.r8_n[2] + (uint32_t)c];
+    int2 e = g.cells8[mad_index(a, b, c, g.r8_n)];
     return Cell{cell8_code(e.x), math::as_f32((uint32_t)e.y)};
   }
   a = (i - g.r128_org[0]) >> 7;
   b = (j - g.r128_org[1]) >> 7;
   c = (k - g.r128_org[2]) >> 7;
   if ((uint32_t)a < (uint32_t)g.r128_n[0] && (uint32_t)b < (uint32_t)g.r128_n[1] && (uint32_t)c < (uint32_t)g.r128_n[2]) {
-    int2 e = g.cells128[((uint32_t)a * (uint32_t)g.r128_n[1] + (uint32_t)b) * (uint32_t)g.r128_n[2] + (uint32_t)c];
+    int2 e = g.cells128[mad_index(a, b, c, g.r128_n)];
     return Cell{e.x, math::as_f32((uint32_t)e.y)};
   }
   for (int32_t r = 0; r < g.root_count; ++r) {
@@ -595,7 +609,15 @@ inline uint64_t g_walk_outside = 0;
 // affine map.
 __host__ __device__ __forceinline__ uint32_t walk_index(const DevGrid& g, const int32_t v[3]) {
   const uint32_t a = (uint32_t)v[0], b = (uint32_t)v[1], c = (uint32_t)v[2];
+#if defined(__HIP_DEVICE_COMPILE__) && VPT_WALK_MAD24_ASM
+  // Experiment: two full-rate v_mad_u32_u24 (the compiler otherwise folds the first mul24 + add into a
+  // v_mad_u64_u32).  The instruction masks its operands to 24 bits as mul24 does: the same value.
+  uint32_t ab, idx;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(ab) : "v"(a), "s"((uint32_t)g.w8_n[1]), "v"(b));
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(idx) : "v"(ab), "s"((uint32_t)g.w8_n[2]), "v"(c));
+#else
   const uint32_t idx = math::mul24(math::mul24(a, (uint32_t)g.w8_n[1]) + b, (uint32_t)g.w8_n[2]) + c;
+#endif
   return idx < g.w8_max ? idx : g.w8_max;
 }
 
