@@ -141,9 +141,12 @@ __host__ __device__ __forceinline__ int32_t cell8_code(int32_t x) {
 }
 __host__ __device__ __forceinline__ bool cell8_interior(int32_t x) { return ((x ^ (x << 1)) & (1 << 31)) != 0; }
 
-// Row-major index (a * n1 + b) * n2 + c of a table cell (a, b, c inside the table).  Experiment
-// (VPT_WALK_MAD24_ASM): two full-rate v_mad_u32_u24, whose operands are below 2^24 for tables of up to 4096
-// cells a side; the compiler otherwise emits v_mad_u64_u32 for these.
+// Row-major index (a * n1 + b) * n2 + c of a table cell (a, b, c inside the table): two full-rate
+// v_mad_u32_u24, whose operands are below 2^24 for tables of up to 4096 cells a side; the compiler otherwise
+// emits v_mad_u64_u32 for these (r06zb, with walk_index's: C3 335.6 / 336.4 vs 336.6 / 337.3 ms, C4 flat).
+#ifndef VPT_WALK_MAD24_ASM
+#define VPT_WALK_MAD24_ASM 1
+#endif
 __host__ __device__ __forceinline__ uint32_t mad_index(int32_t a, int32_t b, int32_t c, const int32_t n[3]) {
 #if defined(__HIP_DEVICE_COMPILE__) && VPT_WALK_MAD24_ASM
   uint32_t ab, idx;
@@ -610,8 +613,7 @@ inline uint64_t g_walk_outside = 0;
 __host__ __device__ __forceinline__ uint32_t walk_index(const DevGrid& g, const int32_t v[3]) {
   const uint32_t a = (uint32_t)v[0], b = (uint32_t)v[1], c = (uint32_t)v[2];
 #if defined(__HIP_DEVICE_COMPILE__) && VPT_WALK_MAD24_ASM
-  // Experiment: two full-rate v_mad_u32_u24 (the compiler otherwise folds the first mul24 + add into a
-  // v_mad_u64_u32).  The instruction masks its operands to 24 bits as mul24 does: the same value.
+  // Two full-rate v_mad_u32_u24 (the compiler otherwise folds the first mul24 + add into a v_mad_u64_u32).  The instruction masks its operands to 24 bits as mul24 does: the same value.
   uint32_t ab, idx;
   asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(ab) : "v"(a), "s"((uint32_t)g.w8_n[1]), "v"(b));
   asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(idx) : "v"(ab), "s"((uint32_t)g.w8_n[2]), "v"(c));
