@@ -358,12 +358,24 @@ int vpt_gpu_kernel_variant(const vpt_gpu_ctx* ctx, int* has_temperature, int* ru
  * VPT_ORDER_COST_WAVE_MAJOR: wave by wave, each wave's tiles costliest first.
  * VPT_ORDER_COST_TILE_MAJOR: the whole range as one costliest-first list -- tiles ranked by cost in
  * groups of 64, each group's waves consecutively (64 lanes = 64 tiles of one wave).
- * VPT_ORDER_COST_TAIL (default): wave-major, then the last ~6 x (resident lanes / T) waves
+ * VPT_ORDER_COST_TAIL: wave-major, then the last ~6 x (resident lanes / T) waves
  * tile-major, so the launch drains on cheap (sky) jobs without concentrating the whole launch on
- * the densest tiles.  Costs: vpt_gpu_tile_costs.  Other ranges run in jid order. */
-enum { VPT_ORDER_JID = 0, VPT_ORDER_COST_WAVE_MAJOR = 1, VPT_ORDER_COST_TILE_MAJOR = 2, VPT_ORDER_COST_TAIL = 3 };
+ * the densest tiles.
+ * VPT_ORDER_COST_SAME_TILE (default): tile by tile, costliest first, each tile's waves consecutively --
+ * the 64 lanes of a wavefront take one tile's jobs of 64 waves, so they trace the same pixels and their
+ * rays walk the same cells until they scatter; the range drains on the cheapest tiles.  Launches that
+ * add with film atomics (the ordered film off, feeds, debug launches) take VPT_ORDER_COST_TAIL instead:
+ * 64 lanes would add to one pixel at once.  Costs: vpt_gpu_tile_costs.  Other ranges run in jid order. */
+enum {
+  VPT_ORDER_JID = 0,
+  VPT_ORDER_COST_WAVE_MAJOR = 1,
+  VPT_ORDER_COST_TILE_MAJOR = 2,
+  VPT_ORDER_COST_TAIL = 3,
+  VPT_ORDER_COST_SAME_TILE = 4
+};
 int vpt_gpu_set_job_order(vpt_gpu_ctx* ctx, int mode);
-/* VPT_ORDER_COST_TAIL's tile-major wave count (0 = auto: 6 x resident lanes / T, rounded up). */
+/* VPT_ORDER_COST_TAIL's tile-major wave count (0 = auto: 6 x resident lanes / T, rounded up); also the
+ * fallback of VPT_ORDER_COST_SAME_TILE. */
 int vpt_gpu_set_job_order_tail(vpt_gpu_ctx* ctx, int waves);
 /* The per-tile cost estimates (float[T], may be NULL) and the tile ranks by descending cost
  * (uint32[T], may be NULL): HDDA steps + 4 x majorant optical depth of 5 primary rays per tile. */

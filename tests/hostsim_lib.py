@@ -50,7 +50,7 @@ def fptr(a):
 def render_jobs(cfg, density, temperature, jid_begin, jid_count, records=False, bb=None, rng_mode=0, order=None,
                 tail_waves=0):
     """order: tile ranks (uint32[T]) for a whole-wave range, taken in the GPU's job-order mapping
-    (ordered_job) with the last tail_waves waves tile-major."""
+    (ordered_job) with the last tail_waves waves tile-major (-1: the same-tile order)."""
     film = np.zeros((cfg.height, cfg.width, 4), np.float32)
     tile_area = int(cfg.tile_size[0] * cfg.tile_size[1])
     rec = np.full((jid_count * tile_area, 3), np.nan, np.float32) if records else None

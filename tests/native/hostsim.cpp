@@ -33,6 +33,7 @@ struct HostEnv {
   const uint32_t* perm = nullptr;   // explicit job order (vpt_gpu_set_job_permutation)
   uint32_t order_tail_k0 = 0;
   uint32_t order_tail_n = 0;
+  uint32_t order_group = vpt::kOrderGroup;
   const HostEnv* args() const { return this; }  // (the kernel reads its launch arguments through args())
   int32_t count(bool pred) { return pred ? 1 : 0; }  // one lane
   vpt::LaneCold cold_{};
@@ -82,7 +83,8 @@ struct HostEnv {
 }  // namespace
 
 // order != nullptr: [jid_begin, jid_begin + jid_count) is whole waves and items are taken in the
-// kernel's cost order (order = tile ranks; the last tail_waves waves tile-major, see ordered_job).
+// kernel's cost order (order = tile ranks; the last tail_waves waves tile-major, see ordered_job; tail_waves < 0:
+// the same-tile order).
 extern "C" int vpths_render_jobs_order(const vpt_configuration* cfg, const vpt_grid_desc* density,
                                        const vpt_grid_desc* temperature, const float* bb500, uint64_t jid_begin,
                                        uint64_t jid_count, float* film, float* records, vpt_counters* counters,
@@ -121,6 +123,10 @@ extern "C" int vpths_render_jobs_order(const vpt_configuration* cfg, const vpt_g
               S.pixel_mode ? g_pixel_chunk : 1u};
   if (order) {
     env.order = order;
+    if (tail_waves < 0) {  // VPT_ORDER_COST_SAME_TILE: every wave tile-major, one tile per group
+      tail_waves = (int)(jid_count / S.T);
+      env.order_group = 1;
+    }
     env.order_tail_n = (uint32_t)tail_waves;
     env.order_tail_k0 = (uint32_t)(jid_count - (uint64_t)tail_waves * S.T);
   }

@@ -44,7 +44,7 @@ def test_orders_render_the_same_film(setup):
     base = _frame(it)
     _check(base, film_o)
     for mode in (capi.VPT_ORDER_JID, capi.VPT_ORDER_COST_WAVE_MAJOR, capi.VPT_ORDER_COST_TILE_MAJOR,
-                 capi.VPT_ORDER_COST_TAIL):
+                 capi.VPT_ORDER_COST_TAIL, capi.VPT_ORDER_COST_SAME_TILE):
         it.set_job_order(mode)
         _check(_frame(it), film_o)
     # caller-supplied costs: the reverse of the estimates

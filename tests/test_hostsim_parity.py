@@ -105,7 +105,7 @@ def test_tiles_only_grid():
     assert c_o["draws"] > 0 and c_o["draws"] == c_h["draws"]
 
 
-@pytest.mark.parametrize("tail_waves", [0, 1, 3])
+@pytest.mark.parametrize("tail_waves", [0, 1, 3, -1])
 @pytest.mark.parametrize("size", [(40, 24), (80, 72), (64, 64)])
 def test_job_order_permutation_keeps_samples(tail_waves, size):
     """The kernel's cost-ordered scheduling (vpt_gpu_set_job_order) maps items onto the same jobs:

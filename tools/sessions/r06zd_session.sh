@@ -1,0 +1,13 @@
+#!/bin/bash
+# r06zd: evidence on the final binary (full-rate table indexes): the whole GPU suite and smoke, then the roofline
+# inputs (PMC traffic + kernel trace, the C3 bench line; kernel counter passes) for C3 and C4, and C4's bench line.
+set -u
+export TMPDIR=/tmp
+STEPS="pytest smoke" bash tools/gpu_check.sh r06zd || exit $?
+grep -E "passed|failed" gpurun_out/r06zd/pytest_gpu.log | tail -1
+bash tools/profile_round.sh r06zd c3 || exit $?
+bash tools/profile_round.sh r06zd c4 || exit $?
+bash tools/kernel_counters.sh r06zd c3 || exit $?
+bash tools/kernel_counters.sh r06zd c4 || exit $?
+timeout -k 10 300 python bench.py --config c4 --steps 5 --warmup 1 --cpu-budget 6 > gpurun_out/r06zd/bench_c4.json 2> gpurun_out/r06zd/bench_c4.err || exit 1
+for f in gpurun_out/r06zd_c3/bench.log gpurun_out/r06zd/bench_c4.json; do python3 -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); x=d['dropin']; print('$f', d['value'], d['ms_per_step'], d['roofline']['frac'], d['parity'].get('bit_identical'), {k: x.get(k) for k in ['ms_frames','bit_identical_to_one_launch']}, x['first_call'].get('total_ms'))"; done

@@ -97,6 +97,7 @@ DDA_ROW_DTYPE = np.dtype([("ijk", "<i4", (3,)), ("t", "<f4"), ("value", "<f4"), 
 assert DDA_ROW_DTYPE.itemsize == 36
 VPT_RNG_REFERENCE, VPT_RNG_PIXEL = 0, 1
 VPT_ORDER_JID, VPT_ORDER_COST_WAVE_MAJOR, VPT_ORDER_COST_TILE_MAJOR, VPT_ORDER_COST_TAIL = 0, 1, 2, 3
+VPT_ORDER_COST_SAME_TILE = 4
 VPT_FILM_ATOMIC, VPT_FILM_ORDERED = 0, 1
 EVENT_NAMES = ("new_ray", "sampled_point", "null", "scatter_terminated", "scatter", "absorbed")
 

@@ -22,8 +22,13 @@
       return ::vpt::set_error(VPT_E_HIP, std::string(#call " failed: ") + hipGetErrorString(e_));            \
   } while (0)
 
+// A context's job order (vpt_gpu_set_job_order); A/B builds override it.
+#ifndef VPT_DEFAULT_JOB_ORDER
+#define VPT_DEFAULT_JOB_ORDER VPT_ORDER_COST_SAME_TILE
+#endif
+
 // The density-only kernel takes its run-skipping variant when this share of the interior cells has a run
-// radius >= 2 (C2's cube: 1.0; the cloud: below it).
+// radius >= 2 (C2's cube: 1.0; the cloud: below it; r06zb: C3 on it 21 % slower).
 #ifndef VPT_RUNS_MIN_FRACTION
 #define VPT_RUNS_MIN_FRACTION 0.25
 #endif
@@ -89,7 +94,7 @@ struct vpt_gpu_ctx {
   int grid_blocks = 0;               // resident capacity (or the set_tuning override)
   int cus = 1;                       // compute units of the device
   bool grid_user = false;            // grid_blocks set by vpt_gpu_set_tuning: use it as is
-  int order_mode = VPT_ORDER_COST_TAIL;
+  int order_mode = VPT_DEFAULT_JOB_ORDER;
   int order_tail_waves = 0;        // VPT_ORDER_COST_TAIL: tile-major waves (0 = auto)
   uint32_t* order = nullptr;       // tile ranks by descending cost (device), built on first use
   std::vector<float> tile_cost;    // host copy of the estimates

@@ -347,6 +347,7 @@ int vpt::host::render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, 
   env.perm = nullptr;
   env.order_tail_k0 = 0;
   env.order_tail_n = 0;
+  env.order_group = vpt::kOrderGroup;
   // Partly filled launches (a few work items per resident lane: small frames, few waves, a GPU's share
   // of a frame dealt over several): a launch lasts as long as its slowest jobs, and a job's lane runs
   // faster with fewer waves per SIMD, so the grid is sized to round(1 + 1.8 x) blocks per CU (at most
@@ -398,8 +399,12 @@ int vpt::host::render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, 
     if ((rc = ensure_order(ctx))) return rc;
     const uint32_t n = (uint32_t)(jid_count / T);
     uint32_t tail = 0;  // VPT_ORDER_COST_WAVE_MAJOR
-    if (ctx->order_mode == VPT_ORDER_COST_TILE_MAJOR) tail = n;
-    if (ctx->order_mode == VPT_ORDER_COST_TAIL) {
+    // same-tile order only where each sample has a slot of its own (the ordered film): with film atomics a
+    // wavefront's 64 lanes would add to one pixel at once
+    const bool same_tile = ctx->order_mode == VPT_ORDER_COST_SAME_TILE && ordered && !ctx->frame_waves;
+    if (ctx->order_mode == VPT_ORDER_COST_TILE_MAJOR || same_tile) tail = n;
+    if (same_tile) env.order_group = 1;
+    if (ctx->order_mode == VPT_ORDER_COST_TAIL || (ctx->order_mode == VPT_ORDER_COST_SAME_TILE && !same_tile)) {
       // the last ~6 x (resident lanes / T) waves (C3: 61 of 256): measured best of 2x..16x
       const uint64_t lanes = (uint64_t)blocks * vpt::kBlockThreads;
       const uint64_t want = ctx->order_tail_waves > 0 ? (uint64_t)ctx->order_tail_waves : (6 * lanes + T - 1) / T;
@@ -884,7 +889,7 @@ int vpt_gpu_film_order_info(const vpt_gpu_ctx* ctx, int* mode, uint64_t* buffer_
 }
 
 int vpt_gpu_set_job_order(vpt_gpu_ctx* ctx, int mode) {
-  if (!ctx || mode < VPT_ORDER_JID || mode > VPT_ORDER_COST_TAIL)
+  if (!ctx || mode < VPT_ORDER_JID || mode > VPT_ORDER_COST_SAME_TILE)
     return vpt::set_error(VPT_E_INVALID, "vpt_gpu_set_job_order: bad argument");
   ctx->order_mode = mode;
   return VPT_OK;

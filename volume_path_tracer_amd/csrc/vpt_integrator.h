@@ -1103,27 +1103,29 @@ __host__ __device__ __forceinline__ void eval_collision(ScenePtr sp, const DevSc
 // item k -> job (wave w, tile order[i]) with `order` = tiles by descending estimated cost.
 // Items before tail_k0 (= whole waves x T) run wave by wave, each wave costliest tile first.  The
 // last tail_n waves run as one costliest-first list, so the launch drains on cheap (sky) jobs: the
-// rank list is cut into groups of kOrderGroup tiles and a group's tail_n waves are consecutive
-// items, wave by wave -- the 64 lanes of a wavefront trace 64 different tiles (one tile per lane
-// would put the wavefront's film atomics on the same 64 addresses).
+// rank list is cut into groups of `group` tiles and a group's tail_n waves are consecutive items, wave
+// by wave.  group 64 (VPT_ORDER_COST_TAIL / _TILE_MAJOR): the 64 lanes of a wavefront trace 64 different
+// tiles (one tile per lane would put the wavefront's film atomics on the same 64 addresses).  group 1
+// (VPT_ORDER_COST_SAME_TILE, tail_n = every wave, ordered-film launches only): one tile's waves
+// consecutively -- a wavefront's lanes trace the same 64 pixels, and their rays walk the same cells.
 constexpr uint32_t kOrderGroup = 64;
 __host__ __device__ __forceinline__ uint64_t ordered_job(uint32_t k, uint32_t T, const uint32_t* order, uint32_t tail_k0,
-                                                         uint32_t tail_n) {
+                                                         uint32_t tail_n, uint32_t group) {
   if (k < tail_k0) {
     const uint32_t w = k / T;
     return (uint64_t)w * T + order[k - w * T];
   }
   k -= tail_k0;
-  const uint32_t full = T / kOrderGroup, span = kOrderGroup * tail_n;
+  const uint32_t full = T / group, span = group * tail_n;
   uint32_t w, i;
   if (k < full * span) {
     const uint32_t g = k / span, r = k - g * span;
-    w = r / kOrderGroup;
-    i = g * kOrderGroup + (r - w * kOrderGroup);
-  } else {
-    const uint32_t R = T - full * kOrderGroup, r = k - full * span;
+    w = r / group;
+    i = g * group + (r - w * group);
+  } else {  // (never with group 1: full * span covers the tail)
+    const uint32_t R = T - full * group, r = k - full * span;
     w = r / R;
-    i = full * kOrderGroup + (r - w * R);
+    i = full * group + (r - w * R);
   }
   return (uint64_t)(tail_k0 / T + w) * T + order[i];
 }
@@ -1245,7 +1247,8 @@ __host__ __device__ __forceinline__ void lane_iteration(ScenePtr sp, Lane& ln, E
       if (const uint32_t* const perm = env.args()->perm)
         j = perm[j];
       else if (const uint32_t* const order = env.args()->order)
-        j = ordered_job((uint32_t)j, (uint32_t)S.T, order, env.args()->order_tail_k0, env.args()->order_tail_n);
+        j = ordered_job((uint32_t)j, (uint32_t)S.T, order, env.args()->order_tail_k0, env.args()->order_tail_n,
+                        env.args()->order_group);
       if (Debug) {
         ln.jid_local = j;
         ln.n_events = 0;

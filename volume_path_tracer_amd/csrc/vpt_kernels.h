@@ -56,6 +56,7 @@ struct KernelArgs {
   const uint32_t* perm;              // explicit job order (item k -> job perm[k]), overrides order
   uint32_t order_tail_k0;
   uint32_t order_tail_n;
+  uint32_t order_group;               // tiles per group of the tile-major part (64; 1: same-tile order)
   vpt_event* events;                 // Logger events (trace launches only)
   unsigned long long* event_count;
   uint64_t event_cap;

@@ -263,7 +263,8 @@ class Integrator:
 
     def set_job_order(self, mode: int) -> None:
         """Scheduling order of whole-wave launches: capi.VPT_ORDER_JID (TileProvider order),
-        VPT_ORDER_COST_WAVE_MAJOR, VPT_ORDER_COST_TILE_MAJOR or VPT_ORDER_COST_TAIL (default).
+        VPT_ORDER_COST_WAVE_MAJOR, VPT_ORDER_COST_TILE_MAJOR, VPT_ORDER_COST_TAIL or VPT_ORDER_COST_SAME_TILE
+        (default; launches that add with film atomics take VPT_ORDER_COST_TAIL).
         Samples never depend on it."""
         capi.check(capi.lib().vpt_gpu_set_job_order(self.h, int(mode)), "vpt_gpu_set_job_order")
 
