@@ -364,8 +364,10 @@ int vpt_gpu_kernel_variant(const vpt_gpu_ctx* ctx, int* has_temperature, int* ru
  * VPT_ORDER_COST_SAME_TILE (default): tile by tile, costliest first, each tile's waves consecutively --
  * the 64 lanes of a wavefront take one tile's jobs of 64 waves, so they trace the same pixels and their
  * rays walk the same cells until they scatter; the range drains on the cheapest tiles.  Launches that
- * add with film atomics (the ordered film off, feeds, debug launches) take VPT_ORDER_COST_TAIL instead:
- * 64 lanes would add to one pixel at once.  Costs: vpt_gpu_tile_costs.  Other ranges run in jid order. */
+ * add with film atomics (the ordered film off, feeds, debug launches) take VPT_ORDER_COST_TAIL instead
+ * (64 lanes would add to one pixel at once), and so do partly filled launches (a few jobs per resident
+ * lane: C2, a GPU's share of a frame), where it measured slower.  Costs: vpt_gpu_tile_costs.  Other
+ * ranges run in jid order. */
 enum {
   VPT_ORDER_JID = 0,
   VPT_ORDER_COST_WAVE_MAJOR = 1,

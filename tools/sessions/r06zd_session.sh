@@ -1,10 +1,10 @@
 #!/bin/bash
-# r06zd: evidence on the final binary (full-rate table indexes): the whole GPU suite and smoke, then the roofline
-# inputs (PMC traffic + kernel trace, the C3 bench line; kernel counter passes) for C3 and C4, and C4's bench line.
+# r06zd: the roofline inputs on the final binary (full-rate table indexes, the same-tile job order): PMC traffic +
+# kernel trace and the C3 bench line, kernel counter passes, for C3 and C4, and C4's bench line (the GPU suite and
+# smoke on this binary: r06zf).
 set -u
 export TMPDIR=/tmp
-STEPS="pytest smoke" bash tools/gpu_check.sh r06zd || exit $?
-grep -E "passed|failed" gpurun_out/r06zd/pytest_gpu.log | tail -1
+mkdir -p gpurun_out/r06zd
 bash tools/profile_round.sh r06zd c3 || exit $?
 bash tools/profile_round.sh r06zd c4 || exit $?
 bash tools/kernel_counters.sh r06zd c3 || exit $?

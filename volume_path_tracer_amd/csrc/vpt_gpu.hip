@@ -399,9 +399,13 @@ int vpt::host::render(vpt_gpu_ctx* ctx, uint64_t jid_begin, uint64_t jid_count, 
     if ((rc = ensure_order(ctx))) return rc;
     const uint32_t n = (uint32_t)(jid_count / T);
     uint32_t tail = 0;  // VPT_ORDER_COST_WAVE_MAJOR
-    // same-tile order only where each sample has a slot of its own (the ordered film): with film atomics a
-    // wavefront's 64 lanes would add to one pixel at once
-    const bool same_tile = ctx->order_mode == VPT_ORDER_COST_SAME_TILE && ordered && !ctx->frame_waves;
+    // Same-tile order only where each sample has a slot of its own (the ordered film): with film atomics a
+    // wavefront's 64 lanes would add to one pixel at once.  And not in partly filled launches (a few jobs per
+    // lane, the latency kernel with the context's gates), which last as long as their costliest jobs: r06ze, C2
+    // 98.1-98.5 vs 96.4-96.9 ms, C3's 8-GPU share (32 waves) 65.0-65.7 vs 62.6-63.6 with the cost tail.  Full
+    // launches: C3 321.8-322.0 vs 334.3-334.5 ms, C4 71.0-71.2 vs 80.2-80.7 (profiles/r06ze_same_tile_ab.txt).
+    const bool same_tile = ctx->order_mode == VPT_ORDER_COST_SAME_TILE && ordered && !ctx->frame_waves &&
+                           !(use_lat && !latency);
     if (ctx->order_mode == VPT_ORDER_COST_TILE_MAJOR || same_tile) tail = n;
     if (same_tile) env.order_group = 1;
     if (ctx->order_mode == VPT_ORDER_COST_TAIL || (ctx->order_mode == VPT_ORDER_COST_SAME_TILE && !same_tile)) {
