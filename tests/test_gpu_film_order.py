@@ -73,6 +73,26 @@ def test_multi_wave_film_bit_identical(name, w, h, n, runs, waves, lat):
     assert info["buffer_bytes"] >= waves * T * 64 * 12
 
 
+@pytest.mark.parametrize("name", ["c3", "c4"])
+def test_job_orders_on_a_full_launch_bit_identical(name):
+    """The same-tile job order (VPT_ORDER_COST_SAME_TILE, the default of full ordered-film launches: a wavefront's
+    lanes take one tile's jobs of consecutive waves) and the cost tail, on a launch that fills its grid (one block
+    set by set_tuning: neither the partly filled rule nor the latency kernel applies), render the oracle's film
+    bit for bit -- and so the same film as each other."""
+    from volume_path_tracer_amd.render import Integrator
+
+    wl = workload(name, width=96, height=64, spp=70, grid_n=64)
+    dens, temp = _grids(wl)
+    it = Integrator(wl.cfg, dens, temp, device=0)
+    it.set_tuning(grid_blocks=1)
+    T = wl.cfg.jobs_per_wave()
+    f_o, _, _ = O.render_jobs(wl.cfg, *_oracle(dens, temp), 0, 70 * T)
+    for mode in (capi.VPT_ORDER_COST_SAME_TILE, capi.VPT_ORDER_COST_TAIL, capi.VPT_ORDER_JID):
+        it.set_job_order(mode)
+        _assert_bitwise(_film(it, 0, 70 * T), f_o, f"{name} order {mode}")
+    assert it.film_order_info()["atomic_launches"] == 0
+
+
 @pytest.mark.parametrize("cap_jobs", ["two_waves", "ragged"])
 def test_split_launches_keep_the_order(cap_jobs):
     """A sample-buffer cap below the launch's size splits it into consecutive launches -- whole waves (cost order
