@@ -676,7 +676,9 @@ int create_on(const vpt_configuration* cfg, const HostGrids& grids, const float*
   ctx->scene.gate_min = has_temperature ? 8 : 6;
   ctx->scene.gate_idle = 8;
   ctx->scene.gate_eval = 36;
-  ctx->scene.gate_walk = 4;
+  // The temperature kernel's walk loops while any lane walks (gate_walk 1) since the same-tile order: C4 67.3-67.8
+  // ms vs 71.1-71.3 at 4, best of 3 twice (r06zg, profiles/r06zg_gates_same_tile.txt); C3 stays at 4 (1-3: flat).
+  ctx->scene.gate_walk = has_temperature ? 1 : 4;
   ctx->scene.pixel_mode = 0;
   ctx->scene.wave_lanes = 64;
   ctx->scene.tile_area = (uint32_t)(ctx->scene.tw * ctx->scene.th);
