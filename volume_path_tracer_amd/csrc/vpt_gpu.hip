@@ -674,9 +674,11 @@ int create_on(const vpt_configuration* cfg, const HostGrids& grids, const float*
   // 6:12:32:4 366.6 ms, C4 103.7 vs 104.4).  The temperature kernel's rare blocks wait for 8 lanes since the film
   // regroup (C4 83.3-83.6 vs 83.9-84.3 ms over 4 alternating runs, profiles/archive/r05gates2_c4_gate_min.txt).
   ctx->scene.gate_min = has_temperature ? 8 : 6;
-  // The temperature kernel runs its rare blocks at any count only once < 4 lanes walk (r06zj, same-tile order:
-  // C4 64.2-64.3 ms vs 67.2-67.4 at 8, profiles/r06zj_c4_gates.txt).
-  ctx->scene.gate_idle = has_temperature ? 4 : 8;
+  // The temperature kernel runs its rare blocks at any count only once no lane walks (same-tile order; C4 at
+  // gate_idle 8 / 4 / 2 / 1: 67.2-67.4 / 64.2-64.3 / 62.8 / 61.5 ms, profiles/r06zj_c4_gates.txt,
+  // r06zk_gates_idle.txt).  (C3 measured 317.7 ms at 4 vs 321.9 at 8, but the density kernel's partly filled
+  // launches -- C2, a GPU's share -- read the same gates and were tuned at 8: not changed.)
+  ctx->scene.gate_idle = has_temperature ? 1 : 8;
   ctx->scene.gate_eval = 36;
   // The temperature kernel's walk loops while any lane walks (gate_walk 1) since the same-tile order: C4 67.3-67.8
   // ms vs 71.1-71.3 at 4, best of 3 twice (r06zg, profiles/r06zg_gates_same_tile.txt); C3 stays at 4 (1-3: flat).
